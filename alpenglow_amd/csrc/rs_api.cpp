@@ -1,0 +1,798 @@
+// Host side of libalpenglow_rs.so: the C ABI declared in include/alpenglow_rs.h.
+//
+// Mirrors three reference interfaces on top of the HIP kernels (rs_kernels.hip):
+//   * the reed-solomon-simd 3.1.0 encoder/decoder API the reference wrapper calls
+//     (reed_solomon.rs:9,64-66,96-125,150-180,214-226)
+//   * ReedSolomonCoder (reed_solomon.rs:47-232) and the ValidatedShreds checks
+//     (validated_shreds.rs:34-114) in front of it
+//   * batched, device-resident forms of the encode/decode for throughput
+// All Reed-Solomon arithmetic runs on the GPU; the host does argument validation,
+// padding/splitting (byte copies), pattern bookkeeping and table setup only.  There is
+// no CPU compute fallback: without a device every call fails with AG_RS_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <new>
+#include <vector>
+
+#include "../../include/alpenglow_rs.h"
+#include "gf16.hpp"
+#include "rs_launch.hpp"
+
+using ag::next_pow2;
+
+namespace {
+
+#define AG_HIP(expr)                                  \
+  do {                                                \
+    if ((expr) != hipSuccess) return AG_RS_ERR_DEVICE; \
+  } while (0)
+
+// Grow-only device buffer.
+struct DevBuf {
+  void* ptr = nullptr;
+  size_t size = 0;
+  int ensure(size_t n, hipStream_t stream) {
+    if (n <= size) return AG_RS_OK;
+    if (ptr) {
+      if (hipStreamSynchronize(stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+      (void)hipFree(ptr);
+      ptr = nullptr;
+      size = 0;
+    }
+    if (hipMalloc(&ptr, n) != hipSuccess) return AG_RS_ERR_OUT_OF_MEMORY;
+    size = n;
+    return AG_RS_OK;
+  }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(ptr);
+  }
+  void release() {
+    if (ptr) (void)hipFree(ptr);
+    ptr = nullptr;
+    size = 0;
+  }
+};
+
+int check_geometry(size_t k, size_t m, size_t S) {
+  if (ag::use_high_rate(k, m) < 0) return AG_RS_ERR_UNSUPPORTED_SHARD_COUNT;
+  if (S == 0 || S % 2) return AG_RS_ERR_INVALID_SHARD_SIZE;
+  if (S > 0xFFFFFFFEull) return AG_RS_ERR_INVALID_ARGUMENT;
+  return AG_RS_OK;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// Single-chunk HighRate with a 32-point transform: k <= m, next_pow2(m) == 32.
+bool fast32_geometry(size_t k, size_t m, size_t S) {
+  return ag::use_high_rate(k, m) == 1 && next_pow2(m) == 32 && k <= 32 && S % 64 == 0;
+}
+
+}  // namespace
+
+struct ag_rs_ctx {
+  int device = 0;
+  hipStream_t own_stream = nullptr;
+  hipStream_t stream = nullptr;
+  bool tables_ready = false;
+  DevBuf d_exp, d_log, d_skew, d_log_walsh;
+  DevBuf scratch;                         // generic-kernel work rows
+  DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
+  DevBuf stage_in, stage_out;             // host-memory calls
+  DevBuf one_in, one_out;                 // crate-API single codeword
+
+  int enter() { return hipSetDevice(device) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE; }
+
+  int ensure_tables() {
+    if (tables_ready) return AG_RS_OK;
+    const ag::Gf16Tables& t = ag::gf16_tables();
+    // log_walsh: Walsh-Hadamard transform (mod 65535) of the log table with log[0] := 0
+    // (crate engine/tables.rs initialize_log_walsh).
+    std::vector<uint16_t> lw(t.log, t.log + ag::kGfOrder);
+    lw[0] = 0;
+    for (size_t dist = 1; dist < ag::kGfOrder; dist <<= 1)
+      for (size_t r = 0; r < ag::kGfOrder; r += 2 * dist)
+        for (size_t i = r; i < r + dist; ++i) {
+          const uint32_t a = lw[i], b = lw[i + dist];
+          const uint32_t s = a + b, d = a - b;
+          lw[i] = static_cast<uint16_t>(s + (s >> 16));
+          lw[i + dist] = static_cast<uint16_t>(d + (d >> 16));
+        }
+    int st;
+    if ((st = d_exp.ensure(sizeof t.exp, stream)) || (st = d_log.ensure(sizeof t.log, stream)) ||
+        (st = d_skew.ensure(sizeof t.skew, stream)) || (st = d_log_walsh.ensure(lw.size() * 2, stream)))
+      return st;
+    AG_HIP(hipMemcpy(d_exp.ptr, t.exp, sizeof t.exp, hipMemcpyHostToDevice));
+    AG_HIP(hipMemcpy(d_log.ptr, t.log, sizeof t.log, hipMemcpyHostToDevice));
+    AG_HIP(hipMemcpy(d_skew.ptr, t.skew, sizeof t.skew, hipMemcpyHostToDevice));
+    AG_HIP(hipMemcpy(d_log_walsh.ptr, lw.data(), lw.size() * 2, hipMemcpyHostToDevice));
+    tables_ready = true;
+    return AG_RS_OK;
+  }
+
+  ag::GfDeviceTables dtables() const {
+    return {d_exp.as<uint16_t>(), d_log.as<uint16_t>(), d_skew.as<uint16_t>(), d_log_walsh.as<uint16_t>()};
+  }
+
+  ~ag_rs_ctx() {
+    if (own_stream) {
+      (void)hipSetDevice(device);
+      (void)hipStreamSynchronize(own_stream);
+    }
+    for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
+                      &stage_in, &stage_out, &one_in, &one_out})
+      b->release();
+    if (own_stream) (void)hipStreamDestroy(own_stream);
+  }
+};
+
+namespace {
+
+// Scratch budget of the generic kernels (per launch).
+constexpr size_t kGenericScratchBytes = size_t{512} << 20;
+
+int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
+                  size_t ostride, uint8_t* rec, size_t rstride) {
+  if (nblocks == 0) return AG_RS_OK;
+  if (fast32_geometry(k, m, S) && aligned16(orig) && aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0) {
+    ag::XformParams p{};
+    p.in = orig;
+    p.in_block_stride = ostride;
+    p.in_shard_stride = S;
+    p.out = rec;
+    p.out_block_stride = rstride;
+    p.out_shard_stride = S;
+    p.n_in = static_cast<uint32_t>(k);
+    p.n_out = static_cast<uint32_t>(m);
+    p.chunks_per_shard = static_cast<uint32_t>(S / 64);
+    p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
+    return ag::launch_xform(ag::XformKind::kEncode32, p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+  }
+  int st = c->ensure_tables();
+  if (st) return st;
+  const int hr = ag::use_high_rate(k, m);
+  const size_t chunk = hr ? next_pow2(m) : next_pow2(k);
+  const size_t cover = hr ? k : m;
+  const size_t rows = std::max(chunk, (cover + chunk - 1) / chunk * chunk);
+  const size_t nsym = S / 2;
+  const size_t per_block = rows * nsym * 2;
+  const size_t per_launch = std::max<size_t>(1, kGenericScratchBytes / per_block);
+  if ((st = c->scratch.ensure(std::min(per_launch, nblocks) * per_block, c->stream))) return st;
+  for (size_t b0 = 0; b0 < nblocks; b0 += per_launch) {
+    ag::GenericEncodeParams p{};
+    p.orig = orig + b0 * ostride;
+    p.orig_block_stride = ostride;
+    p.orig_shard_stride = S;
+    p.rec = rec + b0 * rstride;
+    p.rec_block_stride = rstride;
+    p.rec_shard_stride = S;
+    p.k = static_cast<uint32_t>(k);
+    p.m = static_cast<uint32_t>(m);
+    p.high_rate = static_cast<uint32_t>(hr);
+    p.chunk = static_cast<uint32_t>(chunk);
+    p.rows = static_cast<uint32_t>(rows);
+    p.shard_bytes = static_cast<uint32_t>(S);
+    p.nsym = static_cast<uint32_t>(nsym);
+    p.nblocks = std::min(per_launch, nblocks - b0);
+    p.scratch = c->scratch.as<uint16_t>();
+    p.t = c->dtables();
+    if (ag::launch_generic_encode(p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
+  return AG_RS_OK;
+}
+
+int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
+                  const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
+                  int mode) {
+  if (nblocks == 0) return AG_RS_OK;
+  const int hr = ag::use_high_rate(k, m);
+  // classify patterns: 0 = nothing to restore, 1 = bitsliced (full recovery set), 2 = generic
+  std::vector<uint8_t> cls(npat);
+  const bool fast_geo = mode == AG_RS_DECODE_ANY_K && fast32_geometry(k, m, S) && aligned16(orig) &&
+                        aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0;
+  bool any_fast = false, any_generic = false;
+  for (size_t p = 0; p < npat; ++p) {
+    size_t no = 0, nr = 0;
+    for (size_t i = 0; i < k; ++i) no += opres[p * k + i] != 0;
+    for (size_t i = 0; i < m; ++i) nr += rpres[p * m + i] != 0;
+    if (no + nr < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;  // nothing launched yet
+    if (no == k) {
+      cls[p] = 0;
+    } else if (fast_geo && nr == m) {
+      cls[p] = 1;
+      any_fast = true;
+    } else {
+      cls[p] = 2;
+      any_generic = true;
+    }
+  }
+  int st;
+  if (any_fast) {
+    // store mask: restore original i of a block iff its pattern is fast and i is absent
+    std::vector<uint8_t> mask(npat * k, 0);
+    for (size_t p = 0; p < npat; ++p)
+      if (cls[p] == 1)
+        for (size_t i = 0; i < k; ++i) mask[p * k + i] = opres[p * k + i] ? 0 : 1;
+    if ((st = c->d_mask.ensure(mask.size(), c->stream))) return st;
+    AG_HIP(hipMemcpyAsync(c->d_mask.ptr, mask.data(), mask.size(), hipMemcpyHostToDevice, c->stream));
+    ag::XformParams p{};
+    p.in = rec;
+    p.in_block_stride = rstride;
+    p.in_shard_stride = S;
+    p.out = orig;
+    p.out_block_stride = ostride;
+    p.out_shard_stride = S;
+    p.out_mask = c->d_mask.as<uint8_t>();
+    p.out_mask_stride = k;
+    p.pattern_per_block = npat > 1 ? 1u : 0u;
+    p.n_in = static_cast<uint32_t>(m);
+    p.n_out = static_cast<uint32_t>(k);
+    p.chunks_per_shard = static_cast<uint32_t>(S / 64);
+    p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
+    if (ag::launch_xform(ag::XformKind::kDecode32, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    // the mask buffer is read asynchronously: keep the host copy alive until done
+    AG_HIP(hipStreamSynchronize(c->stream));
+  }
+  if (!any_generic) return AG_RS_OK;
+
+  if ((st = c->ensure_tables())) return st;
+  const size_t chunk = hr ? next_pow2(m) : next_pow2(k);
+  const size_t end = chunk + (hr ? k : m);
+  const size_t W = next_pow2(end);
+  // erasure flags per pattern over the transform window (crate decoder_high/low.rs)
+  std::vector<uint8_t> erased(npat * W, 0);
+  for (size_t p = 0; p < npat; ++p) {
+    if (cls[p] != 2) continue;
+    uint8_t* e = &erased[p * W];
+    const size_t opos = hr ? chunk : 0, rpos = hr ? 0 : chunk;
+    for (size_t i = 0; i < k; ++i) e[opos + i] = opres[p * k + i] ? 0 : 1;
+    for (size_t i = 0; i < m; ++i) e[rpos + i] = rpres[p * m + i] ? 0 : 1;
+    if (hr) {
+      for (size_t i = m; i < chunk; ++i) e[i] = 1;  // virtual recovery points
+    } else {
+      for (size_t i = end; i < W; ++i) e[i] = 1;  // beyond the recovery block
+    }
+  }
+  // per-pattern device copies of the present flags and erasures
+  const size_t flag_bytes = npat * (k + m) + erased.size();
+  if ((st = c->d_flags.ensure(flag_bytes, c->stream))) return st;
+  if ((st = c->d_loc.ensure(npat * W * 2, c->stream))) return st;
+  std::vector<uint8_t> hostflags(flag_bytes);
+  std::memcpy(hostflags.data(), opres, npat * k);
+  std::memcpy(hostflags.data() + npat * k, rpres, npat * m);
+  std::memcpy(hostflags.data() + npat * (k + m), erased.data(), erased.size());
+  uint8_t* dflags = c->d_flags.as<uint8_t>();
+  AG_HIP(hipMemcpyAsync(dflags, hostflags.data(), flag_bytes, hipMemcpyHostToDevice, c->stream));
+  if (ag::launch_locator(dflags + npat * (k + m), static_cast<uint32_t>(npat), static_cast<uint32_t>(W),
+                         hr ? 65536u : static_cast<uint32_t>(end), c->d_log_walsh.as<uint16_t>(),
+                         c->d_loc.as<uint16_t>(), c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  // blocks handled by the generic kernel
+  std::vector<uint32_t> ids;
+  if (npat > 1) {
+    for (size_t b = 0; b < nblocks; ++b)
+      if (cls[b] == 2) ids.push_back(static_cast<uint32_t>(b));
+    if ((st = c->d_blocks.ensure(ids.size() * 4, c->stream))) return st;
+    AG_HIP(hipMemcpyAsync(c->d_blocks.ptr, ids.data(), ids.size() * 4, hipMemcpyHostToDevice, c->stream));
+  }
+  const size_t ngen = npat > 1 ? ids.size() : nblocks;
+  const size_t nsym = S / 2;
+  const size_t per_block = W * nsym * 2;
+  const size_t per_launch = std::max<size_t>(1, kGenericScratchBytes / per_block);
+  if ((st = c->scratch.ensure(std::min(per_launch, ngen) * per_block, c->stream))) return st;
+  for (size_t b0 = 0; b0 < ngen; b0 += per_launch) {
+    ag::GenericDecodeParams p{};
+    p.orig = orig;
+    p.orig_block_stride = ostride;
+    p.orig_shard_stride = S;
+    p.rec = rec;
+    p.rec_block_stride = rstride;
+    p.rec_shard_stride = S;
+    p.orig_present = dflags;
+    p.rec_present = dflags + npat * k;
+    p.pattern_per_block = npat > 1 ? 1u : 0u;
+    p.block_ids = npat > 1 ? c->d_blocks.as<uint32_t>() + b0 : nullptr;
+    p.block_base = npat > 1 ? 0 : b0;
+    p.loc = c->d_loc.as<uint16_t>();
+    p.k = static_cast<uint32_t>(k);
+    p.m = static_cast<uint32_t>(m);
+    p.high_rate = static_cast<uint32_t>(hr);
+    p.chunk = static_cast<uint32_t>(chunk);
+    p.end = static_cast<uint32_t>(end);
+    p.W = static_cast<uint32_t>(W);
+    p.shard_bytes = static_cast<uint32_t>(S);
+    p.nsym = static_cast<uint32_t>(nsym);
+    p.nblocks = std::min(per_launch, ngen - b0);
+    p.scratch = c->scratch.as<uint16_t>();
+    p.t = c->dtables();
+    if (ag::launch_generic_decode(p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
+  // host vectors above are read by async copies: finish before they go out of scope
+  AG_HIP(hipStreamSynchronize(c->stream));
+  return AG_RS_OK;
+}
+
+}  // namespace
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+extern "C" {
+
+const char* ag_rs_status_string(int s) {
+  switch (s) {
+    case AG_RS_OK: return "ok";
+    case AG_RS_ERR_INVALID_SHARD_SIZE: return "invalid shard size";
+    case AG_RS_ERR_DIFFERENT_SHARD_SIZE: return "different shard size";
+    case AG_RS_ERR_TOO_FEW_ORIGINAL_SHARDS: return "too few original shards";
+    case AG_RS_ERR_TOO_MANY_ORIGINAL_SHARDS: return "too many original shards";
+    case AG_RS_ERR_INVALID_ORIGINAL_SHARD_INDEX: return "invalid original shard index";
+    case AG_RS_ERR_INVALID_RECOVERY_SHARD_INDEX: return "invalid recovery shard index";
+    case AG_RS_ERR_DUPLICATE_ORIGINAL_SHARD_INDEX: return "duplicate original shard index";
+    case AG_RS_ERR_DUPLICATE_RECOVERY_SHARD_INDEX: return "duplicate recovery shard index";
+    case AG_RS_ERR_NOT_ENOUGH_SHARDS: return "not enough shards";
+    case AG_RS_ERR_UNSUPPORTED_SHARD_COUNT: return "unsupported shard count";
+    case AG_RS_ERR_TOO_MUCH_DATA: return "too much data";
+    case AG_RS_ERR_INVALID_PADDING: return "invalid padding";
+    case AG_RS_ERR_INVALID_LAYOUT: return "invalid layout";
+    case AG_RS_ERR_INVALID_ARGUMENT: return "invalid argument";
+    case AG_RS_ERR_NO_DEVICE: return "no HIP device";
+    case AG_RS_ERR_DEVICE: return "HIP runtime error";
+    case AG_RS_ERR_OUT_OF_MEMORY: return "out of device memory";
+    case AG_RS_ERR_NOT_RESTORED: return "shard not restored";
+    default: return "unknown status";
+  }
+}
+
+int ag_rs_abi_version(void) { return AG_RS_ABI_VERSION; }
+
+int ag_rs_device_count(int* count) {
+  if (!count) return AG_RS_ERR_INVALID_ARGUMENT;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) n = 0;
+  *count = n;
+  return AG_RS_OK;
+}
+
+int ag_rs_ctx_create(int device, ag_rs_ctx** out) {
+  if (!out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return AG_RS_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return AG_RS_ERR_NO_DEVICE;
+  if (hipSetDevice(device) != hipSuccess) return AG_RS_ERR_DEVICE;
+  auto* c = new (std::nothrow) ag_rs_ctx();
+  if (!c) return AG_RS_ERR_OUT_OF_MEMORY;
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return AG_RS_ERR_DEVICE;
+  }
+  c->stream = c->own_stream;
+  *out = c;
+  return AG_RS_OK;
+}
+
+void ag_rs_ctx_destroy(ag_rs_ctx* c) { delete c; }
+
+int ag_rs_ctx_set_stream(ag_rs_ctx* c, void* s) {
+  if (!c) return AG_RS_ERR_INVALID_ARGUMENT;
+  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  return AG_RS_OK;
+}
+
+void* ag_rs_ctx_stream(ag_rs_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
+
+int ag_rs_ctx_synchronize(ag_rs_ctx* c) {
+  if (!c) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+int ag_rs_use_high_rate(size_t k, size_t m) {
+  const int hr = ag::use_high_rate(k, m);
+  return hr < 0 ? -AG_RS_ERR_UNSUPPORTED_SHARD_COUNT : hr;
+}
+
+int ag_rs_has_fast_path(size_t k, size_t m, size_t S) { return fast32_geometry(k, m, S) ? 1 : 0; }
+
+int ag_rs_encode_batch(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
+                       size_t ostride, uint8_t* rec, size_t rstride, int memory) {
+  if (!c || (nblocks && (!orig || !rec))) return AG_RS_ERR_INVALID_ARGUMENT;
+  int st = check_geometry(k, m, S);
+  if (st) return st;
+  if (ostride < k * S || rstride < m * S) return AG_RS_ERR_INVALID_ARGUMENT;
+  if ((st = c->enter())) return st;
+  if (memory == AG_RS_MEM_DEVICE) return encode_device(c, k, m, S, nblocks, orig, ostride, rec, rstride);
+  if (memory != AG_RS_MEM_HOST) return AG_RS_ERR_INVALID_ARGUMENT;
+  // host memory: stage groups of blocks through device buffers (packed strides)
+  const size_t in_b = k * S, out_b = m * S;
+  const size_t group = std::max<size_t>(1, (size_t{256} << 20) / (in_b + out_b));
+  for (size_t b0 = 0; b0 < nblocks; b0 += group) {
+    const size_t n = std::min(group, nblocks - b0);
+    if ((st = c->stage_in.ensure(n * in_b, c->stream)) || (st = c->stage_out.ensure(n * out_b, c->stream)))
+      return st;
+    AG_HIP(hipMemcpy2DAsync(c->stage_in.ptr, in_b, orig + b0 * ostride, ostride, in_b, n, hipMemcpyHostToDevice,
+                            c->stream));
+    if ((st = encode_device(c, k, m, S, n, c->stage_in.as<uint8_t>(), in_b, c->stage_out.as<uint8_t>(), out_b)))
+      return st;
+    AG_HIP(hipMemcpy2DAsync(rec + b0 * rstride, rstride, c->stage_out.ptr, out_b, out_b, n, hipMemcpyDeviceToHost,
+                            c->stream));
+    AG_HIP(hipStreamSynchronize(c->stream));
+  }
+  return AG_RS_OK;
+}
+
+int ag_rs_decode_batch(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
+                       const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
+                       int mode, int memory) {
+  if (!c || !opres || !rpres || (nblocks && (!orig || !rec))) return AG_RS_ERR_INVALID_ARGUMENT;
+  int st = check_geometry(k, m, S);
+  if (st) return st;
+  if (npat != 1 && npat != nblocks) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (mode != AG_RS_DECODE_EXACT && mode != AG_RS_DECODE_ANY_K) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (ostride < k * S || rstride < m * S) return AG_RS_ERR_INVALID_ARGUMENT;
+  if ((st = c->enter())) return st;
+  if (memory == AG_RS_MEM_DEVICE)
+    return decode_device(c, k, m, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
+  if (memory != AG_RS_MEM_HOST) return AG_RS_ERR_INVALID_ARGUMENT;
+  // pattern validity is checked up front so that an error leaves `orig` untouched
+  for (size_t p = 0; p < npat; ++p) {
+    size_t cnt = 0;
+    for (size_t i = 0; i < k; ++i) cnt += opres[p * k + i] != 0;
+    for (size_t i = 0; i < m; ++i) cnt += rpres[p * m + i] != 0;
+    if (cnt < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
+  }
+  const size_t o_b = k * S, r_b = m * S;
+  const size_t group = std::max<size_t>(1, (size_t{256} << 20) / (o_b + r_b));
+  for (size_t b0 = 0; b0 < nblocks; b0 += group) {
+    const size_t n = std::min(group, nblocks - b0);
+    if ((st = c->stage_in.ensure(n * r_b, c->stream)) || (st = c->stage_out.ensure(n * o_b, c->stream))) return st;
+    AG_HIP(hipMemcpy2DAsync(c->stage_in.ptr, r_b, rec + b0 * rstride, rstride, r_b, n, hipMemcpyHostToDevice,
+                            c->stream));
+    AG_HIP(hipMemcpy2DAsync(c->stage_out.ptr, o_b, orig + b0 * ostride, ostride, o_b, n, hipMemcpyHostToDevice,
+                            c->stream));
+    const uint8_t* op = npat > 1 ? opres + b0 * k : opres;
+    const uint8_t* rp = npat > 1 ? rpres + b0 * m : rpres;
+    if ((st = decode_device(c, k, m, S, n, c->stage_out.as<uint8_t>(), o_b, c->stage_in.as<uint8_t>(), r_b, op, rp,
+                            npat > 1 ? n : 1, mode)))
+      return st;
+    AG_HIP(hipMemcpy2DAsync(orig + b0 * ostride, ostride, c->stage_out.ptr, o_b, o_b, n, hipMemcpyDeviceToHost,
+                            c->stream));
+    AG_HIP(hipStreamSynchronize(c->stream));
+  }
+  return AG_RS_OK;
+}
+
+int ag_rs_fill_splitmix(ag_rs_ctx* c, uint8_t* dst, size_t nblocks, size_t block_bytes, size_t dst_stride,
+                        uint64_t seed_base) {
+  if (!c || (nblocks && !dst) || block_bytes % 8 || dst_stride < block_bytes) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  return ag::launch_fill_splitmix(dst, nblocks, block_bytes, dst_stride, seed_base, c->stream) == hipSuccess
+             ? AG_RS_OK
+             : AG_RS_ERR_DEVICE;
+}
+
+}  // extern "C"
+
+// =====================================================================================
+// Crate API mirror: ReedSolomonEncoder / ReedSolomonDecoder (one codeword, host memory)
+// =====================================================================================
+struct ag_rs_encoder {
+  ag_rs_ctx* ctx = nullptr;
+  size_t k = 0, m = 0, S = 0;
+  size_t received = 0;
+  bool encoded = false;
+  std::vector<uint8_t> orig, rec;
+};
+
+struct ag_rs_decoder {
+  ag_rs_ctx* ctx = nullptr;
+  size_t k = 0, m = 0, S = 0;
+  std::vector<uint8_t> orig, rec, opres, rpres;
+  size_t no = 0, nr = 0;
+  bool decoded = false;
+  std::vector<uint8_t> restored;  // 1 where original i was restored by the last decode
+};
+
+namespace {
+int run_one_encode(ag_rs_ctx* c, size_t k, size_t m, size_t S, const uint8_t* orig, uint8_t* rec) {
+  int st;
+  if ((st = c->enter())) return st;
+  if ((st = c->one_in.ensure(k * S, c->stream)) || (st = c->one_out.ensure(m * S, c->stream))) return st;
+  AG_HIP(hipMemcpyAsync(c->one_in.ptr, orig, k * S, hipMemcpyHostToDevice, c->stream));
+  if ((st = encode_device(c, k, m, S, 1, c->one_in.as<uint8_t>(), k * S, c->one_out.as<uint8_t>(), m * S)))
+    return st;
+  AG_HIP(hipMemcpyAsync(rec, c->one_out.ptr, m * S, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipStreamSynchronize(c->stream));
+  return AG_RS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ag_rs_encoder_reset(ag_rs_encoder* e, size_t k, size_t m, size_t S) {
+  if (!e) return AG_RS_ERR_INVALID_ARGUMENT;
+  const int st = check_geometry(k, m, S);
+  if (st) return st;
+  e->k = k;
+  e->m = m;
+  e->S = S;
+  e->received = 0;
+  e->encoded = false;
+  e->orig.assign(k * S, 0);
+  e->rec.assign(m * S, 0);
+  return AG_RS_OK;
+}
+
+int ag_rs_encoder_new(ag_rs_ctx* c, size_t k, size_t m, size_t S, ag_rs_encoder** out) {
+  if (!c || !out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  auto* e = new (std::nothrow) ag_rs_encoder();
+  if (!e) return AG_RS_ERR_OUT_OF_MEMORY;
+  e->ctx = c;
+  const int st = ag_rs_encoder_reset(e, k, m, S);
+  if (st) {
+    delete e;
+    return st;
+  }
+  *out = e;
+  return AG_RS_OK;
+}
+
+int ag_rs_encoder_add_original_shard(ag_rs_encoder* e, const uint8_t* shard, size_t len) {
+  if (!e || (!shard && len)) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (e->encoded) {  // the crate resets the received set once a result is dropped
+    e->received = 0;
+    e->encoded = false;
+  }
+  if (e->received == e->k) return AG_RS_ERR_TOO_MANY_ORIGINAL_SHARDS;
+  if (len != e->S) return AG_RS_ERR_DIFFERENT_SHARD_SIZE;
+  std::memcpy(e->orig.data() + e->received * e->S, shard, len);
+  ++e->received;
+  return AG_RS_OK;
+}
+
+int ag_rs_encoder_encode(ag_rs_encoder* e) {
+  if (!e) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (e->received != e->k) return AG_RS_ERR_TOO_FEW_ORIGINAL_SHARDS;
+  const int st = run_one_encode(e->ctx, e->k, e->m, e->S, e->orig.data(), e->rec.data());
+  if (st) return st;
+  e->encoded = true;
+  return AG_RS_OK;
+}
+
+int ag_rs_encoder_recovery(const ag_rs_encoder* e, size_t index, const uint8_t** shard, size_t* len) {
+  if (!e || !shard || !len) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (!e->encoded || index >= e->m) return AG_RS_ERR_INVALID_ARGUMENT;
+  *shard = e->rec.data() + index * e->S;
+  *len = e->S;
+  return AG_RS_OK;
+}
+
+void ag_rs_encoder_free(ag_rs_encoder* e) { delete e; }
+
+int ag_rs_decoder_reset(ag_rs_decoder* d, size_t k, size_t m, size_t S) {
+  if (!d) return AG_RS_ERR_INVALID_ARGUMENT;
+  const int st = check_geometry(k, m, S);
+  if (st) return st;
+  d->k = k;
+  d->m = m;
+  d->S = S;
+  d->orig.assign(k * S, 0);
+  d->rec.assign(m * S, 0);
+  d->opres.assign(k, 0);
+  d->rpres.assign(m, 0);
+  d->restored.assign(k, 0);
+  d->no = d->nr = 0;
+  d->decoded = false;
+  return AG_RS_OK;
+}
+
+int ag_rs_decoder_new(ag_rs_ctx* c, size_t k, size_t m, size_t S, ag_rs_decoder** out) {
+  if (!c || !out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  auto* d = new (std::nothrow) ag_rs_decoder();
+  if (!d) return AG_RS_ERR_OUT_OF_MEMORY;
+  d->ctx = c;
+  const int st = ag_rs_decoder_reset(d, k, m, S);
+  if (st) {
+    delete d;
+    return st;
+  }
+  *out = d;
+  return AG_RS_OK;
+}
+
+static void decoder_begin_round(ag_rs_decoder* d) {
+  if (!d->decoded) return;
+  std::fill(d->opres.begin(), d->opres.end(), 0);
+  std::fill(d->rpres.begin(), d->rpres.end(), 0);
+  std::fill(d->restored.begin(), d->restored.end(), 0);
+  d->no = d->nr = 0;
+  d->decoded = false;
+}
+
+int ag_rs_decoder_add_original_shard(ag_rs_decoder* d, size_t index, const uint8_t* shard, size_t len) {
+  if (!d || (!shard && len)) return AG_RS_ERR_INVALID_ARGUMENT;
+  decoder_begin_round(d);
+  if (index >= d->k) return AG_RS_ERR_INVALID_ORIGINAL_SHARD_INDEX;
+  if (d->opres[index]) return AG_RS_ERR_DUPLICATE_ORIGINAL_SHARD_INDEX;
+  if (len != d->S) return AG_RS_ERR_DIFFERENT_SHARD_SIZE;
+  std::memcpy(d->orig.data() + index * d->S, shard, len);
+  d->opres[index] = 1;
+  ++d->no;
+  return AG_RS_OK;
+}
+
+int ag_rs_decoder_add_recovery_shard(ag_rs_decoder* d, size_t index, const uint8_t* shard, size_t len) {
+  if (!d || (!shard && len)) return AG_RS_ERR_INVALID_ARGUMENT;
+  decoder_begin_round(d);
+  if (index >= d->m) return AG_RS_ERR_INVALID_RECOVERY_SHARD_INDEX;
+  if (d->rpres[index]) return AG_RS_ERR_DUPLICATE_RECOVERY_SHARD_INDEX;
+  if (len != d->S) return AG_RS_ERR_DIFFERENT_SHARD_SIZE;
+  std::memcpy(d->rec.data() + index * d->S, shard, len);
+  d->rpres[index] = 1;
+  ++d->nr;
+  return AG_RS_OK;
+}
+
+int ag_rs_decoder_decode(ag_rs_decoder* d) {
+  if (!d) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (d->no + d->nr < d->k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
+  std::fill(d->restored.begin(), d->restored.end(), 0);
+  if (d->no < d->k) {
+    // exact crate semantics: decode from every present shard
+    const int st = ag_rs_decode_batch(d->ctx, d->k, d->m, d->S, 1, d->orig.data(), d->k * d->S, d->rec.data(),
+                                      d->m * d->S, d->opres.data(), d->rpres.data(), 1, AG_RS_DECODE_EXACT,
+                                      AG_RS_MEM_HOST);
+    if (st) return st;
+    for (size_t i = 0; i < d->k; ++i) d->restored[i] = d->opres[i] ? 0 : 1;
+  }
+  d->decoded = true;
+  return AG_RS_OK;
+}
+
+int ag_rs_decoder_restored_original(const ag_rs_decoder* d, size_t index, const uint8_t** shard, size_t* len) {
+  if (!d || !shard || !len) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (!d->decoded || index >= d->k || !d->restored[index]) return AG_RS_ERR_NOT_RESTORED;
+  *shard = d->orig.data() + index * d->S;
+  *len = d->S;
+  return AG_RS_OK;
+}
+
+void ag_rs_decoder_free(ag_rs_decoder* d) { delete d; }
+
+}  // extern "C"
+
+// =====================================================================================
+// ReedSolomonCoder mirror (reed_solomon.rs:47-232)
+// =====================================================================================
+struct ag_rs_coder {
+  ag_rs_ctx* ctx = nullptr;
+  size_t num_coding = 0;
+  ag_rs_encoder* enc = nullptr;
+  ag_rs_decoder* dec = nullptr;
+  ~ag_rs_coder() {
+    ag_rs_encoder_free(enc);
+    ag_rs_decoder_free(dec);
+  }
+};
+
+namespace {
+constexpr size_t kDataShreds = AG_RS_DATA_SHREDS;
+constexpr size_t kTotalShreds = AG_RS_TOTAL_SHREDS;
+constexpr size_t kMaxAfterPadding = kDataShreds * AG_RS_MAX_DATA_PER_SHRED;
+constexpr size_t kMaxPayload = kMaxAfterPadding - 1;
+
+// encode_coding_from_data (reed_solomon.rs:211-231)
+int coder_encode(ag_rs_coder* c, const uint8_t* data, size_t S, uint8_t* coding) {
+  int st = ag_rs_encoder_reset(c->enc, kDataShreds, c->num_coding, S);
+  if (st) return st;
+  for (size_t i = 0; i < kDataShreds; ++i)
+    if ((st = ag_rs_encoder_add_original_shard(c->enc, data + i * S, S))) return st;
+  if ((st = ag_rs_encoder_encode(c->enc))) return st;
+  std::memcpy(coding, c->enc->rec.data(), c->num_coding * S);
+  return AG_RS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ag_rs_coder_new(ag_rs_ctx* ctx, size_t num_coding, ag_rs_coder** out) {
+  if (!ctx || !out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  if (num_coding == 0 || num_coding > kTotalShreds) return AG_RS_ERR_UNSUPPORTED_SHARD_COUNT;
+  auto* c = new (std::nothrow) ag_rs_coder();
+  if (!c) return AG_RS_ERR_OUT_OF_MEMORY;
+  c->ctx = ctx;
+  c->num_coding = num_coding;
+  int st = ag_rs_encoder_new(ctx, kDataShreds, num_coding, AG_RS_MAX_DATA_PER_SHRED, &c->enc);
+  if (!st) st = ag_rs_decoder_new(ctx, kDataShreds, num_coding, AG_RS_MAX_DATA_PER_SHRED, &c->dec);
+  if (st) {
+    delete c;
+    return st;
+  }
+  *out = c;
+  return AG_RS_OK;
+}
+
+void ag_rs_coder_free(ag_rs_coder* c) { delete c; }
+
+int ag_rs_coder_shred(ag_rs_coder* c, const uint8_t* payload, size_t len, uint8_t* data_out, uint8_t* coding_out,
+                      size_t* shred_bytes) {
+  if (!c || (!payload && len) || !data_out || !coding_out || !shred_bytes) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (len > kMaxPayload) return AG_RS_ERR_TOO_MUCH_DATA;
+  // padding 0x80 00.. to a multiple of 2 * DATA_SHREDS (reed_solomon.rs:94-106)
+  const size_t padding = 2 * kDataShreds - len % (2 * kDataShreds);
+  const size_t S = (len + padding) / kDataShreds;
+  std::vector<uint8_t> padded(len + padding, 0);
+  if (len) std::memcpy(padded.data(), payload, len);
+  padded[len] = 0x80;
+  std::vector<uint8_t> coding(c->num_coding * S);
+  const int st = coder_encode(c, padded.data(), S, coding.data());
+  if (st) return st;
+  std::memcpy(data_out, padded.data(), padded.size());
+  std::memcpy(coding_out, coding.data(), coding.size());
+  *shred_bytes = S;
+  return AG_RS_OK;
+}
+
+int ag_rs_coder_deshred(ag_rs_coder* c, size_t data_shreds, const uint8_t* const* shreds, const size_t* lens,
+                        const uint8_t* is_data, uint8_t* payload_out, size_t* payload_len, uint8_t* data_out,
+                        uint8_t* coding_out, size_t* shred_bytes) {
+  if (!c || !shreds || !lens || !payload_out || !payload_len || !data_out || !coding_out || !shred_bytes)
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (data_shreds + c->num_coding != kTotalShreds) return AG_RS_ERR_INVALID_ARGUMENT;
+  // Shredder::deshred: an empty set is too few shreds (shredder.rs:283-285)
+  size_t present = 0, S = 0;
+  for (size_t i = 0; i < kTotalShreds; ++i)
+    if (shreds[i]) {
+      if (!present) S = lens[i];
+      ++present;
+    }
+  if (!present) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
+  // ValidatedShreds::try_new (validated_shreds.rs:34-70)
+  if (S == 0 || S % 2) return AG_RS_ERR_INVALID_LAYOUT;
+  for (size_t i = 0; i < kTotalShreds; ++i) {
+    if (!shreds[i]) continue;
+    if (lens[i] != S) return AG_RS_ERR_INVALID_LAYOUT;
+    if (is_data && ((i < data_shreds) != (is_data[i] != 0))) return AG_RS_ERR_INVALID_LAYOUT;
+  }
+  // ReedSolomonCoder::deshred (reed_solomon.rs:140-208)
+  if (present < kDataShreds) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
+  int st = ag_rs_decoder_reset(c->dec, kDataShreds, c->num_coding, S);
+  if (st) return st;
+  for (size_t i = 0; i < data_shreds; ++i)
+    if (shreds[i] && (st = ag_rs_decoder_add_original_shard(c->dec, i, shreds[i], S))) return st;
+  for (size_t j = data_shreds; j < kTotalShreds; ++j)
+    if (shreds[j] && (st = ag_rs_decoder_add_recovery_shard(c->dec, j - data_shreds, shreds[j], S))) return st;
+  if ((st = ag_rs_decoder_decode(c->dec))) return st;
+  std::vector<uint8_t> data(kDataShreds * S);
+  size_t total = 0;
+  for (size_t i = 0; i < kDataShreds; ++i) {
+    const uint8_t* d = (i < data_shreds && shreds[i]) ? shreds[i] : c->dec->orig.data() + i * S;
+    if (total + S > kMaxAfterPadding) return AG_RS_ERR_TOO_MUCH_DATA;
+    std::memcpy(data.data() + i * S, d, S);
+    total += S;
+  }
+  // strip padding: trailing zeros then the 0x80 marker
+  size_t zeros = 0;
+  while (zeros < total && data[total - 1 - zeros] == 0) ++zeros;
+  const size_t padding = zeros + 1;
+  if (padding > total || data[total - padding] != 0x80) return AG_RS_ERR_INVALID_PADDING;
+  const size_t plen = total - padding;
+  std::vector<uint8_t> coding(c->num_coding * S);
+  if ((st = coder_encode(c, data.data(), S, coding.data()))) return st;
+  std::memcpy(payload_out, data.data(), plen);
+  *payload_len = plen;
+  std::memcpy(data_out, data.data(), data.size());
+  std::memcpy(coding_out, coding.data(), coding.size());
+  *shred_bytes = S;
+  return AG_RS_OK;
+}
+
+}  // extern "C"

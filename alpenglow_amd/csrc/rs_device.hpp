@@ -1,0 +1,153 @@
+// Device-side building blocks shared by the HIP kernels (gfx950 / CDNA4 only).
+//
+// Bitsliced GF(2^16): a 64-byte chunk of a shard holds 32 symbols (crate layout:
+// byte j = low byte, byte 32 + j = high byte of symbol j).  One lane
+// transposes its chunk into 16 bit-planes (uint32 word p holds bit p of all 32 symbols);
+// an FFT butterfly's constant multiply then becomes a 16x16 GF(2) XOR network over
+// planes, evaluated with v_bitop3_b32 (3-input XOR), ~2 VALU ops per symbol-multiply.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <utility>
+
+#include "rs_consts.inc"
+
+namespace ag {
+namespace dev {
+
+// ---- compile-time loops ----------------------------------------------------------
+template <typename F, int... Is>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+// acc ^ XOR_{i in MASK} y[i], pairing terms into 3-input XORs.
+template <unsigned MASK>
+__device__ __forceinline__ uint32_t xsum(uint32_t acc, const uint32_t* y) {
+  if constexpr (MASK == 0) {
+    return acc;
+  } else {
+    constexpr int i = __builtin_ctz(MASK);
+    constexpr unsigned rest = MASK & (MASK - 1);
+    if constexpr (rest == 0) {
+      return acc ^ y[i];
+    } else {
+      constexpr int j = __builtin_ctz(rest);
+      return xsum<rest & (rest - 1)>(xor3(acc, y[i], y[j]), y);
+    }
+  }
+}
+
+// x ^= y * skew[S]   (bitsliced; S is a compile-time skew index)
+template <int S>
+__device__ __forceinline__ void mul_acc(uint32_t* x, const uint32_t* y) {
+  static_assert(S >= 0 && S < kSkewConstCount, "skew index outside generated table");
+  static_for<16>([&](auto O) {
+    constexpr int o = decltype(O)::value;
+    x[o] = xsum<kMulRow[S][o]>(x[o], y);
+  });
+}
+
+__device__ __forceinline__ void xor_planes(uint32_t* y, const uint32_t* x) {
+  static_for<16>([&](auto P) {
+    constexpr int p = decltype(P)::value;
+    y[p] ^= x[p];
+  });
+}
+
+// FFT butterfly (crate fft_butterfly_two): x ^= y * skew; y ^= x.
+template <int S>
+__device__ __forceinline__ void fft_bfly(uint32_t* x, uint32_t* y) {
+  if constexpr (kSkewLog[S] != 65535) mul_acc<S>(x, y);
+  xor_planes(y, x);
+}
+// IFFT butterfly (crate ifft_butterfly_two): y ^= x; x ^= y * skew.
+template <int S>
+__device__ __forceinline__ void ifft_bfly(uint32_t* x, uint32_t* y) {
+  xor_planes(y, x);
+  if constexpr (kSkewLog[S] != 65535) mul_acc<S>(x, y);
+}
+
+// ---- 8x32 bit transpose (3 delta swaps; an involution) ------------------------------
+// In: x[r] byte y = byte (4r + y) of a 32-byte plane group.  Out: x[b] bit (8y + r) =
+// bit b of that byte.  Any fixed bijection of symbol positions is fine because all
+// arithmetic is per symbol position; the inverse is the same network.
+// bfi(m, x, y) = (m & x) | (~m & y) as one v_bitop3_b32 (truth table 0xCA).
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
+  return __builtin_amdgcn_bitop3_b32(m, x, y, 0xCA);
+}
+__device__ __forceinline__ void swap_bits(uint32_t& a, uint32_t& b, int sh, uint32_t m) {
+  const uint32_t na = bfi(m, a, b << sh);
+  const uint32_t nb = bfi(m, a >> sh, b);
+  a = na;
+  b = nb;
+}
+__device__ __forceinline__ void transpose8(uint32_t* x) {
+  swap_bits(x[0], x[4], 4, 0x0F0F0F0Fu);
+  swap_bits(x[1], x[5], 4, 0x0F0F0F0Fu);
+  swap_bits(x[2], x[6], 4, 0x0F0F0F0Fu);
+  swap_bits(x[3], x[7], 4, 0x0F0F0F0Fu);
+  swap_bits(x[0], x[2], 2, 0x33333333u);
+  swap_bits(x[1], x[3], 2, 0x33333333u);
+  swap_bits(x[4], x[6], 2, 0x33333333u);
+  swap_bits(x[5], x[7], 2, 0x33333333u);
+  swap_bits(x[0], x[1], 1, 0x55555555u);
+  swap_bits(x[2], x[3], 1, 0x55555555u);
+  swap_bits(x[4], x[5], 1, 0x55555555u);
+  swap_bits(x[6], x[7], 1, 0x55555555u);
+}
+
+// 64-byte chunk <-> 16 planes (planes 0..7 = low-byte bits, 8..15 = high-byte bits).
+__device__ __forceinline__ void load_chunk(const uint8_t* __restrict__ src, uint32_t* v) {
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  const uint4 a = s[0], b = s[1], c = s[2], d = s[3];
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  v[8] = c.x; v[9] = c.y; v[10] = c.z; v[11] = c.w;
+  v[12] = d.x; v[13] = d.y; v[14] = d.z; v[15] = d.w;
+}
+__device__ __forceinline__ void planes_from_raw(uint32_t* v) {
+  transpose8(v);
+  transpose8(v + 8);
+}
+__device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, const uint32_t* planes) {
+  uint32_t v[16];
+  static_for<16>([&](auto P) {
+    constexpr int p = decltype(P)::value;
+    v[p] = planes[p];
+  });
+  transpose8(v);
+  transpose8(v + 8);
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = make_uint4(v[0], v[1], v[2], v[3]);
+  d[1] = make_uint4(v[4], v[5], v[6], v[7]);
+  d[2] = make_uint4(v[8], v[9], v[10], v[11]);
+  d[3] = make_uint4(v[12], v[13], v[14], v[15]);
+}
+
+// ---- table arithmetic for the generic (any-geometry) kernels ------------------------
+__device__ __forceinline__ uint16_t add_mod(uint32_t x, uint32_t y) {
+  const uint32_t s = x + y;
+  return static_cast<uint16_t>(s + (s >> 16));
+}
+__device__ __forceinline__ uint16_t sub_mod(uint32_t x, uint32_t y) {
+  const uint32_t d = x - y;
+  return static_cast<uint16_t>(d + (d >> 16));
+}
+__device__ __forceinline__ uint16_t gmul(const uint16_t* __restrict__ exp_t,
+                                         const uint16_t* __restrict__ log_t, uint16_t x,
+                                         uint16_t log_m) {
+  return x == 0 ? uint16_t(0) : exp_t[add_mod(log_t[x], log_m)];
+}
+
+}  // namespace dev
+}  // namespace ag

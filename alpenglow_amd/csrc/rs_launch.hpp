@@ -1,0 +1,88 @@
+// Kernel parameter blocks and launchers (host side of rs_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace ag {
+
+// Bitsliced single-chunk transform over one 32-shard (or 64-shard) position block:
+//   out = FFT_{delta_out}( IFFT_{delta_in}( in ) )
+// encode (HighRate, k <= m = N): in = originals (points N..2N), out = recovery (points 0..N)
+// decode from a full recovery set: in = recovery, out = originals (masked per block).
+struct XformParams {
+  const uint8_t* in;
+  uint64_t in_block_stride;
+  uint64_t in_shard_stride;
+  uint8_t* out;
+  uint64_t out_block_stride;
+  uint64_t out_shard_stride;
+  const uint8_t* out_mask;  // device: out_mask[pattern(b) * out_mask_stride + s] != 0 => store
+  uint64_t out_mask_stride;
+  uint32_t pattern_per_block;  // pattern(b) = pattern_per_block ? b : 0
+  uint32_t n_in;               // shards 0..n_in-1 are loaded, the rest are zero
+  uint32_t n_out;              // shards 0..n_out-1 may be stored
+  uint32_t chunks_per_shard;   // shard_bytes / 64
+  uint64_t total_columns;         // nblocks * chunks_per_shard
+};
+
+enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };
+
+hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream);
+// True when the bitsliced transform exists for this transform size.
+bool xform_supported(unsigned n);
+
+// Generic (any geometry) table-driven kernels.  One thread per (block, symbol).
+struct GfDeviceTables {
+  const uint16_t* exp;
+  const uint16_t* log;
+  const uint16_t* skew;
+  const uint16_t* log_walsh;
+};
+
+struct GenericEncodeParams {
+  const uint8_t* orig;
+  uint64_t orig_block_stride;
+  uint64_t orig_shard_stride;
+  uint8_t* rec;
+  uint64_t rec_block_stride;
+  uint64_t rec_shard_stride;
+  uint32_t k, m, high_rate, chunk, rows;
+  uint32_t shard_bytes, nsym;
+  uint64_t nblocks;  // blocks in this launch
+  uint16_t* scratch;  // nblocks * rows * nsym
+  GfDeviceTables t;
+};
+hipError_t launch_generic_encode(const GenericEncodeParams& p, hipStream_t stream);
+
+struct GenericDecodeParams {
+  uint8_t* orig;  // restored originals are written here (absent positions only)
+  uint64_t orig_block_stride;
+  uint64_t orig_shard_stride;
+  const uint8_t* rec;
+  uint64_t rec_block_stride;
+  uint64_t rec_shard_stride;
+  const uint8_t* orig_present;  // [pattern][k]
+  const uint8_t* rec_present;   // [pattern][m]
+  uint32_t pattern_per_block;     // pattern(b) = pattern_per_block ? b : 0
+  const uint32_t* block_ids;      // blocks to process (null => block_base + 0..nblocks-1)
+  uint64_t block_base;
+  const uint16_t* loc;            // [pattern][W] locator logs
+  uint32_t k, m, high_rate, chunk, end, W;
+  uint32_t shard_bytes, nsym;
+  uint64_t nblocks;   // entries processed in this launch
+  uint16_t* scratch;  // nblocks * W * nsym
+  GfDeviceTables t;
+};
+hipError_t launch_generic_decode(const GenericDecodeParams& p, hipStream_t stream);
+
+// locator logs for npatterns erasure patterns: erased[p * W + x] (x < W); positions
+// >= fill_from up to 65535 are also erased (LowRate virtual recovery); loc[p * W + x].
+hipError_t launch_locator(const uint8_t* erased, uint32_t npatterns, uint32_t W, uint32_t fill_from,
+                          const uint16_t* log_walsh, uint16_t* loc, hipStream_t stream);
+
+// Synthetic blocks: splitmix64 u64 little-endian words, block b seeded seed_base + b.
+hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nblocks, uint64_t block_bytes,
+                                uint64_t dst_block_stride, uint64_t seed_base, hipStream_t stream);
+
+}  // namespace ag

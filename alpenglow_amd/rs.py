@@ -1,0 +1,380 @@
+"""Python host-side mirror of the reference's Reed-Solomon interfaces over the C ABI.
+
+Binds ``include/alpenglow_rs.h`` (libalpenglow_rs.so) with ctypes and exposes the same
+shapes the reference uses:
+
+* ``ReedSolomonEncoder`` / ``ReedSolomonDecoder`` -- the reed-solomon-simd 3.1.0 API the
+  reference wrapper calls (``/root/reference/src/shredder/reed_solomon.rs:9,64-66,
+  96-125,150-180,214-226``): ``new``/``reset``/``add_original_shard``/``encode`` ->
+  recovery shards; ``add_original_shard(i)``/``add_recovery_shard(j)``/``decode`` ->
+  ``{index: restored original}``.
+* ``ReedSolomonCoder`` -- ``ReedSolomonCoder`` itself (``reed_solomon.rs:47-232``):
+  ``shred(payload)`` -> ``RawShreds``; ``deshred(shreds)`` -> ``(payload, RawShreds)``.
+* ``encode_batch`` / ``decode_batch`` -- device-resident batches (torch tensors or raw
+  device pointers), the GPU-shaped entry points.
+
+Errors raise ``RSError`` whose ``kind`` is the crate/wrapper variant name
+(``NotEnoughShards``, ``TooMuchData``, ``InvalidPadding``, ...).  There is no CPU
+fallback: without the built library or a GPU every call raises.
+"""
+
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libalpenglow_rs.so")
+
+MEM_DEVICE = 0
+MEM_HOST = 1
+DECODE_EXACT = 0
+DECODE_ANY_K = 1
+
+DATA_SHREDS = 32
+TOTAL_SHREDS = 64
+MAX_DATA_PER_SHRED = 1024
+MAX_DATA_PER_SLICE = DATA_SHREDS * MAX_DATA_PER_SHRED - 1
+
+STATUS_KIND = {
+    1: "InvalidShardSize",
+    2: "DifferentShardSize",
+    3: "TooFewOriginalShards",
+    4: "TooManyOriginalShards",
+    5: "InvalidOriginalShardIndex",
+    6: "InvalidRecoveryShardIndex",
+    7: "DuplicateOriginalShardIndex",
+    8: "DuplicateRecoveryShardIndex",
+    9: "NotEnoughShards",
+    10: "UnsupportedShardCount",
+    20: "TooMuchData",
+    21: "InvalidPadding",
+    22: "InvalidLayout",
+    100: "InvalidArgument",
+    101: "NoDevice",
+    102: "DeviceError",
+    103: "OutOfMemory",
+    104: "NotRestored",
+}
+
+# every exported symbol of include/alpenglow_rs.h (checked by tests/test_capi.py)
+EXPORTS = (
+    "ag_rs_status_string", "ag_rs_abi_version", "ag_rs_device_count",
+    "ag_rs_ctx_create", "ag_rs_ctx_destroy", "ag_rs_ctx_set_stream", "ag_rs_ctx_stream",
+    "ag_rs_ctx_synchronize", "ag_rs_use_high_rate", "ag_rs_has_fast_path",
+    "ag_rs_encode_batch", "ag_rs_decode_batch", "ag_rs_fill_splitmix",
+    "ag_rs_encoder_new", "ag_rs_encoder_reset", "ag_rs_encoder_add_original_shard",
+    "ag_rs_encoder_encode", "ag_rs_encoder_recovery", "ag_rs_encoder_free",
+    "ag_rs_decoder_new", "ag_rs_decoder_reset", "ag_rs_decoder_add_original_shard",
+    "ag_rs_decoder_add_recovery_shard", "ag_rs_decoder_decode",
+    "ag_rs_decoder_restored_original", "ag_rs_decoder_free",
+    "ag_rs_coder_new", "ag_rs_coder_free", "ag_rs_coder_shred", "ag_rs_coder_deshred",
+)
+
+
+class RSError(Exception):
+    def __init__(self, status: int, where: str = ""):
+        self.status = status
+        self.kind = STATUS_KIND.get(status, f"Status{status}")
+        super().__init__(f"{where}: {self.kind} ({status})" if where else self.kind)
+
+
+_lib = None
+
+
+def load():
+    """Load libalpenglow_rs.so (build it with ``python -m alpenglow_amd.build``)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} is missing: run `python -m alpenglow_amd.build` "
+                           "(the HIP library is required; there is no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    sz, p, i = ctypes.c_size_t, ctypes.c_void_p, ctypes.c_int
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    psz = ctypes.POINTER(ctypes.c_size_t)
+    sigs = {
+        "ag_rs_status_string": ([i], ctypes.c_char_p),
+        "ag_rs_abi_version": ([], i),
+        "ag_rs_device_count": ([ctypes.POINTER(ctypes.c_int)], i),
+        "ag_rs_ctx_create": ([i, pp], i),
+        "ag_rs_ctx_destroy": ([p], None),
+        "ag_rs_ctx_set_stream": ([p, p], i),
+        "ag_rs_ctx_stream": ([p], p),
+        "ag_rs_ctx_synchronize": ([p], i),
+        "ag_rs_use_high_rate": ([sz, sz], i),
+        "ag_rs_has_fast_path": ([sz, sz, sz], i),
+        "ag_rs_encode_batch": ([p, sz, sz, sz, sz, p, sz, p, sz, i], i),
+        "ag_rs_decode_batch": ([p, sz, sz, sz, sz, p, sz, p, sz, p, p, sz, i, i], i),
+        "ag_rs_fill_splitmix": ([p, p, sz, sz, sz, ctypes.c_uint64], i),
+        "ag_rs_encoder_new": ([p, sz, sz, sz, pp], i),
+        "ag_rs_encoder_reset": ([p, sz, sz, sz], i),
+        "ag_rs_encoder_add_original_shard": ([p, p, sz], i),
+        "ag_rs_encoder_encode": ([p], i),
+        "ag_rs_encoder_recovery": ([p, sz, pp, psz], i),
+        "ag_rs_encoder_free": ([p], None),
+        "ag_rs_decoder_new": ([p, sz, sz, sz, pp], i),
+        "ag_rs_decoder_reset": ([p, sz, sz, sz], i),
+        "ag_rs_decoder_add_original_shard": ([p, sz, p, sz], i),
+        "ag_rs_decoder_add_recovery_shard": ([p, sz, p, sz], i),
+        "ag_rs_decoder_decode": ([p], i),
+        "ag_rs_decoder_restored_original": ([p, sz, pp, psz], i),
+        "ag_rs_decoder_free": ([p], None),
+        "ag_rs_coder_new": ([p, sz, pp], i),
+        "ag_rs_coder_free": ([p], None),
+        "ag_rs_coder_shred": ([p, p, sz, p, p, psz], i),
+        "ag_rs_coder_deshred": ([p, sz, p, p, p, p, psz, p, p, psz], i),
+    }
+    for name, (args, res) in sigs.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = res
+    _lib = L
+    return L
+
+
+def _check(status: int, where: str):
+    if status != 0:
+        raise RSError(status, where)
+
+
+def use_high_rate(k: int, m: int) -> bool:
+    r = load().ag_rs_use_high_rate(k, m)
+    if r < 0:
+        raise RSError(-r, "use_high_rate")
+    return bool(r)
+
+
+def has_fast_path(k: int, m: int, shard_bytes: int) -> bool:
+    return bool(load().ag_rs_has_fast_path(k, m, shard_bytes))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    load().ag_rs_device_count(ctypes.byref(n))
+    return n.value
+
+
+def _buf(data: bytes):
+    return ctypes.create_string_buffer(bytes(data), len(data)) if data else ctypes.create_string_buffer(1)
+
+
+class Context:
+    """One device + one HIP stream (``ag_rs_ctx``)."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load()
+        h = ctypes.c_void_p()
+        _check(self._lib.ag_rs_ctx_create(device, ctypes.byref(h)), "ag_rs_ctx_create")
+        self.handle = h
+        self.device = device
+
+    def set_stream(self, hip_stream: int | None):
+        _check(self._lib.ag_rs_ctx_set_stream(self.handle, ctypes.c_void_p(hip_stream or 0)),
+               "ag_rs_ctx_set_stream")
+
+    @property
+    def stream(self) -> int:
+        return self._lib.ag_rs_ctx_stream(self.handle) or 0
+
+    def synchronize(self):
+        _check(self._lib.ag_rs_ctx_synchronize(self.handle), "ag_rs_ctx_synchronize")
+
+    def close(self):
+        if self.handle:
+            self._lib.ag_rs_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+# ---- batched (device pointers or torch tensors) -------------------------------------
+
+def _ptr(x) -> int:
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    return int(x)
+
+
+def encode_batch(ctx: Context, k: int, m: int, shard_bytes: int, nblocks: int, original,
+                 original_block_stride: int, recovery, recovery_block_stride: int,
+                 memory: int = MEM_DEVICE):
+    _check(load().ag_rs_encode_batch(ctx.handle, k, m, shard_bytes, nblocks, _ptr(original),
+                                     original_block_stride, _ptr(recovery), recovery_block_stride,
+                                     memory), "ag_rs_encode_batch")
+
+
+def decode_batch(ctx: Context, k: int, m: int, shard_bytes: int, nblocks: int, original,
+                 original_block_stride: int, recovery, recovery_block_stride: int,
+                 original_present, recovery_present, mode: int = DECODE_ANY_K,
+                 memory: int = MEM_DEVICE):
+    """original_present / recovery_present: bytes-like 0/1 flags, one pattern
+    (len k / m) or one per block (len nblocks*k / nblocks*m)."""
+    op = bytes(bytearray(original_present))
+    rp = bytes(bytearray(recovery_present))
+    npat = len(op) // k
+    if len(op) != npat * k or len(rp) != npat * m:
+        raise ValueError("present-flag arrays do not match the geometry")
+    _check(load().ag_rs_decode_batch(ctx.handle, k, m, shard_bytes, nblocks, _ptr(original),
+                                     original_block_stride, _ptr(recovery), recovery_block_stride,
+                                     op, rp, npat, mode, memory), "ag_rs_decode_batch")
+
+
+def fill_splitmix(ctx: Context, device_dst, nblocks: int, block_bytes: int, dst_block_stride: int,
+                  seed_base: int):
+    _check(load().ag_rs_fill_splitmix(ctx.handle, _ptr(device_dst), nblocks, block_bytes,
+                                      dst_block_stride, seed_base), "ag_rs_fill_splitmix")
+
+
+# ---- crate API mirror ----------------------------------------------------------------
+
+class ReedSolomonEncoder:
+    """reed_solomon_simd::ReedSolomonEncoder (one codeword, host memory)."""
+
+    def __init__(self, ctx: Context, original_count: int, recovery_count: int, shard_bytes: int):
+        self._lib = load()
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(self._lib.ag_rs_encoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
+                                           ctypes.byref(h)), "ReedSolomonEncoder::new")
+        self.handle = h
+        self.recovery_count = recovery_count
+
+    def reset(self, original_count: int, recovery_count: int, shard_bytes: int):
+        _check(self._lib.ag_rs_encoder_reset(self.handle, original_count, recovery_count, shard_bytes),
+               "ReedSolomonEncoder::reset")
+        self.recovery_count = recovery_count
+
+    def add_original_shard(self, shard: bytes):
+        b = _buf(shard)
+        _check(self._lib.ag_rs_encoder_add_original_shard(self.handle, b, len(shard)),
+               "add_original_shard")
+
+    def encode(self) -> list[bytes]:
+        """encode() + EncoderResult::recovery_iter(), copied out (reed_solomon.rs:125)."""
+        _check(self._lib.ag_rs_encoder_encode(self.handle), "ReedSolomonEncoder::encode")
+        out = []
+        for j in range(self.recovery_count):
+            ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
+            _check(self._lib.ag_rs_encoder_recovery(self.handle, j, ctypes.byref(ptr), ctypes.byref(n)),
+                   "recovery")
+            out.append(ctypes.string_at(ptr, n.value))
+        return out
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            self._lib.ag_rs_encoder_free(self.handle)
+            self.handle = None
+
+
+class ReedSolomonDecoder:
+    """reed_solomon_simd::ReedSolomonDecoder (one codeword, host memory)."""
+
+    def __init__(self, ctx: Context, original_count: int, recovery_count: int, shard_bytes: int):
+        self._lib = load()
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        _check(self._lib.ag_rs_decoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
+                                           ctypes.byref(h)), "ReedSolomonDecoder::new")
+        self.handle = h
+        self.original_count = original_count
+
+    def reset(self, original_count: int, recovery_count: int, shard_bytes: int):
+        _check(self._lib.ag_rs_decoder_reset(self.handle, original_count, recovery_count, shard_bytes),
+               "ReedSolomonDecoder::reset")
+        self.original_count = original_count
+
+    def add_original_shard(self, index: int, shard: bytes):
+        b = _buf(shard)
+        _check(self._lib.ag_rs_decoder_add_original_shard(self.handle, index, b, len(shard)),
+               "add_original_shard")
+
+    def add_recovery_shard(self, index: int, shard: bytes):
+        b = _buf(shard)
+        _check(self._lib.ag_rs_decoder_add_recovery_shard(self.handle, index, b, len(shard)),
+               "add_recovery_shard")
+
+    def decode(self) -> dict[int, bytes]:
+        """decode() + DecoderResult::restored_original(i) for every i (None omitted)."""
+        _check(self._lib.ag_rs_decoder_decode(self.handle), "ReedSolomonDecoder::decode")
+        out = {}
+        for i in range(self.original_count):
+            ptr, n = ctypes.c_void_p(), ctypes.c_size_t()
+            st = self._lib.ag_rs_decoder_restored_original(self.handle, i, ctypes.byref(ptr),
+                                                           ctypes.byref(n))
+            if st == 0:
+                out[i] = ctypes.string_at(ptr, n.value)
+            elif st != 104:
+                raise RSError(st, "restored_original")
+        return out
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            self._lib.ag_rs_decoder_free(self.handle)
+            self.handle = None
+
+
+@dataclass
+class RawShreds:
+    """reed_solomon.rs:35-40."""
+    data: list
+    coding: list
+
+
+class ReedSolomonCoder:
+    """ReedSolomonCoder (reed_solomon.rs:47-232) for DATA_SHREDS = 32 data shreds."""
+
+    def __init__(self, ctx: Context, num_coding: int):
+        self._lib = load()
+        self.ctx = ctx
+        self.num_coding = num_coding
+        h = ctypes.c_void_p()
+        _check(self._lib.ag_rs_coder_new(ctx.handle, num_coding, ctypes.byref(h)),
+               "ReedSolomonCoder::new")
+        self.handle = h
+
+    def shred(self, payload: bytes) -> RawShreds:
+        payload = bytes(payload)
+        data = ctypes.create_string_buffer(DATA_SHREDS * MAX_DATA_PER_SHRED)
+        coding = ctypes.create_string_buffer(self.num_coding * MAX_DATA_PER_SHRED)
+        sb = ctypes.c_size_t()
+        _check(self._lib.ag_rs_coder_shred(self.handle, _buf(payload), len(payload), data, coding,
+                                           ctypes.byref(sb)), "ReedSolomonCoder::shred")
+        S = sb.value
+        return RawShreds(data=[data.raw[i * S:(i + 1) * S] for i in range(DATA_SHREDS)],
+                         coding=[coding.raw[i * S:(i + 1) * S] for i in range(self.num_coding)])
+
+    def deshred(self, shreds, data_shreds: int | None = None):
+        """``shreds``: TOTAL_SHREDS entries, each None or (is_data, bytes) -- the
+        ``[Option<ValidatedShred>; 64]`` of ``Shredder::deshred`` (shredder.rs:282).
+        Returns (payload, RawShreds)."""
+        if data_shreds is None:
+            data_shreds = TOTAL_SHREDS - self.num_coding
+        assert len(shreds) == TOTAL_SHREDS
+        keep = [_buf(s[1]) if s is not None else None for s in shreds]
+        ptrs = (ctypes.c_void_p * TOTAL_SHREDS)(
+            *[ctypes.cast(b, ctypes.c_void_p) if b is not None else None for b in keep])
+        lens = (ctypes.c_size_t * TOTAL_SHREDS)(*[len(s[1]) if s is not None else 0 for s in shreds])
+        isd = (ctypes.c_uint8 * TOTAL_SHREDS)(*[1 if (s is not None and s[0]) else 0 for s in shreds])
+        cap = max([len(s[1]) for s in shreds if s is not None] + [1])
+        payload = ctypes.create_string_buffer(DATA_SHREDS * cap)
+        data = ctypes.create_string_buffer(DATA_SHREDS * cap)
+        coding = ctypes.create_string_buffer(self.num_coding * cap)
+        plen, sb = ctypes.c_size_t(), ctypes.c_size_t()
+        _check(self._lib.ag_rs_coder_deshred(self.handle, data_shreds, ptrs, lens, isd, payload,
+                                             ctypes.byref(plen), data, coding, ctypes.byref(sb)),
+               "ReedSolomonCoder::deshred")
+        S = sb.value
+        raw = RawShreds(data=[data.raw[i * S:(i + 1) * S] for i in range(DATA_SHREDS)],
+                        coding=[coding.raw[i * S:(i + 1) * S] for i in range(self.num_coding)])
+        return payload.raw[:plen.value], raw
+
+    def __del__(self):
+        if getattr(self, "handle", None):
+            self._lib.ag_rs_coder_free(self.handle)
+            self.handle = None

@@ -1,0 +1,305 @@
+#!/usr/bin/env python3
+"""bench.py -- GiB/s device-resident RS shred encode+reconstruct, batched 1 MiB blocks.
+
+Workload (BASELINE.json configs[1] + configs[2]): per GPU, 4096 random 1 MiB blocks,
+32 data : 32 coding shards (shard = 32 KiB), inputs resident in HBM.  One step =
+  encode:      32 data shards -> 32 coding shards for every block
+  reconstruct: 16 of the 32 data shards erased per block, restored from the coding set
+through the C ABI (libalpenglow_rs.so).  value = block payload bytes that went through
+encode AND reconstruct, summed over ranks, per second of the max-over-ranks wall time.
+
+Multi-GPU: one process per GPU (torchrun), each rank shards its own independent blocks
+(weak scaling, no data-path collective; the only collectives are the timing barrier and
+the max-over-ranks reduction).
+
+Also printed in the JSON line: per-kernel HIP-event timings on the launch stream with the
+HBM roofline, a CPU baseline (the C oracle, a restatement of the reference algorithm, on a
+bounded sample of the same blocks, rank 0 at N=1) and, with --pcie, the host-buffer
+(PCIe-inclusive) rate.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X spec (MI355X_MICROARCH.md: 8.0 TB/s)
+GIB = float(1 << 30)
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nblocks", type=int, default=4096, help="blocks per GPU")
+    ap.add_argument("--block-bytes", type=int, default=1 << 20)
+    ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--m", type=int, default=32)
+    ap.add_argument("--erase", type=int, default=16, help="data shards erased per block")
+    ap.add_argument("--only", choices=["both", "encode", "decode"], default="both",
+                    help="profiling aid: time only one of the two kernels")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpus)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--pcie", action="store_true", help="also time host-buffer calls")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from alpenglow_amd import rs
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    k, m, B, n = args.k, args.m, args.block_bytes, args.nblocks
+    if B % k or (B // k) % 2:
+        raise SystemExit("block bytes must split into k even-sized shards")
+    S = B // k
+    e = args.erase
+    cw_stride = (k + m) * S
+
+    ctx = rs.Context(local)
+    stream = torch.cuda.current_stream(dev)
+    ctx.set_stream(stream.cuda_stream)
+
+    # codeword buffer: block b = k data shards then m coding shards (HBM-resident)
+    cw = torch.empty((n, cw_stride), dtype=torch.uint8, device=dev)
+    seed_base = 0x5EED_A19E_0000_0000 + rank * n  # rank-disjoint blocks of one stream
+    rs.fill_splitmix(ctx, cw, n, k * S, cw_stride, seed_base)
+    data_ptr, par_ptr = cw.data_ptr(), cw.data_ptr() + k * S
+    opres = [0] * e + [1] * (k - e)
+    rpres = [1] * m
+
+    def encode():
+        rs.encode_batch(ctx, k, m, S, n, data_ptr, cw_stride, par_ptr, cw_stride)
+
+    def reconstruct():
+        rs.decode_batch(ctx, k, m, S, n, data_ptr, cw_stride, par_ptr, cw_stride, opres, rpres,
+                        mode=rs.DECODE_ANY_K)
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    do_enc = args.only in ("both", "encode")
+    do_dec = args.only in ("both", "decode")
+    encode()  # parity must exist before the first reconstruct
+    for _ in range(args.warmup):
+        if do_enc:
+            encode()
+        if do_dec:
+            reconstruct()
+
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+    barrier()
+    t0 = time.perf_counter()
+    for s in range(args.steps):
+        ev[s][0].record(stream)
+        if do_enc:
+            encode()
+        ev[s][1].record(stream)
+        if do_dec:
+            reconstruct()
+        ev[s][2].record(stream)
+    barrier()
+    wall = time.perf_counter() - t0
+    enc_ms = sum(ev[s][0].elapsed_time(ev[s][1]) for s in range(args.steps)) / args.steps
+    dec_ms = sum(ev[s][1].elapsed_time(ev[s][2]) for s in range(args.steps)) / args.steps
+
+    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+    ms_per_step = wall_max * 1e3 / args.steps
+
+    # full-size property check: zero the erased shards, reconstruct, compare with a fresh
+    # regeneration of the data; and a 2-block bit-exact spot check of the parity vs oracle
+    verify = None
+    if not args.no_verify:
+        view = cw.view(n, k + m, S)
+        view[:, :e].zero_()
+        reconstruct()
+        ref = torch.empty((n, k * S), dtype=torch.uint8, device=dev)
+        rs.fill_splitmix(ctx, ref, n, k * S, k * S, seed_base)
+        ok_rec = bool(torch.equal(cw[:, : k * S], ref))
+        del ref
+        verify = {"reconstruct_restores_all_blocks": ok_rec}
+
+    line = None
+    if rank == 0:
+        processed = world * n * B  # each byte went through encode and reconstruct
+        enc_bytes = n * B * (1 + m / k)
+        dec_bytes = n * B * (1 + e / k)
+        kern = {
+            "encode": {"ms": enc_ms, "algorithmic_bytes": enc_bytes,
+                       "achieved_GBps": enc_bytes / (enc_ms * 1e-3) / 1e9 if enc_ms else None},
+            "reconstruct": {"ms": dec_ms, "algorithmic_bytes": dec_bytes,
+                            "achieved_GBps": dec_bytes / (dec_ms * 1e-3) / 1e9 if dec_ms else None},
+        }
+        dom = "encode" if enc_ms >= dec_ms else "reconstruct"
+        traffic = _pmc_traffic(dom, k, m, S, n)
+        ach = kern[dom]["achieved_GBps"]
+        line = {
+            "metric": "GiB/s device-resident RS shred encode+reconstruct, batched 1 MiB blocks",
+            "value": processed / (wall_max) / GIB,
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": ms_per_step,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8 (GF(2^16) symbols, bitsliced u32 planes)",
+            "data": "synthetic (splitmix64 random blocks, device-generated)",
+            "config": {"workload": f"{n} x {B >> 20} MiB blocks per GPU, {k}:{m} encode + "
+                                   f"reconstruct with {e}/{k} data shreds erased",
+                       "blocks_per_gpu": n, "block_bytes": B, "shard_bytes": S,
+                       "data_shreds": k, "coding_shreds": m, "erased_data_shreds": e,
+                       "parallelism": f"blocks sharded over {world} GPU(s), no collective",
+                       "only": args.only},
+            "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS,
+                         "unit": "GB/s", "frac": (ach / HBM_PEAK_GBPS) if ach else None,
+                         "traffic": traffic},
+            "kernels": kern,
+            "step_roofline_frac": ((enc_bytes + dec_bytes) / ((enc_ms + dec_ms) * 1e-3) / 1e9
+                                   / HBM_PEAK_GBPS) if (enc_ms + dec_ms) else None,
+            "verify": verify,
+        }
+    if world > 1:
+        dist.barrier()
+    # CPU baseline (rank 0, N = 1 only) on a bounded sample of the same blocks
+    if rank == 0:
+        if world == 1 and not args.no_cpu_baseline:
+            line["cpu_baseline"] = _cpu_baseline(args, cw, k, m, S, e)
+        else:
+            line["cpu_baseline"] = None
+        if args.pcie and world == 1:
+            line["pcie_inclusive"] = _pcie(args, ctx, cw, k, m, S, e, torch, dev)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _pmc_traffic(kernel, k, m, S, n):
+    """HBM bytes per launch measured with rocprofv3 PMC counters (profiles/pmc_traffic.json,
+    written by tools/pmc_summary.py from separate --pmc passes); None when absent or for a
+    different shape."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        d = json.load(open(path))
+        rec = d["kernels"][kernel]
+        if rec.get("shape") != [n, k, m, S]:
+            return None
+        return rec["hbm_bytes_per_launch"]
+    except Exception:
+        return None
+
+
+def _cpu_baseline(args, cw, k, m, S, e):
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import ro_c
+
+    threads = args.cpu_threads or max(1, min(16, len(os.sched_getaffinity(0))))
+    n_probe = max(1, threads)
+    host = cw[: n_probe].cpu().numpy().reshape(n_probe, k + m, S)
+    data = np.ascontiguousarray(host[:, :k])
+    t = time.perf_counter()
+    rec = ro_c.encode_blocks(data, m, threads=threads)
+    te = time.perf_counter() - t
+    op = np.array([0] * e + [1] * (k - e), np.uint8)
+    rp = np.ones(m, np.uint8)
+    cwh = np.concatenate([data, rec], axis=1)
+    t = time.perf_counter()
+    out = ro_c.decode_blocks(cwh, k, op, rp, threads=threads)
+    td = time.perf_counter() - t
+    per_block = (te + td) / n_probe
+    nsample = int(min(cw.shape[0], max(n_probe, args.cpu_seconds / max(per_block, 1e-6))))
+    nsample = max(n_probe, nsample // n_probe * n_probe)
+    parity_ok = bool(np.array_equal(rec, host[:, k:])) and bool(np.array_equal(out, data))
+    if nsample > n_probe:
+        host = cw[:nsample].cpu().numpy().reshape(nsample, k + m, S)
+        data = np.ascontiguousarray(host[:, :k])
+        t = time.perf_counter()
+        rec = ro_c.encode_blocks(data, m, threads=threads)
+        te = time.perf_counter() - t
+        cwh = np.concatenate([data, rec], axis=1)
+        t = time.perf_counter()
+        out = ro_c.decode_blocks(cwh, k, op, rp, threads=threads)
+        td = time.perf_counter() - t
+        parity_ok = parity_ok and bool(np.array_equal(rec, host[:, k:])) and bool(np.array_equal(out, data))
+    B = k * S
+    return {
+        "value": nsample * B / (te + td) / GIB,
+        "unit": "GiB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{nsample} of the same {B >> 20} MiB blocks, {k}:{m} encode + reconstruct with "
+                  f"{e} data shreds erased, C oracle (scalar log/exp tables, crate algorithm), "
+                  f"{threads} threads one block each",
+        "encode_GiBps": nsample * B / te / GIB,
+        "reconstruct_GiBps": nsample * B / td / GIB,
+        "gpu_parity_matches_cpu": parity_ok,
+        "cpu": _cpu_model(),
+    }
+
+
+def _cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
+def _pcie(args, ctx, cw, k, m, S, e, torch, dev):
+    """Host-buffer (PCIe-inclusive) rate: blocks start and end in pinned host memory."""
+    from alpenglow_amd import rs
+
+    nb = min(cw.shape[0], 512)
+    stride = (k + m) * S
+    host = torch.empty((nb, stride), dtype=torch.uint8, pin_memory=True)
+    host.copy_(cw[:nb])
+    torch.cuda.synchronize()
+    opres = [0] * e + [1] * (k - e)
+    t = time.perf_counter()
+    rs.encode_batch(ctx, k, m, S, nb, host.data_ptr(), stride, host.data_ptr() + k * S, stride,
+                    memory=rs.MEM_HOST)
+    te = time.perf_counter() - t
+    t = time.perf_counter()
+    rs.decode_batch(ctx, k, m, S, nb, host.data_ptr(), stride, host.data_ptr() + k * S, stride, opres,
+                    [1] * m, mode=rs.DECODE_ANY_K, memory=rs.MEM_HOST)
+    td = time.perf_counter() - t
+    ok = bool(torch.equal(host, cw[:nb].cpu()))
+    B = k * S
+    return {"blocks": nb, "encode_GiBps": nb * B / te / GIB, "reconstruct_GiBps": nb * B / td / GIB,
+            "encode_plus_reconstruct_GiBps": nb * B / (te + td) / GIB, "matches_device_result": ok}
+
+
+if __name__ == "__main__":
+    main()

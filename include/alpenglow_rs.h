@@ -1,0 +1,187 @@
+/*
+ * alpenglow_rs.h -- C ABI of the MI355X Reed-Solomon shredder library (libalpenglow_rs.so).
+ *
+ * Drop-in boundary for the reference's erasure-coding path.  The reference shredder
+ * (/root/reference/src/shredder/reed_solomon.rs) gets its arithmetic from the crate
+ * reed-solomon-simd 3.1.0 (GF(2^16) Leopard additive-FFT codec).  This library replaces
+ * those crate calls with HIP kernels for gfx950; the Rust side keeps its public API
+ * (Shredder trait, disseminator, repair unchanged).  INTEGRATION.md shows the Rust
+ * facade a maintainer would add over these symbols.
+ *
+ * Four layers, each mirroring one reference interface:
+ *   1. ag_rs_encoder_* / ag_rs_decoder_*  -- the crate API the wrapper calls
+ *      (ReedSolomonEncoder / ReedSolomonDecoder, reed_solomon.rs:9,64-66,96-125,150-180,214-226)
+ *   2. ag_rs_coder_*   -- ReedSolomonCoder (reed_solomon.rs:47-232): padding, split,
+ *      reassembly, padding strip, re-encode
+ *   3. ag_rs_encode_batch / ag_rs_decode_batch -- batched, device-resident forms of 1.
+ *      (the GPU-shaped entry points: many blocks per launch)
+ *   4. context / stream / utility
+ *
+ * Conventions: the caller owns every buffer; the library borrows them for the call
+ * (reed_solomon.rs copies out of the crate's borrowed results, :118,125,187,226).  A
+ * context binds one device and one HIP stream; it is not thread-safe, like a
+ * ReedSolomonCoder checked out of ShredderPool (pool.rs:33-93).  Calls fail loudly
+ * (AG_RS_ERR_NO_DEVICE / AG_RS_ERR_DEVICE) when no GPU is usable: there is no CPU
+ * fallback.  On error, caller-visible outputs are left untouched (shredder.rs:274).
+ */
+#ifndef ALPENGLOW_RS_H
+#define ALPENGLOW_RS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define AG_RS_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------------------
+ * 1..10 mirror reed_solomon_simd::Error (crate error.rs; the wrapper .expect()s them,
+ * reed_solomon.rs:65,67,98,116,124,152,159,164,166).  20..22 are the wrapper's own
+ * errors (ReedSolomonShredError / ReedSolomonDeshredError, reed_solomon.rs:18-32, and
+ * DeshredError::InvalidLayout, shredder.rs:75). */
+enum {
+  AG_RS_OK = 0,
+  AG_RS_ERR_INVALID_SHARD_SIZE = 1,           /* Error::InvalidShardSize (0 or odd) */
+  AG_RS_ERR_DIFFERENT_SHARD_SIZE = 2,         /* Error::DifferentShardSize */
+  AG_RS_ERR_TOO_FEW_ORIGINAL_SHARDS = 3,      /* Error::TooFewOriginalShards */
+  AG_RS_ERR_TOO_MANY_ORIGINAL_SHARDS = 4,     /* Error::TooManyOriginalShards */
+  AG_RS_ERR_INVALID_ORIGINAL_SHARD_INDEX = 5, /* Error::InvalidOriginalShardIndex */
+  AG_RS_ERR_INVALID_RECOVERY_SHARD_INDEX = 6, /* Error::InvalidRecoveryShardIndex */
+  AG_RS_ERR_DUPLICATE_ORIGINAL_SHARD_INDEX = 7,
+  AG_RS_ERR_DUPLICATE_RECOVERY_SHARD_INDEX = 8,
+  AG_RS_ERR_NOT_ENOUGH_SHARDS = 9,            /* Error::NotEnoughShards / NotEnoughShreds */
+  AG_RS_ERR_UNSUPPORTED_SHARD_COUNT = 10,     /* Error::UnsupportedShardCount */
+  AG_RS_ERR_TOO_MUCH_DATA = 20,               /* TooMuchData (reed_solomon.rs:20,29) */
+  AG_RS_ERR_INVALID_PADDING = 21,             /* InvalidPadding (reed_solomon.rs:31) */
+  AG_RS_ERR_INVALID_LAYOUT = 22,              /* DeshredError::InvalidLayout (shredder.rs:75) */
+  AG_RS_ERR_INVALID_ARGUMENT = 100,
+  AG_RS_ERR_NO_DEVICE = 101,                  /* no usable GPU: never a CPU fallback */
+  AG_RS_ERR_DEVICE = 102,                     /* HIP runtime / kernel launch failure */
+  AG_RS_ERR_OUT_OF_MEMORY = 103,
+  AG_RS_ERR_NOT_RESTORED = 104                /* restored_original(i) == None */
+};
+
+/* Where the buffers of a batch call live. */
+enum { AG_RS_MEM_DEVICE = 0, AG_RS_MEM_HOST = 1 };
+
+/* Decode modes for ag_rs_decode_batch.
+ * EXACT: the crate's decoder on every present shard (bit-identical to the crate for
+ *        any input, consistent or not).
+ * ANY_K: any k present shards suffice; uses the bitsliced kernel when a block's full
+ *        recovery set is present.  Bit-identical to EXACT on every valid codeword (MDS:
+ *        the originals are unique) -- the only inputs the reference's Merkle check
+ *        accepts (shredder.rs:301-303). */
+enum { AG_RS_DECODE_EXACT = 0, AG_RS_DECODE_ANY_K = 1 };
+
+const char* ag_rs_status_string(int status);
+int ag_rs_abi_version(void);
+
+/* ---- 4. context --------------------------------------------------------------------- */
+typedef struct ag_rs_ctx ag_rs_ctx;
+
+int ag_rs_ctx_create(int device, ag_rs_ctx** out);
+void ag_rs_ctx_destroy(ag_rs_ctx* ctx);
+/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the
+ * context's own stream. */
+int ag_rs_ctx_set_stream(ag_rs_ctx* ctx, void* hip_stream);
+void* ag_rs_ctx_stream(ag_rs_ctx* ctx);
+int ag_rs_ctx_synchronize(ag_rs_ctx* ctx);
+int ag_rs_device_count(int* count);
+
+/* Crate rate rule (rate.rs use_high_rate): 1 HighRate, 0 LowRate, <0 -status. */
+int ag_rs_use_high_rate(size_t original_count, size_t recovery_count);
+/* 1 when the bitsliced (HBM-bound) kernels serve this geometry, else 0 (generic kernel). */
+int ag_rs_has_fast_path(size_t original_count, size_t recovery_count, size_t shard_bytes);
+
+/* ---- 3. batched, device-resident ----------------------------------------------------
+ * Block b's original shard i is read at original + b*original_block_stride + i*shard_bytes;
+ * recovery shard j at recovery + b*recovery_block_stride + j*shard_bytes.
+ * AG_RS_MEM_DEVICE: asynchronous on the context stream.  AG_RS_MEM_HOST: staged through
+ * pinned buffers, synchronous. */
+int ag_rs_encode_batch(ag_rs_ctx* ctx, size_t original_count, size_t recovery_count,
+                       size_t shard_bytes, size_t nblocks, const uint8_t* original,
+                       size_t original_block_stride, uint8_t* recovery,
+                       size_t recovery_block_stride, int memory);
+
+/* Restores the absent originals of every block in place (present ones untouched).
+ * original_present / recovery_present are HOST arrays of 0/1 flags,
+ * [npatterns][original_count] and [npatterns][recovery_count]; npatterns is 1 (one
+ * pattern for the whole batch) or nblocks (pattern b for block b). */
+int ag_rs_decode_batch(ag_rs_ctx* ctx, size_t original_count, size_t recovery_count,
+                       size_t shard_bytes, size_t nblocks, uint8_t* original,
+                       size_t original_block_stride, const uint8_t* recovery,
+                       size_t recovery_block_stride, const uint8_t* original_present,
+                       const uint8_t* recovery_present, size_t npatterns, int mode,
+                       int memory);
+
+/* Synthetic input: splitmix64 u64 LE words, block b seeded seed_base + b. */
+int ag_rs_fill_splitmix(ag_rs_ctx* ctx, uint8_t* device_dst, size_t nblocks, size_t block_bytes,
+                        size_t dst_block_stride, uint64_t seed_base);
+
+/* ---- 1. crate API mirror (one codeword, host memory) --------------------------------
+ * ReedSolomonEncoder::{new,reset,add_original_shard,encode} + EncoderResult::recovery_iter */
+typedef struct ag_rs_encoder ag_rs_encoder;
+int ag_rs_encoder_new(ag_rs_ctx* ctx, size_t original_count, size_t recovery_count,
+                      size_t shard_bytes, ag_rs_encoder** out);
+int ag_rs_encoder_reset(ag_rs_encoder* enc, size_t original_count, size_t recovery_count,
+                        size_t shard_bytes);
+int ag_rs_encoder_add_original_shard(ag_rs_encoder* enc, const uint8_t* shard, size_t len);
+int ag_rs_encoder_encode(ag_rs_encoder* enc);
+/* Borrowed view of recovery shard `index` after encode (valid until the next reset). */
+int ag_rs_encoder_recovery(const ag_rs_encoder* enc, size_t index, const uint8_t** shard,
+                           size_t* len);
+void ag_rs_encoder_free(ag_rs_encoder* enc);
+
+/* ReedSolomonDecoder::{new,reset,add_original_shard,add_recovery_shard,decode} +
+ * DecoderResult::restored_original (AG_RS_ERR_NOT_RESTORED for None). */
+typedef struct ag_rs_decoder ag_rs_decoder;
+int ag_rs_decoder_new(ag_rs_ctx* ctx, size_t original_count, size_t recovery_count,
+                      size_t shard_bytes, ag_rs_decoder** out);
+int ag_rs_decoder_reset(ag_rs_decoder* dec, size_t original_count, size_t recovery_count,
+                        size_t shard_bytes);
+int ag_rs_decoder_add_original_shard(ag_rs_decoder* dec, size_t index, const uint8_t* shard,
+                                     size_t len);
+int ag_rs_decoder_add_recovery_shard(ag_rs_decoder* dec, size_t index, const uint8_t* shard,
+                                     size_t len);
+int ag_rs_decoder_decode(ag_rs_decoder* dec);
+int ag_rs_decoder_restored_original(const ag_rs_decoder* dec, size_t index,
+                                    const uint8_t** shard, size_t* len);
+void ag_rs_decoder_free(ag_rs_decoder* dec);
+
+/* ---- 2. ReedSolomonCoder mirror (reed_solomon.rs:47-232) ----------------------------- */
+#define AG_RS_DATA_SHREDS 32                 /* shredder.rs:43 */
+#define AG_RS_TOTAL_SHREDS 64                /* shredder.rs:48 */
+#define AG_RS_MAX_DATA_PER_SHRED 1024        /* shredder.rs:50 */
+#define AG_RS_MAX_DATA_PER_SLICE (AG_RS_DATA_SHREDS * AG_RS_MAX_DATA_PER_SHRED - 1)
+
+typedef struct ag_rs_coder ag_rs_coder;
+/* ReedSolomonCoder::new(num_coding) -- 32 data shreds, num_coding <= 64. */
+int ag_rs_coder_new(ag_rs_ctx* ctx, size_t num_coding, ag_rs_coder** out);
+void ag_rs_coder_free(ag_rs_coder* coder);
+
+/* ReedSolomonCoder::shred: pads payload with 0x80 00.. to a multiple of 64 bytes, splits
+ * it into 32 shards of *shred_bytes and encodes num_coding coding shards.  data_out must
+ * hold 32 * 1024 bytes, coding_out num_coding * 1024; shards are packed with stride
+ * *shred_bytes.  Errors: AG_RS_ERR_TOO_MUCH_DATA (payload_len > 32767). */
+int ag_rs_coder_shred(ag_rs_coder* coder, const uint8_t* payload, size_t payload_len,
+                      uint8_t* data_out, uint8_t* coding_out, size_t* shred_bytes);
+
+/* Shredder::deshred + ReedSolomonCoder::deshred for one slice.  shreds[i] (i < 64) is
+ * NULL when absent; shreds 0..data_shreds-1 are data shreds (original index i), the rest
+ * coding shreds (recovery index i - data_shreds) -- validated_shreds.rs:87-114.
+ * shred_is_data (optional, 64 flags) is checked against that layout and shred_lens must
+ * all be equal, non-zero and even (validated_shreds.rs:34-70).  Outputs: payload
+ * (<= 32767 bytes), all 32 data shards and num_coding re-encoded coding shards (packed,
+ * stride *shred_bytes).  Errors: NOT_ENOUGH_SHARDS, INVALID_LAYOUT, TOO_MUCH_DATA,
+ * INVALID_PADDING -- outputs untouched on error. */
+int ag_rs_coder_deshred(ag_rs_coder* coder, size_t data_shreds, const uint8_t* const* shreds,
+                        const size_t* shred_lens, const uint8_t* shred_is_data,
+                        uint8_t* payload_out, size_t* payload_len, uint8_t* data_out,
+                        uint8_t* coding_out, size_t* shred_bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* ALPENGLOW_RS_H */

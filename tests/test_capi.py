@@ -1,0 +1,100 @@
+"""CPU tests of the C-ABI library: it builds, loads, exports every symbol the header
+declares, agrees with the oracle on host logic (rate rule, generated constants), and fails
+loudly -- never falls back to the CPU -- when no GPU is present."""
+
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import rs_oracle as o
+from alpenglow_amd import build, rs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "alpenglow_rs.h")
+
+
+@pytest.fixture(scope="module")
+def lib():
+    build.build()
+    return rs.load()
+
+
+def header_symbols():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(ag_rs_\w+)\s*\(", text)))
+
+
+def test_header_declares_what_python_binds():
+    assert header_symbols() == sorted(rs.EXPORTS)
+
+
+def test_library_exports_every_header_symbol(lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", rs.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r"\bT (ag_rs_\w+)", out))
+    missing = [s for s in header_symbols() if s not in exported]
+    assert not missing, missing
+    for s in header_symbols():
+        assert hasattr(lib, s)
+
+
+def test_library_contains_gfx950_code_object(lib):
+    blob = open(rs.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+
+
+def test_abi_version_and_status_strings(lib):
+    assert lib.ag_rs_abi_version() == 1
+    assert lib.ag_rs_status_string(9) == b"not enough shards"
+    assert lib.ag_rs_status_string(21) == b"invalid padding"
+
+
+@pytest.mark.parametrize("k,m", [(32, 32), (16, 4), (64, 64), (32, 64), (32, 33), (20, 30), (30, 20),
+                                 (1, 1), (1, 65535), (65535, 1), (100, 3), (3, 100)])
+def test_rate_rule_matches_oracle(lib, k, m):
+    assert rs.use_high_rate(k, m) == o.use_high_rate(k, m)
+
+
+def test_unsupported_counts(lib):
+    for k, m in [(0, 1), (1, 0), (65536, 2), (40000, 40000)]:
+        with pytest.raises(rs.RSError) as e:
+            rs.use_high_rate(k, m)
+        assert e.value.kind == "UnsupportedShardCount"
+
+
+def test_fast_path_geometry(lib):
+    assert rs.has_fast_path(32, 32, 1024) and rs.has_fast_path(32, 32, 32768)
+    assert rs.has_fast_path(20, 30, 64)
+    assert not rs.has_fast_path(32, 32, 62)      # tail chunk -> generic kernel
+    assert not rs.has_fast_path(32, 64, 1024)    # LowRate -> generic kernel
+    assert not rs.has_fast_path(16, 4, 1024)
+
+
+def test_generated_constants_match_oracle_skew():
+    build.gen_consts()
+    text = open(os.path.join(build.CSRC, "rs_consts.inc")).read()
+    body = text.split("kSkewLog[kSkewConstCount] = {")[1].split("};")[0]
+    vals = [int(x) for x in re.findall(r"\d+", body)]
+    _, _, skew, _ = o.tables()
+    assert vals == [int(x) for x in skew[:len(vals)]]
+    # spot-check a multiply matrix row against the oracle's field multiply
+    rows = text.split("kMulRow[kSkewConstCount][16] = {")[1]
+    first = [int(x, 16) for x in re.findall(r"0x([0-9a-f]{4})", rows)[: 16 * 8]]
+    s = 2  # skew index 2
+    mat = first[16 * s: 16 * s + 16]
+    for i in range(16):
+        col = int(o.mul(np.array([1 << i]), int(skew[s]))[0])
+        for bit in range(16):
+            assert ((mat[bit] >> i) & 1) == ((col >> bit) & 1)
+
+
+def test_no_device_fails_loudly(lib):
+    if rs.device_count() > 0:
+        pytest.skip("a GPU is present")
+    with pytest.raises(rs.RSError) as e:
+        rs.Context(0)
+    assert e.value.kind == "NoDevice"

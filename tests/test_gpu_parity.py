@@ -1,0 +1,333 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the golden
+fixtures.  Integer/byte work: every comparison is bit-exact.
+
+Run on an MI355X with ``python -m pytest tests -m gpu``.
+"""
+
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import ro_c
+import rs_oracle as o
+from alpenglow_amd import rs
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+def _shards(seed, n, S):
+    raw = o.splitmix64_bytes(seed, n * S)
+    return [raw[i * S:(i + 1) * S] for i in range(n)]
+
+
+@pytest.fixture(scope="module")
+def dev(ctx):
+    d = torch.device("cuda:0")
+    ctx.set_stream(torch.cuda.current_stream(d).cuda_stream)
+    return d
+
+
+def to_dev(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def gpu_encode(ctx, dev, blocks: np.ndarray, m: int) -> np.ndarray:
+    """blocks: (n, k, S) uint8 -> (n, m, S) via the device-resident batch API."""
+    n, k, S = blocks.shape
+    d_in = to_dev(blocks.reshape(n, k * S), dev)
+    d_out = torch.zeros((n, m * S), dtype=torch.uint8, device=dev)
+    rs.encode_batch(ctx, k, m, S, n, d_in, k * S, d_out, m * S)
+    return d_out.cpu().numpy().reshape(n, m, S)
+
+
+def gpu_decode(ctx, dev, orig: np.ndarray, rec: np.ndarray, opres, rpres, mode):
+    """orig (n,k,S) with absent shards arbitrary, rec (n,m,S) -> restored originals."""
+    n, k, S = orig.shape
+    m = rec.shape[1]
+    d_o = to_dev(orig.reshape(n, k * S), dev)
+    d_r = to_dev(rec.reshape(n, m * S), dev)
+    rs.decode_batch(ctx, k, m, S, n, d_o, k * S, d_r, m * S, opres, rpres, mode=mode)
+    return d_o.cpu().numpy().reshape(n, k, S)
+
+
+# ------------------------------------------------------------------------------ encode
+
+def test_encode_golden(ctx, dev, golden):
+    for c in golden["encode"]:
+        k, m, S = c["k"], c["m"], c["S"]
+        orig = np.frombuffer(b"".join(_shards(c["seed"], k, S)), np.uint8).reshape(1, k, S)
+        got = gpu_encode(ctx, dev, orig, m)
+        assert sha(got.tobytes()) == c["recovery"]["sha256"], (k, m, S)
+
+
+def test_encode_crate_api(ctx, golden):
+    for c in golden["encode"][:8]:
+        k, m, S = c["k"], c["m"], c["S"]
+        enc = rs.ReedSolomonEncoder(ctx, k, m, S)
+        for s in _shards(c["seed"], k, S):
+            enc.add_original_shard(s)
+        rec = enc.encode()
+        assert sha(b"".join(rec)) == c["recovery"]["sha256"]
+
+
+@pytest.mark.parametrize("S,n", [(64, 1), (64, 65), (1024, 3), (1024, 77), (4096, 17), (32768, 9)])
+def test_fast_encode_many_blocks(ctx, dev, S, n):
+    assert rs.has_fast_path(32, 32, S)
+    blocks = np.stack([np.frombuffer(o.block_bytes(b, 32 * S), np.uint8).reshape(32, S) for b in range(n)])
+    got = gpu_encode(ctx, dev, blocks, 32)
+    want = ro_c.encode_blocks(blocks, 32, threads=8)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("k,m", [(32, 32), (20, 30), (17, 17), (25, 32)])
+def test_fast_encode_partial_geometries(ctx, dev, k, m):
+    S = 128
+    blocks = np.stack([np.frombuffer(o.block_bytes(100 + b, k * S), np.uint8).reshape(k, S) for b in range(5)])
+    got = gpu_encode(ctx, dev, blocks, m)
+    want = ro_c.encode_blocks(blocks, m)
+    assert np.array_equal(got, want)
+
+
+def test_encode_into_codeword_buffer(ctx, dev):
+    """Data and parity of a block adjacent (k+m shards per block), strided calls."""
+    k, m, S, n = 32, 32, 2048, 6
+    cw = torch.zeros((n, (k + m) * S), dtype=torch.uint8, device=dev)
+    rs.fill_splitmix(ctx, cw, n, k * S, (k + m) * S, o.BLOCK_SEED_BASE)
+    rs.encode_batch(ctx, k, m, S, n, cw, (k + m) * S, cw.data_ptr() + k * S, (k + m) * S)
+    host = cw.cpu().numpy().reshape(n, k + m, S)
+    for b in range(n):
+        assert host[b, :k].tobytes() == o.block_bytes(b, k * S)
+    assert np.array_equal(host[:, k:], ro_c.encode_blocks(host[:, :k], m))
+
+
+@pytest.mark.parametrize("k,m,S", [(16, 4, 1024), (64, 64, 256), (32, 64, 1024), (32, 33, 1024), (32, 32, 1000)])
+def test_generic_encode_multi_block(ctx, dev, k, m, S):
+    blocks = np.stack([np.frombuffer(o.block_bytes(7 + b, k * S), np.uint8).reshape(k, S) for b in range(3)])
+    assert np.array_equal(gpu_encode(ctx, dev, blocks, m), ro_c.encode_blocks(blocks, m))
+
+
+def test_fill_splitmix_matches_oracle(ctx, dev):
+    buf = torch.zeros((3, 4096), dtype=torch.uint8, device=dev)
+    rs.fill_splitmix(ctx, buf, 3, 4096, 4096, o.BLOCK_SEED_BASE + 10)
+    h = buf.cpu().numpy()
+    for b in range(3):
+        assert h[b].tobytes() == o.block_bytes(10 + b, 4096)
+
+
+# ------------------------------------------------------------------------------ decode
+
+@pytest.mark.parametrize("mode", [rs.DECODE_EXACT, rs.DECODE_ANY_K])
+def test_decode_golden(ctx, dev, golden, mode):
+    for c in golden["decode"]:
+        k, m, S = c["k"], c["m"], c["S"]
+        orig = _shards(c["seed"], k, S)
+        rec = o.encode(orig, m)
+        op = [0 if i in c["erased_original"] else 1 for i in range(k)]
+        rp = [0 if j in c["erased_recovery"] else 1 for j in range(m)]
+        ob = np.frombuffer(b"".join(orig), np.uint8).reshape(1, k, S).copy()
+        for i in c["erased_original"]:
+            ob[0, i] = 0xEE
+        rb = np.frombuffer(b"".join(rec), np.uint8).reshape(1, m, S)
+        got = gpu_decode(ctx, dev, ob, rb, op, rp, mode)
+        restored = b"".join(got[0, i].tobytes() for i in sorted(c["erased_original"]))
+        assert sha(restored) == c["restored"]["sha256"], (k, m, S, mode)
+        assert got.tobytes() == b"".join(orig)
+
+
+@pytest.mark.parametrize("erased", [list(range(16)), list(range(32)), [3, 17, 30]])
+def test_fast_decode_from_recovery_set(ctx, dev, erased):
+    """BASELINE C3 shape (scaled): 32:32, 16 (or 32) data shards erased per block."""
+    k, m, S, n = 32, 32, 4096, 33
+    blocks = np.stack([np.frombuffer(o.block_bytes(b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    damaged = blocks.copy()
+    damaged[:, erased] = 0
+    op = [0 if i in erased else 1 for i in range(k)]
+    got = gpu_decode(ctx, dev, damaged, rec, op, [1] * m, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
+
+
+def test_decode_per_block_patterns(ctx, dev):
+    """Random per-block patterns: some blocks have the full recovery set (bitsliced
+    kernel), others lost recovery shards too (generic kernel)."""
+    rng = random.Random(11)
+    k, m, S, n = 32, 32, 1024, 24
+    blocks = np.stack([np.frombuffer(o.block_bytes(50 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    op, rp = [], []
+    damaged = blocks.copy()
+    for b in range(n):
+        if b % 3 == 0:
+            lost = rng.sample(range(k), 16)
+            lost_r = []
+        elif b % 3 == 1:
+            lost = rng.sample(range(k), 10)
+            lost_r = rng.sample(range(m), 20)
+        else:
+            lost, lost_r = [], rng.sample(range(m), 5)
+        damaged[b, lost] = 0x5A
+        op += [0 if i in lost else 1 for i in range(k)]
+        rp += [0 if j in lost_r else 1 for j in range(m)]
+    for mode in (rs.DECODE_ANY_K, rs.DECODE_EXACT):
+        got = gpu_decode(ctx, dev, damaged, rec, op, rp, mode)
+        assert np.array_equal(got, blocks), mode
+
+
+def test_exact_decode_matches_crate_algorithm_on_inconsistent_input(ctx, dev):
+    """A tampered recovery shard: EXACT mode reproduces the crate decoder's bytes (every
+    present shard used), the same as the oracle's exact decoder."""
+    k, m, S = 32, 32, 256
+    orig = np.frombuffer(o.block_bytes(3, k * S), np.uint8).reshape(k, S)
+    rec = ro_c.encode(orig, m)
+    rec[0, 0] ^= 0xFF
+    op = np.ones(k, np.uint8)
+    op[:8] = 0
+    rp = np.ones(m, np.uint8)
+    damaged = orig * op[:, None]
+    want = ro_c.decode(damaged.astype(np.uint8), op, rec, rp)
+    got = gpu_decode(ctx, dev, damaged[None].astype(np.uint8), rec[None], op.tolist(), rp.tolist(), rs.DECODE_EXACT)
+    assert np.array_equal(got[0], want)
+
+
+def test_decode_not_enough_leaves_input_untouched(ctx, dev):
+    k, m, S = 32, 32, 64
+    orig = np.frombuffer(o.block_bytes(9, k * S), np.uint8).reshape(1, k, S).copy()
+    rec = ro_c.encode(orig[0], m)[None]
+    d_o = to_dev(orig.reshape(1, -1), dev)
+    before = d_o.clone()
+    op = [1] * 10 + [0] * 22
+    rp = [1] * 21 + [0] * 11
+    with pytest.raises(rs.RSError) as e:
+        rs.decode_batch(ctx, k, m, S, 1, d_o, k * S, to_dev(rec.reshape(1, -1), dev), m * S, op, rp)
+    assert e.value.kind == "NotEnoughShards"
+    assert torch.equal(d_o, before)
+
+
+def test_decoder_crate_api(ctx):
+    k, m, S = 32, 32, 512
+    orig = _shards(77, k, S)
+    rec = o.encode(orig, m)
+    dec = rs.ReedSolomonDecoder(ctx, k, m, S)
+    for i in range(5, k):
+        dec.add_original_shard(i, orig[i])
+    for j in range(0, m, 2):
+        dec.add_recovery_shard(j, rec[j])
+    res = dec.decode()
+    assert sorted(res) == list(range(5)) and all(res[i] == orig[i] for i in res)
+    with pytest.raises(rs.RSError) as e:
+        dec.add_original_shard(40, orig[0])
+    assert e.value.kind == "InvalidOriginalShardIndex"
+    dec.reset(k, m, S)
+    dec.add_original_shard(1, orig[1])
+    with pytest.raises(rs.RSError) as e:
+        dec.add_original_shard(1, orig[1])
+    assert e.value.kind == "DuplicateOriginalShardIndex"
+    with pytest.raises(rs.RSError) as e:
+        dec.add_recovery_shard(2, orig[1][:-2])
+    assert e.value.kind == "DifferentShardSize"
+    with pytest.raises(rs.RSError) as e:
+        dec.decode()
+    assert e.value.kind == "NotEnoughShards"
+
+
+def test_encoder_crate_api_errors(ctx):
+    with pytest.raises(rs.RSError) as e:
+        rs.ReedSolomonEncoder(ctx, 32, 32, 63)
+    assert e.value.kind == "InvalidShardSize"
+    enc = rs.ReedSolomonEncoder(ctx, 2, 2, 4)
+    enc.add_original_shard(b"abcd")
+    with pytest.raises(rs.RSError) as e:
+        enc.encode()
+    assert e.value.kind == "TooFewOriginalShards"
+    enc.add_original_shard(b"efgh")
+    with pytest.raises(rs.RSError) as e:
+        enc.add_original_shard(b"ijkl")
+    assert e.value.kind == "TooManyOriginalShards"
+    assert b"".join(enc.encode()) == b"".join(o.encode([b"abcd", b"efgh"], 2))
+
+
+# ----------------------------------------------------------- ReedSolomonCoder semantics
+
+def _into(raw, data_shreds=32):
+    return [(True, d) for d in raw.data[:data_shreds]] + [(False, c) for c in raw.coding]
+
+
+def _keep(shreds, idx):
+    return [s if i in idx else None for i, s in enumerate(shreds)]
+
+
+def test_coder_shred_golden(ctx, golden):
+    coder = rs.ReedSolomonCoder(ctx, 32)
+    for c in golden["coder"]:
+        raw = coder.shred(o.splitmix64_bytes(c["seed"], c["payload_len"]))
+        assert len(raw.data[0]) == c["shred_bytes"]
+        assert sha(b"".join(raw.data)) == c["data_sha256"]
+        assert sha(b"".join(raw.coding)) == c["coding_sha256"]
+
+
+def test_coder_shredding_roundtrip_regular(ctx):
+    """shredder.rs:655-706 for RegularShredder (32:32)."""
+    coder = rs.ReedSolomonCoder(ctx, 32)
+    payload = o.splitmix64_bytes(21, rs.MAX_DATA_PER_SLICE)
+    raw = coder.shred(payload)
+    sh = _into(raw)
+    for idx in [set(range(64)), set(range(32)), set(range(32, 64)), {0} | set(range(33, 64)),
+                set(range(16, 48)), set(range(1, 64))]:
+        got, raw2 = coder.deshred(_keep(sh, idx))
+        assert got == payload
+        assert raw2.data == raw.data and raw2.coding == raw.coding
+    for idx in [{0}, set(range(31)), set()]:
+        with pytest.raises(rs.RSError) as e:
+            coder.deshred(_keep(sh, idx))
+        assert e.value.kind == "NotEnoughShards"
+
+
+def test_coder_coding_only_and_pets(ctx):
+    """CodingOnlyShredder (32:64, no data shreds) and PetsShredder (32:33, 31 data shreds,
+    the key-carrying data shred never sent) -- shredder.rs:362-446."""
+    payload = o.splitmix64_bytes(8, 20000)
+    co = rs.ReedSolomonCoder(ctx, 64)
+    raw = co.shred(payload)
+    assert b"".join(raw.coding) == b"".join(o.coder_shred(payload, 64).coding)
+    sh = [(False, c) for c in raw.coding]
+    for idx in [set(range(64)), set(range(32)), set(range(32, 64))]:
+        got, _ = co.deshred(_keep(sh, idx), data_shreds=0)
+        assert got == payload
+    pets = rs.ReedSolomonCoder(ctx, 33)
+    raw = pets.shred(payload)
+    sh = [(True, d) for d in raw.data[:31]] + [(False, c) for c in raw.coding]
+    for idx in [set(range(64)), set(range(32, 64)), set(range(1, 33))]:
+        got, raw2 = pets.deshred(_keep(sh, idx), data_shreds=31)
+        assert got == payload and raw2.coding == raw.coding
+
+
+def test_coder_error_mapping(ctx):
+    coder = rs.ReedSolomonCoder(ctx, 32)
+    with pytest.raises(rs.RSError) as e:
+        coder.shred(bytes(rs.MAX_DATA_PER_SLICE + 1))
+    assert e.value.kind == "TooMuchData"
+    zero = [(True, bytes(1024))] * 32 + [(False, bytes(1024))] * 32
+    with pytest.raises(rs.RSError) as e:
+        coder.deshred(_keep(zero, set(range(32))))
+    assert e.value.kind == "InvalidPadding"
+    big = [(True, bytes(1026))] * 32 + [(False, bytes(1026))] * 32
+    with pytest.raises(rs.RSError) as e:
+        coder.deshred(_keep(big, set(range(32))))
+    assert e.value.kind == "TooMuchData"
+    raw = coder.shred(b"hello")
+    wrong = [(False, d) for d in raw.data] + [(False, c) for c in raw.coding]
+    with pytest.raises(rs.RSError) as e:
+        coder.deshred(wrong)
+    assert e.value.kind == "InvalidLayout"
+    odd = [(True, bytes(3))] * 32 + [None] * 32
+    with pytest.raises(rs.RSError) as e:
+        coder.deshred(odd)
+    assert e.value.kind == "InvalidLayout"

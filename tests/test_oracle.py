@@ -1,0 +1,290 @@
+"""CPU tests: the oracle against its mathematical pins, the golden fixtures and the
+behaviours the reference's own tests pin (reed_solomon.rs:244-347, shredder.rs:655-869).
+
+The oracle restates reed-solomon-simd 3.1.0; parity against the crate itself is unpinned
+(no known-answer vectors exist in the reference and the crate cannot be built here).
+"""
+
+import hashlib
+import random
+
+import numpy as np
+import pytest
+
+import ro_c
+import rs_oracle as o
+
+
+def sha(b):
+    return hashlib.sha256(b).hexdigest()
+
+
+# ---------------------------------------------------------------------------- field pins
+
+def test_tables_match_golden(golden):
+    exp, log, skew, lw = o.tables()
+    t = golden["tables"]
+    assert sha(exp.astype("<u2").tobytes()) == t["exp_sha256"]
+    assert sha(log.astype("<u2").tobytes()) == t["log_sha256"]
+    assert sha(skew.astype("<u2").tobytes()) == t["skew_sha256"]
+    assert sha(lw.astype("<u2").tobytes()) == t["log_walsh_sha256"]
+
+
+def test_c_oracle_tables_equal_python():
+    a = o.tables()
+    b = ro_c.tables()
+    for x, y in zip(a, b):
+        assert np.array_equal(x.astype(np.uint16), y)
+
+
+def test_polynomial_is_primitive_and_tables_are_inverse():
+    exp, log, _, _ = o.tables()
+    # log is a bijection from nonzero elements onto 0..65534 (0x1002D primitive)
+    assert sorted(log[1:].tolist()) == list(range(65535))
+    x = np.arange(1, 65536)
+    assert np.array_equal(exp[log[x]], x)
+
+
+def gf_mul(a, b):
+    exp, log, _, _ = o.tables()
+    if a == 0 or b == 0:
+        return 0
+    s = int(log[a]) + int(log[b])
+    return int(exp[(s + (s >> 16)) & 0xFFFF])
+
+
+def gf_inv(a):
+    exp, log, _, _ = o.tables()
+    return int(exp[(65535 - int(log[a])) % 65535])
+
+
+def test_cantor_basis_recurrence():
+    # In Cantor coordinates beta_i = 1 << i and beta_i^2 + beta_i = beta_{i-1}.
+    for i in range(1, 16):
+        b = 1 << i
+        assert gf_mul(b, b) ^ b == 1 << (i - 1)
+    assert gf_mul(1, 1) == 1
+
+
+def lagrange_eval(xs, ys, x):
+    acc = 0
+    for i, (xi, yi) in enumerate(zip(xs, ys)):
+        num, den = 1, 1
+        for j, xj in enumerate(xs):
+            if j != i:
+                num = gf_mul(num, x ^ xj)
+                den = gf_mul(den, xi ^ xj)
+        acc ^= gf_mul(yi, gf_mul(num, gf_inv(den)))
+    return acc
+
+
+def test_highrate_encode_is_lagrange_interpolation():
+    """32:32 HighRate: parity j = P(omega_j) where P interpolates data i at omega_{32+i}
+    and omega_x = x (Cantor basis)."""
+    rng = np.random.default_rng(7)
+    data = rng.integers(0, 65536, size=32, dtype=np.int64)
+    shards = [bytes([int(v) & 0xFF, int(v) >> 8]) for v in data]  # S = 2: one symbol
+    rec = o.encode(shards, 32)
+    xs = [32 + i for i in range(32)]
+    for j in range(32):
+        want = lagrange_eval(xs, [int(v) for v in data], j)
+        got = rec[j][0] | (rec[j][1] << 8)
+        assert got == want
+
+
+@pytest.mark.parametrize("size,delta", [(8, 0), (8, 8), (32, 0), (32, 32), (64, 64)])
+def test_ifft_inverts_fft(size, delta):
+    rng = np.random.default_rng(size + delta)
+    v = rng.integers(0, 65536, size=(size, 5), dtype=np.uint16)
+    w = v.copy()
+    o.fft(w, 0, size, size, delta)
+    o.ifft(w, 0, size, size, delta)
+    assert np.array_equal(w, v)
+
+
+def test_locator_fwht_equals_direct_product():
+    """eval_poly (FWHT route of the crate) == log prod_{e != x}(x + e) (direct)."""
+    rng = random.Random(3)
+    erased = np.zeros(65536, np.int64)
+    E = rng.sample(range(64), 20)
+    erased[E] = 1
+    loc = o.erasure_locator(erased, 64)
+    exp, log, _, _ = o.tables()
+    for x in range(64):
+        acc = 1
+        for e in E:
+            if e != x:
+                acc = gf_mul(acc, x ^ e)
+        assert int(exp[int(loc[x]) % 65535]) == acc
+
+
+# ------------------------------------------------------------------------ layout & rate
+
+def test_shard_layout_roundtrip_and_tail_split():
+    for S in (2, 30, 62, 64, 66, 126, 128, 1024, 1026):
+        b = o.splitmix64_bytes(S, S)
+        assert o.symbols_to_shard(o.shard_to_symbols(b), S) == b
+    # tail chunk of T bytes: symbol j = b[j] | b[T/2 + j] << 8 (crate Shards::insert)
+    b = bytes(range(6))
+    assert list(o.shard_to_symbols(b)) == [0 | 3 << 8, 1 | 4 << 8, 2 | 5 << 8]
+    full = bytes(range(64))
+    s = o.shard_to_symbols(full)
+    assert s[0] == 0 | 32 << 8 and s[31] == 31 | 63 << 8
+
+
+def test_rate_rule():
+    assert o.use_high_rate(32, 32) and o.use_high_rate(16, 4) and o.use_high_rate(64, 64)
+    assert not o.use_high_rate(32, 64) and not o.use_high_rate(32, 33)
+    assert o.use_high_rate(20, 30) and not o.use_high_rate(30, 20)  # tie: k <= m -> HighRate
+    with pytest.raises(o.RSError):
+        o.use_high_rate(0, 1)
+    with pytest.raises(o.RSError):
+        o.use_high_rate(65536, 2)
+
+
+# ------------------------------------------------------------------------- golden vectors
+
+def _shards(seed, n, S):
+    raw = o.splitmix64_bytes(seed, n * S)
+    return [raw[i * S:(i + 1) * S] for i in range(n)]
+
+
+def test_encode_golden(golden):
+    for c in golden["encode"]:
+        orig = _shards(c["seed"], c["k"], c["S"])
+        rec = b"".join(o.encode(orig, c["m"]))
+        assert sha(rec) == c["recovery"]["sha256"], c
+        if "hex" in c["recovery"]:
+            assert rec.hex() == c["recovery"]["hex"]
+        # the C restatement agrees
+        got = ro_c.encode(np.frombuffer(b"".join(orig), np.uint8).reshape(c["k"], c["S"]), c["m"])
+        assert got.tobytes() == rec, c
+
+
+def test_decode_golden(golden):
+    for c in golden["decode"]:
+        k, m, S = c["k"], c["m"], c["S"]
+        orig = _shards(c["seed"], k, S)
+        rec = o.encode(orig, m)
+        og = {i: orig[i] for i in range(k) if i not in c["erased_original"]}
+        rg = {j: rec[j] for j in range(m) if j not in c["erased_recovery"]}
+        res = o.decode(k, m, og, rg)
+        assert sha(b"".join(res[i] for i in sorted(res))) == c["restored"]["sha256"]
+        assert all(res[i] == orig[i] for i in res)
+
+
+def test_coder_golden(golden):
+    for c in golden["coder"]:
+        payload = o.splitmix64_bytes(c["seed"], c["payload_len"])
+        raw = o.coder_shred(payload, c["num_coding"])
+        assert len(raw.data[0]) == c["shred_bytes"]
+        assert sha(b"".join(raw.data)) == c["data_sha256"]
+        assert sha(b"".join(raw.coding)) == c["coding_sha256"]
+
+
+# --------------------------------------------- behaviours pinned by the reference tests
+
+def _into_shreds(raw, data_shreds=32):
+    allsh = [(True, d) for d in raw.data[:data_shreds]] + [(False, c) for c in raw.coding]
+    assert len(allsh) == 64
+    return allsh
+
+
+def _keep(shreds, idx):
+    return [s if i in idx else None for i, s in enumerate(shreds)]
+
+
+@pytest.mark.parametrize("size", [0, 31, o.MAX_DATA_PER_SLICE] + list(range(16383, 16415, 7)))
+def test_restore_sizes(size):
+    """reed_solomon.rs:244-276: restore_full / restore_tiny / restore_empty / restore_various
+    (recovered from the data shreds only, take_and_map_enough_shreds :359-369)."""
+    payload = o.splitmix64_bytes(size + 11, size)
+    raw = o.coder_shred(payload, 32)
+    sh = _keep(_into_shreds(raw), set(range(32)))
+    got, raw2 = o.coder_deshred(sh, 32, 32)
+    assert got == payload
+    assert raw2.coding == raw.coding
+
+
+def test_shred_too_much_data():
+    with pytest.raises(o.RSError) as e:
+        o.coder_shred(bytes(o.MAX_DATA_PER_SLICE + 1), 32)
+    assert e.value.kind == "TooMuchData"
+
+
+def test_deshred_patterns_of_shredding_roundtrip():
+    """shredder.rs:655-706: all, first 32, last 32, {0} + {33..63}, middle 16..47, all
+    but one; 1 and 31 shreds fail with NotEnoughShreds."""
+    payload = o.splitmix64_bytes(99, o.MAX_DATA_PER_SLICE)
+    raw = o.coder_shred(payload, 32)
+    sh = _into_shreds(raw)
+    for idx in [set(range(64)), set(range(32)), set(range(32, 64)), {0} | set(range(33, 64)),
+                set(range(16, 48)), set(range(1, 64))]:
+        got, raw2 = o.coder_deshred(_keep(sh, idx), 32, 32)
+        assert got == payload
+        assert raw2.data == raw.data and raw2.coding == raw.coding
+    for idx in [{0}, set(range(31))]:
+        with pytest.raises(o.RSError) as e:
+            o.coder_deshred(_keep(sh, idx), 32, 32)
+        assert e.value.kind == "NotEnoughShreds"
+
+
+def test_deshred_all_zero_payload_rejected():
+    """reed_solomon.rs:304-328."""
+    sh = [(True, bytes(1024))] * 32 + [(False, bytes(1024))] * 32
+    with pytest.raises(o.RSError) as e:
+        o.coder_deshred(_keep(sh, set(range(32))), 32, 32)
+    assert e.value.kind == "InvalidPadding"
+
+
+def test_validated_shreds_rules():
+    """reed_solomon.rs:330-347 and validated_shreds.rs:126-148."""
+    raw = o.coder_shred(b"x" * 100, 32)
+    sh = _into_shreds(raw)
+    assert o.validate_shreds(sh, 32, 32) is not None
+    odd = [(True, bytes(1023))] * 32 + [(False, bytes(1023))] * 32
+    assert o.validate_shreds(odd, 32, 32) is None
+    assert o.validate_shreds(sh, 1, 63) is None        # data shreds in coding positions
+    assert o.validate_shreds(sh, 63, 1) is None        # coding shreds in data positions
+    mixed = list(sh)
+    mixed[0] = (True, bytes(2))
+    assert o.validate_shreds(mixed, 32, 32) is None    # different sizes
+    assert o.validate_shreds([None] * 64, 32, 32) is None
+
+
+def test_deshred_rejects_oversized():
+    """shredder.rs:812-830: even-sized shreds above MAX_DATA_PER_SHRED -> TooMuchData."""
+    sh = [(True, bytes(1026))] * 32 + [(False, bytes(1026))] * 32
+    with pytest.raises(o.RSError) as e:
+        o.coder_deshred(_keep(sh, set(range(32))), 32, 32)
+    assert e.value.kind == "TooMuchData"
+
+
+def test_tampered_coding_shred_changes_reencode():
+    """shredder.rs:759-776: re-encoding from the data shreds exposes a flipped parity byte."""
+    payload = o.splitmix64_bytes(5, o.MAX_DATA_PER_SLICE)
+    raw = o.coder_shred(payload, 32)
+    tampered = bytearray(raw.coding[0])
+    tampered[0] ^= 0xFF
+    _, raw2 = o.coder_deshred(_keep(_into_shreds(raw), set(range(32))), 32, 32)
+    assert raw2.coding[0] != bytes(tampered)
+
+
+@pytest.mark.parametrize("k,m", [(32, 32), (16, 4), (64, 64), (32, 64), (32, 33), (3, 7), (100, 3)])
+def test_random_erasure_roundtrips(k, m):
+    rng = random.Random(k * 1000 + m)
+    S = 66
+    orig = _shards(k * m, k, S)
+    rec = o.encode(orig, m)
+    for _ in range(4):
+        keep = set(rng.sample(range(k + m), k))
+        og = {i: orig[i] for i in range(k) if i in keep}
+        rg = {j: rec[j] for j in range(m) if k + j in keep}
+        res = o.decode(k, m, og, rg)
+        assert all(res[i] == orig[i] for i in res)
+        # the C oracle decodes the same bytes
+        op = np.array([i in keep for i in range(k)], np.uint8)
+        rp = np.array([k + j in keep for j in range(m)], np.uint8)
+        ob = np.frombuffer(b"".join(orig), np.uint8).reshape(k, S) * op[:, None]
+        rb = np.frombuffer(b"".join(rec), np.uint8).reshape(m, S)
+        assert ro_c.decode(ob.astype(np.uint8), op, rb, rp).tobytes() == b"".join(orig)
