@@ -83,6 +83,7 @@ struct ag_rs_ctx {
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf stage_in, stage_out;             // host-memory calls
   DevBuf one_in, one_out;                 // crate-API single codeword
+  std::vector<uint8_t> mask_host;         // last store mask uploaded to d_mask
 
   int enter() { return hipSetDevice(device) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE; }
 
@@ -216,8 +217,13 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     for (size_t p = 0; p < npat; ++p)
       if (cls[p] == 1)
         for (size_t i = 0; i < k; ++i) mask[p * k + i] = opres[p * k + i] ? 0 : 1;
-    if ((st = c->d_mask.ensure(mask.size(), c->stream))) return st;
-    AG_HIP(hipMemcpyAsync(c->d_mask.ptr, mask.data(), mask.size(), hipMemcpyHostToDevice, c->stream));
+    // upload only when the pattern set changed (steady-state batches reuse it, no sync)
+    if (mask != c->mask_host) {
+      AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read mask_host
+      if ((st = c->d_mask.ensure(mask.size(), c->stream))) return st;
+      c->mask_host = mask;
+      AG_HIP(hipMemcpyAsync(c->d_mask.ptr, c->mask_host.data(), mask.size(), hipMemcpyHostToDevice, c->stream));
+    }
     ag::XformParams p{};
     p.in = rec;
     p.in_block_stride = rstride;
@@ -233,8 +239,6 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     p.chunks_per_shard = static_cast<uint32_t>(S / 64);
     p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
     if (ag::launch_xform(ag::XformKind::kDecode32, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
-    // the mask buffer is read asynchronously: keep the host copy alive until done
-    AG_HIP(hipStreamSynchronize(c->stream));
   }
   if (!any_generic) return AG_RS_OK;
 
@@ -367,7 +371,7 @@ int ag_rs_ctx_create(int device, ag_rs_ctx** out) {
   auto* c = new (std::nothrow) ag_rs_ctx();
   if (!c) return AG_RS_ERR_OUT_OF_MEMORY;
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreate(&c->own_stream) != hipSuccess) {
     delete c;
     return AG_RS_ERR_DEVICE;
   }
@@ -380,7 +384,13 @@ void ag_rs_ctx_destroy(ag_rs_ctx* c) { delete c; }
 
 int ag_rs_ctx_set_stream(ag_rs_ctx* c, void* s) {
   if (!c) return AG_RS_ERR_INVALID_ARGUMENT;
-  c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+  c->stream = static_cast<hipStream_t>(s);
+  return AG_RS_OK;
+}
+
+int ag_rs_ctx_reset_stream(ag_rs_ctx* c) {
+  if (!c) return AG_RS_ERR_INVALID_ARGUMENT;
+  c->stream = c->own_stream;
   return AG_RS_OK;
 }
 

@@ -16,6 +16,8 @@
 #include "rs_device.hpp"
 #include "rs_launch.hpp"
 
+#include <cstdlib>
+
 namespace ag {
 namespace {
 
@@ -118,6 +120,115 @@ __device__ __forceinline__ void lds_get(const uint4* lds, int slot, int lane, ui
     v[4 * q + 2] = x.z;
     v[4 * q + 3] = x.w;
   });
+}
+
+// Column geometry of lane `lane` in tile `tile` (idle lanes redo the last column).
+struct ColInfo {
+  bool active;
+  uint64_t blk;
+  uint64_t chunk_off;
+};
+__device__ __forceinline__ ColInfo col_info(const XformParams& p, uint64_t tile, int lane) {
+  const uint64_t col = tile * kXfLanes + lane;
+  ColInfo c;
+  c.active = col < p.total_columns;
+  const uint64_t colc = c.active ? col : p.total_columns - 1;
+  c.blk = colc / p.chunks_per_shard;
+  c.chunk_off = (colc - c.blk * p.chunks_per_shard) * 64;
+  return c;
+}
+
+// Raw (untransposed) 64-byte chunks of this wave's pass-A shards 8*wave + t.
+__device__ __forceinline__ void xf32_load_raw(const XformParams& p, const ColInfo& c, int wave, Regs8& raw) {
+  const uint8_t* base = p.in + c.blk * p.in_block_stride + c.chunk_off;
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = 8 * wave + t;  // wave-uniform condition
+    if (s < p.n_in) {
+      dev::load_chunk(base + s * p.in_shard_stride, raw[t]);
+    } else {
+      static_for<16>([&](auto P) { raw[t][decltype(P)::value] = 0; });
+    }
+  });
+}
+
+// Everything after the loads: transposes, the three passes with their two LDS exchanges,
+// inverse transposes and the masked stores of this wave's pass-C shards.
+template <int DIN, int DOUT>
+__device__ __forceinline__ void xf32_body(const XformParams& p, const ColInfo& c, int wave, int lane, uint4* lds,
+                                          Regs8& ra) {
+  static_for<8>([&](auto T) { dev::planes_from_raw(ra[decltype(T)::value]); });
+  xf32_pass_a<DIN>(wave, ra);
+  Regs8 rb;
+  static_for<2>([&](auto Rho) {  // exchange A -> B: round rho moves slots 4rho..4rho+3
+    constexpr int rho = decltype(Rho)::value;
+    static_for<4>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      lds_put(lds, 4 * wave + u, lane, ra[4 * rho + u]);
+    });
+    __syncthreads();
+    static_for<4>([&](auto W2) {
+      constexpr int w2 = decltype(W2)::value;
+      lds_get(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
+    });
+    __syncthreads();
+  });
+  xf32_pass_b<DIN, DOUT>(rb);
+  static_for<2>([&](auto Rho) {  // exchange B -> C (inverse mapping)
+    constexpr int rho = decltype(Rho)::value;
+    static_for<4>([&](auto W2) {
+      constexpr int w2 = decltype(W2)::value;
+      lds_put(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
+    });
+    __syncthreads();
+    static_for<4>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      lds_get(lds, 4 * wave + u, lane, ra[4 * rho + u]);
+    });
+    __syncthreads();
+  });
+  xf32_pass_c<DOUT>(wave, ra);
+  if (c.active) {
+    uint8_t* base = p.out + c.blk * p.out_block_stride + c.chunk_off;
+    const uint8_t* mask = nullptr;
+    if (p.out_mask) mask = p.out_mask + (p.pattern_per_block ? c.blk : 0) * p.out_mask_stride;
+    static_for<8>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      const uint32_t s = 8 * wave + t;
+      if (s < p.n_out && (mask == nullptr || mask[s])) dev::store_chunk(base + s * p.out_shard_stride, ra[t]);
+    });
+  }
+}
+
+// Persistent variant: one 4-wave workgroup per CU walks tiles blockIdx.x, +gridDim.x, ...
+// and keeps the next tile's 8 raw chunks per lane in flight (128 VGPRs) while it computes
+// the current one -- one wave per SIMD, 512-register budget.
+template <int DIN, int DOUT>
+__global__ __launch_bounds__(256, 1) void xform32_persist_kernel(const XformParams p) {
+  __shared__ uint4 lds[kXfLdsSlots * 4 * kXfLanes];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t ntiles = (p.total_columns + kXfLanes - 1) / kXfLanes;
+  uint64_t tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  Regs8 raw;
+  ColInfo c = col_info(p, tile, lane);
+  xf32_load_raw(p, c, wave, raw);
+  for (;;) {
+    Regs8 ra;
+    static_for<8>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      static_for<16>([&](auto P) { ra[t][decltype(P)::value] = raw[t][decltype(P)::value]; });
+    });
+    const uint64_t next = tile + gridDim.x;
+    const bool more = next < ntiles;
+    const ColInfo cn = col_info(p, more ? next : tile, lane);
+    if (more) xf32_load_raw(p, cn, wave, raw);
+    xf32_body<DIN, DOUT>(p, c, wave, lane, lds, ra);
+    if (!more) break;
+    tile = next;
+    c = cn;
+  }
 }
 
 template <int DIN, int DOUT>
@@ -401,11 +512,38 @@ __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* dst, uint64
 // ---- launchers ----------------------------------------------------------------------
 bool xform_supported(unsigned n) { return n == 32; }
 
+static int g_xform_variant = -1;  // -1: default; 0: one tile per workgroup; 1: persistent
+
+static int xform_variant() {
+  if (g_xform_variant < 0) {
+    const char* e = getenv("AG_RS_XFORM_VARIANT");
+    g_xform_variant = e ? atoi(e) : 0;
+  }
+  return g_xform_variant;
+}
+
 hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream) {
   if (p.total_columns == 0) return hipSuccess;
   const uint64_t groups = (p.total_columns + kXfLanes - 1) / kXfLanes;
   if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  const dim3 grid(static_cast<unsigned>(groups)), block(256);
+  const dim3 block(256);
+  if (xform_variant() == 1) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    const dim3 pgrid(static_cast<unsigned>(groups < static_cast<uint64_t>(cus) ? groups : cus));
+    switch (kind) {
+      case XformKind::kEncode32:
+        hipLaunchKernelGGL((xform32_persist_kernel<32, 0>), pgrid, block, 0, stream, p);
+        break;
+      case XformKind::kDecode32:
+        hipLaunchKernelGGL((xform32_persist_kernel<0, 32>), pgrid, block, 0, stream, p);
+        break;
+      default:
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
+  const dim3 grid(static_cast<unsigned>(groups));
   switch (kind) {
     case XformKind::kEncode32:
       hipLaunchKernelGGL((xform32_kernel<32, 0>), grid, block, 0, stream, p);
@@ -450,4 +588,12 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nblocks, uint64_t block_b
   return hipGetLastError();
 }
 
+void set_xform_variant(int v) { g_xform_variant = v; }
+
 }  // namespace ag
+
+// internal A/B hook (not part of the public header)
+extern "C" int ag_rs_internal_set_xform_variant(int v) {
+  ag::set_xform_variant(v);
+  return 0;
+}

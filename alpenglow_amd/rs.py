@@ -60,7 +60,8 @@ STATUS_KIND = {
 # every exported symbol of include/alpenglow_rs.h (checked by tests/test_capi.py)
 EXPORTS = (
     "ag_rs_status_string", "ag_rs_abi_version", "ag_rs_device_count",
-    "ag_rs_ctx_create", "ag_rs_ctx_destroy", "ag_rs_ctx_set_stream", "ag_rs_ctx_stream",
+    "ag_rs_ctx_create", "ag_rs_ctx_destroy", "ag_rs_ctx_set_stream", "ag_rs_ctx_reset_stream",
+    "ag_rs_ctx_stream",
     "ag_rs_ctx_synchronize", "ag_rs_use_high_rate", "ag_rs_has_fast_path",
     "ag_rs_encode_batch", "ag_rs_decode_batch", "ag_rs_fill_splitmix",
     "ag_rs_encoder_new", "ag_rs_encoder_reset", "ag_rs_encoder_add_original_shard",
@@ -101,6 +102,7 @@ def load():
         "ag_rs_ctx_create": ([i, pp], i),
         "ag_rs_ctx_destroy": ([p], None),
         "ag_rs_ctx_set_stream": ([p, p], i),
+        "ag_rs_ctx_reset_stream": ([p], i),
         "ag_rs_ctx_stream": ([p], p),
         "ag_rs_ctx_synchronize": ([p], i),
         "ag_rs_use_high_rate": ([sz, sz], i),
@@ -171,8 +173,13 @@ class Context:
         self.device = device
 
     def set_stream(self, hip_stream: int | None):
-        _check(self._lib.ag_rs_ctx_set_stream(self.handle, ctypes.c_void_p(hip_stream or 0)),
-               "ag_rs_ctx_set_stream")
+        """Launch on ``hip_stream`` (an int handle, e.g. ``torch.cuda.Stream().cuda_stream``;
+        0 is the null stream).  ``None`` returns to the context's own stream."""
+        if hip_stream is None:
+            _check(self._lib.ag_rs_ctx_reset_stream(self.handle), "ag_rs_ctx_reset_stream")
+        else:
+            _check(self._lib.ag_rs_ctx_set_stream(self.handle, ctypes.c_void_p(hip_stream)),
+                   "ag_rs_ctx_set_stream")
 
     @property
     def stream(self) -> int:

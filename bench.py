@@ -77,7 +77,8 @@ def main():
     cw_stride = (k + m) * S
 
     ctx = rs.Context(local)
-    stream = torch.cuda.current_stream(dev)
+    stream = torch.cuda.Stream(dev)  # explicit stream: torch work, kernels and events share it
+    torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
 
     # codeword buffer: block b = k data shards then m coding shards (HBM-resident)

@@ -83,9 +83,11 @@ typedef struct ag_rs_ctx ag_rs_ctx;
 
 int ag_rs_ctx_create(int device, ag_rs_ctx** out);
 void ag_rs_ctx_destroy(ag_rs_ctx* ctx);
-/* Use an external hipStream_t (e.g. torch's current stream); NULL restores the
- * context's own stream. */
+/* Launch on an external hipStream_t (e.g. torch's current stream).  NULL is the HIP
+ * null stream; ag_rs_ctx_reset_stream returns to the context's own stream (created
+ * blocking, so it is ordered with the null stream). */
 int ag_rs_ctx_set_stream(ag_rs_ctx* ctx, void* hip_stream);
+int ag_rs_ctx_reset_stream(ag_rs_ctx* ctx);
 void* ag_rs_ctx_stream(ag_rs_ctx* ctx);
 int ag_rs_ctx_synchronize(ag_rs_ctx* ctx);
 int ag_rs_device_count(int* count);

@@ -30,13 +30,16 @@ def _shards(seed, n, S):
 
 @pytest.fixture(scope="module")
 def dev(ctx):
+    """All torch work and every library launch go to one explicit (non-null) stream."""
     d = torch.device("cuda:0")
-    ctx.set_stream(torch.cuda.current_stream(d).cuda_stream)
+    s = torch.cuda.Stream(d)
+    torch.cuda.set_stream(s)
+    ctx.set_stream(s.cuda_stream)
     return d
 
 
 def to_dev(a, dev):
-    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    return torch.from_numpy(np.array(a, copy=True)).to(dev)
 
 
 def gpu_encode(ctx, dev, blocks: np.ndarray, m: int) -> np.ndarray:
