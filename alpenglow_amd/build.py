@@ -19,8 +19,8 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
-OBJDIR = os.path.join(LIBDIR, "obj")
-LIB = os.path.join(LIBDIR, "libalpenglow_rs.so")
+OBJDIR = os.path.join(LIBDIR, os.environ.get("AG_RS_OBJ_DIR", "obj"))
+LIB = os.path.join(LIBDIR, os.environ.get("AG_RS_LIB_NAME", "libalpenglow_rs.so"))
 INCLUDE = os.path.join(os.path.dirname(HERE), "include")
 
 ARCH = "gfx950"
@@ -31,7 +31,8 @@ SOURCES = ["rs_kernels.hip", "rs_api.cpp", "gf16.cpp"]
 HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_launch.hpp", "rs_consts.inc"]
 # -fno-slp-vectorize: the SLP vectoriser packs the bitsliced XOR networks into <2 x i32>
 # ops, which lengthens live ranges (measured +40 VGPRs on the transform kernel).
-HIP_FLAGS = ["-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
+HIP_FLAGS = [*os.environ.get("AG_RS_EXTRA_HIPFLAGS", "").split(),
+             "-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
              "-Wall", "-Wno-unused-command-line-argument", f"-I{INCLUDE}", f"-I{CSRC}"]
 
 

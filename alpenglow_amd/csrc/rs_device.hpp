@@ -119,6 +119,10 @@ __device__ __forceinline__ void planes_from_raw(uint32_t* v) {
   transpose8(v);
   transpose8(v + 8);
 }
+using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
+
+// NT: non-temporal stores (streamed once; keeps L2 for the loads).
+template <bool NT = false>
 __device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, const uint32_t* planes) {
   uint32_t v[16];
   static_for<16>([&](auto P) {
@@ -127,11 +131,16 @@ __device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, const uin
   });
   transpose8(v);
   transpose8(v + 8);
-  uint4* d = reinterpret_cast<uint4*>(dst);
-  d[0] = make_uint4(v[0], v[1], v[2], v[3]);
-  d[1] = make_uint4(v[4], v[5], v[6], v[7]);
-  d[2] = make_uint4(v[8], v[9], v[10], v[11]);
-  d[3] = make_uint4(v[12], v[13], v[14], v[15]);
+  u32x4* d = reinterpret_cast<u32x4*>(dst);
+  static_for<4>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    const u32x4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+    if constexpr (NT) {
+      __builtin_nontemporal_store(x, d + q);
+    } else {
+      d[q] = x;
+    }
+  });
 }
 
 // ---- table arithmetic for the generic (any-geometry) kernels ------------------------

@@ -16,8 +16,6 @@
 #include "rs_device.hpp"
 #include "rs_launch.hpp"
 
-#include <cstdlib>
-
 namespace ag {
 namespace {
 
@@ -41,6 +39,9 @@ using Regs8 = uint32_t[8][16];
 // butterfly whose skew index is BASE + 8 * wave (wave-uniform, runtime)
 template <int BASE, bool INV>
 __device__ __forceinline__ void bfly_w(int wave, uint32_t* x, uint32_t* y) {
+#ifdef AG_XF_DIAG_ONE_ROLE
+  wave = 0;  // diagnostic build only: every wave runs role 0's code (wrong output)
+#endif
   switch (wave) {
     case 0: if constexpr (INV) dev::ifft_bfly<BASE>(x, y); else dev::fft_bfly<BASE>(x, y); break;
     case 1: if constexpr (INV) dev::ifft_bfly<BASE + 8>(x, y); else dev::fft_bfly<BASE + 8>(x, y); break;
@@ -122,192 +123,219 @@ __device__ __forceinline__ void lds_get(const uint4* lds, int slot, int lane, ui
   });
 }
 
-// Column geometry of lane `lane` in tile `tile` (idle lanes redo the last column).
-struct ColInfo {
-  bool active;
-  uint64_t blk;
-  uint64_t chunk_off;
+// ---- tile I/O -------------------------------------------------------------------
+// A tile is 64 consecutive 64-byte chunks (global chunk index g = 64 * tile + c; chunk g
+// is chunk g % C of block g / C, C = chunks per shard).  Each of a lane's four 16-byte
+// loads per shard is one slice of a lane-linear 1 KiB wave access: instruction q covers
+// chunks 16q .. 16q+15 of the tile; lane l < 32 takes low-byte quarter (l & 1) of chunk
+// 16q + (l >> 1), lane l + 32 the matching high-byte quarter.  One v_permlane32_swap per
+// register pair then gives every lane the low AND high bytes of 32 symbols (2 chunks x 16
+// symbols): lane l < 32 keeps chunks q = 0, 1, lane l + 32 chunks q = 2, 3.
+struct TileIO {
+  uint64_t off[4];  // byte offset of this lane's 16-byte piece of shard 0, per instruction q
+  uint64_t blk[4];  // block of chunk q (for the per-block store mask)
+  uint32_t valid;   // bit q: chunk q exists (idle pieces re-read the last chunk, never store)
 };
-__device__ __forceinline__ ColInfo col_info(const XformParams& p, uint64_t tile, int lane) {
-  const uint64_t col = tile * kXfLanes + lane;
-  ColInfo c;
-  c.active = col < p.total_columns;
-  const uint64_t colc = c.active ? col : p.total_columns - 1;
-  c.blk = colc / p.chunks_per_shard;
-  c.chunk_off = (colc - c.blk * p.chunks_per_shard) * 64;
-  return c;
+__device__ __forceinline__ TileIO tile_io(const XformParams& p, uint64_t tile, int lane, uint64_t block_stride) {
+  TileIO io;
+  io.valid = 0;
+  const uint32_t quarter = ((lane >> 5) << 1) | (lane & 1);
+  static_for<4>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    const uint64_t g = tile * kXfLanes + 16 * q + ((lane & 31) >> 1);
+    const bool ok = g < p.total_columns;
+    const uint64_t gc = ok ? g : p.total_columns - 1;
+    const uint64_t blk = gc / p.chunks_per_shard;
+    io.blk[q] = blk;
+    io.off[q] = blk * block_stride + (gc - blk * p.chunks_per_shard) * 64 + 16 * quarter;
+    io.valid |= ok ? (1u << q) : 0u;
+  });
+  return io;
 }
 
-// Raw (untransposed) 64-byte chunks of this wave's pass-A shards 8*wave + t.
-__device__ __forceinline__ void xf32_load_raw(const XformParams& p, const ColInfo& c, int wave, Regs8& raw) {
-  const uint8_t* base = p.in + c.blk * p.in_block_stride + c.chunk_off;
+// lanes l and l + 32 exchange register halves (see TileIO); an involution
+__device__ __forceinline__ void swap_halves(uint32_t* v) {
+  static_for<8>([&](auto K) {
+    constexpr int k = decltype(K)::value;
+    const auto r = __builtin_amdgcn_permlane32_swap(v[k], v[k + 8], false, false);
+    v[k] = r[0];
+    v[k + 8] = r[1];
+  });
+}
+
+// Raw 16-byte pieces of this wave's pass-A shards 8*wave + t (before swap / transpose).
+__device__ __forceinline__ void xf32_load_raw(const XformParams& p, const TileIO& io, int wave, Regs8& raw) {
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = 8 * wave + t;  // wave-uniform condition
     if (s < p.n_in) {
-      dev::load_chunk(base + s * p.in_shard_stride, raw[t]);
+      const uint8_t* base = p.in + s * p.in_shard_stride;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        raw[t][4 * q] = x.x;
+        raw[t][4 * q + 1] = x.y;
+        raw[t][4 * q + 2] = x.z;
+        raw[t][4 * q + 3] = x.w;
+      });
     } else {
       static_for<16>([&](auto P) { raw[t][decltype(P)::value] = 0; });
     }
   });
 }
 
-// Everything after the loads: transposes, the three passes with their two LDS exchanges,
-// inverse transposes and the masked stores of this wave's pass-C shards.
-template <int DIN, int DOUT>
-__device__ __forceinline__ void xf32_body(const XformParams& p, const ColInfo& c, int wave, int lane, uint4* lds,
+// Planes -> bytes -> lane-linear pieces, stored where the input pieces were read.
+__device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const TileIO& io, uint32_t qmask,
+                                            const uint32_t* planes) {
+  uint32_t v[16];
+  static_for<16>([&](auto P) {
+    constexpr int i = decltype(P)::value;
+    v[i] = planes[i];
+  });
+  dev::transpose8(v);
+  dev::transpose8(v + 8);
+  swap_halves(v);
+  static_for<4>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    if (qmask & (1u << q))
+      *reinterpret_cast<uint4*>(base + io.off[q]) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  });
+}
+
+// LDS exchange between passes.  Pass A/C slot t of wave w holds shard 8w+t; pass B slot
+// t' of wave w' holds shard w'+4t' (so A-slot t of wave w <-> B-slot 2w+(t>>2) of wave t&3).
+// ROUNDS = 2: each round moves 4 slots per wave through 64 KiB.  (ROUNDS = 4, 32 KiB per
+// round with wave-dependent slot pairing, is kept for experiments: it spills, because the
+// slot indices then depend on the runtime wave id.)
+template <int ROUNDS>
+__device__ __forceinline__ void xf32_exchange_ab(int wave, int lane, uint4* lds, Regs8& ra, Regs8& rb) {
+  if constexpr (ROUNDS == 2) {
+    static_for<2>([&](auto Rho) {
+      constexpr int rho = decltype(Rho)::value;
+      static_for<4>([&](auto U) {
+        constexpr int u = decltype(U)::value;
+        lds_put(lds, 4 * wave + u, lane, ra[4 * rho + u]);
+      });
+      __syncthreads();
+      static_for<4>([&](auto W2) {
+        constexpr int w2 = decltype(W2)::value;
+        lds_get(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
+      });
+      __syncthreads();
+    });
+  } else {
+    static_for<4>([&](auto Rho) {
+      constexpr int rho = decltype(Rho)::value;
+      // writer w sends A-slots t0, t0+4 with t0 = (w+rho)&3 to wave t0
+      static_for<4>([&](auto Wc) {
+        constexpr int w = decltype(Wc)::value;
+        if (wave == w) {
+          constexpr int t0 = (w + rho) & 3;
+          lds_put(lds, 2 * w + 0, lane, ra[t0]);
+          lds_put(lds, 2 * w + 1, lane, ra[t0 + 4]);
+        }
+      });
+      __syncthreads();
+      // reader w' receives from writer w = (w'-rho)&3 into B-slots 2w, 2w+1
+      static_for<4>([&](auto Wc) {
+        constexpr int wr = decltype(Wc)::value;
+        if (wave == wr) {
+          constexpr int w = (wr - rho) & 3;
+          lds_get(lds, 2 * w + 0, lane, rb[2 * w + 0]);
+          lds_get(lds, 2 * w + 1, lane, rb[2 * w + 1]);
+        }
+      });
+      __syncthreads();
+    });
+  }
+}
+
+template <int ROUNDS>
+__device__ __forceinline__ void xf32_exchange_bc(int wave, int lane, uint4* lds, Regs8& rb, Regs8& ra) {
+  if constexpr (ROUNDS == 2) {
+    static_for<2>([&](auto Rho) {
+      constexpr int rho = decltype(Rho)::value;
+      static_for<4>([&](auto W2) {
+        constexpr int w2 = decltype(W2)::value;
+        lds_put(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
+      });
+      __syncthreads();
+      static_for<4>([&](auto U) {
+        constexpr int u = decltype(U)::value;
+        lds_get(lds, 4 * wave + u, lane, ra[4 * rho + u]);
+      });
+      __syncthreads();
+    });
+  } else {
+    static_for<4>([&](auto Rho) {
+      constexpr int rho = decltype(Rho)::value;
+      // writer w' sends B-slots 2w, 2w+1 to pass-C wave w = (w'-rho)&3
+      static_for<4>([&](auto Wc) {
+        constexpr int wp = decltype(Wc)::value;
+        if (wave == wp) {
+          constexpr int w = (wp - rho) & 3;
+          lds_put(lds, 2 * wp + 0, lane, rb[2 * w + 0]);
+          lds_put(lds, 2 * wp + 1, lane, rb[2 * w + 1]);
+        }
+      });
+      __syncthreads();
+      // reader w receives from w' = (w+rho)&3 into C-slots w', w'+4
+      static_for<4>([&](auto Wc) {
+        constexpr int w = decltype(Wc)::value;
+        if (wave == w) {
+          constexpr int wp = (w + rho) & 3;
+          lds_get(lds, 2 * wp + 0, lane, ra[wp]);
+          lds_get(lds, 2 * wp + 1, lane, ra[wp + 4]);
+        }
+      });
+      __syncthreads();
+    });
+  }
+}
+
+// Everything after the loads: half swap + transposes, the three passes with their two
+// LDS exchanges, inverse transposes and the masked stores of this wave's pass-C shards.
+template <int DIN, int DOUT, int ROUNDS>
+__device__ __forceinline__ void xf32_body(const XformParams& p, const TileIO& out_io, int wave, int lane, uint4* lds,
                                           Regs8& ra) {
-  static_for<8>([&](auto T) { dev::planes_from_raw(ra[decltype(T)::value]); });
+  static_for<8>([&](auto T) {
+    swap_halves(ra[decltype(T)::value]);
+    dev::planes_from_raw(ra[decltype(T)::value]);
+  });
   xf32_pass_a<DIN>(wave, ra);
   Regs8 rb;
-  static_for<2>([&](auto Rho) {  // exchange A -> B: round rho moves slots 4rho..4rho+3
-    constexpr int rho = decltype(Rho)::value;
-    static_for<4>([&](auto U) {
-      constexpr int u = decltype(U)::value;
-      lds_put(lds, 4 * wave + u, lane, ra[4 * rho + u]);
-    });
-    __syncthreads();
-    static_for<4>([&](auto W2) {
-      constexpr int w2 = decltype(W2)::value;
-      lds_get(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
-    });
-    __syncthreads();
-  });
+  xf32_exchange_ab<ROUNDS>(wave, lane, lds, ra, rb);
   xf32_pass_b<DIN, DOUT>(rb);
-  static_for<2>([&](auto Rho) {  // exchange B -> C (inverse mapping)
-    constexpr int rho = decltype(Rho)::value;
-    static_for<4>([&](auto W2) {
-      constexpr int w2 = decltype(W2)::value;
-      lds_put(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
-    });
-    __syncthreads();
-    static_for<4>([&](auto U) {
-      constexpr int u = decltype(U)::value;
-      lds_get(lds, 4 * wave + u, lane, ra[4 * rho + u]);
-    });
-    __syncthreads();
-  });
+  xf32_exchange_bc<ROUNDS>(wave, lane, lds, rb, ra);
   xf32_pass_c<DOUT>(wave, ra);
-  if (c.active) {
-    uint8_t* base = p.out + c.blk * p.out_block_stride + c.chunk_off;
-    const uint8_t* mask = nullptr;
-    if (p.out_mask) mask = p.out_mask + (p.pattern_per_block ? c.blk : 0) * p.out_mask_stride;
-    static_for<8>([&](auto T) {
-      constexpr int t = decltype(T)::value;
-      const uint32_t s = 8 * wave + t;
-      if (s < p.n_out && (mask == nullptr || mask[s])) dev::store_chunk(base + s * p.out_shard_stride, ra[t]);
-    });
-  }
-}
-
-// Persistent variant: one 4-wave workgroup per CU walks tiles blockIdx.x, +gridDim.x, ...
-// and keeps the next tile's 8 raw chunks per lane in flight (128 VGPRs) while it computes
-// the current one -- one wave per SIMD, 512-register budget.
-template <int DIN, int DOUT>
-__global__ __launch_bounds__(256, 1) void xform32_persist_kernel(const XformParams p) {
-  __shared__ uint4 lds[kXfLdsSlots * 4 * kXfLanes];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t ntiles = (p.total_columns + kXfLanes - 1) / kXfLanes;
-  uint64_t tile = blockIdx.x;
-  if (tile >= ntiles) return;
-  Regs8 raw;
-  ColInfo c = col_info(p, tile, lane);
-  xf32_load_raw(p, c, wave, raw);
-  for (;;) {
-    Regs8 ra;
-    static_for<8>([&](auto T) {
-      constexpr int t = decltype(T)::value;
-      static_for<16>([&](auto P) { ra[t][decltype(P)::value] = raw[t][decltype(P)::value]; });
-    });
-    const uint64_t next = tile + gridDim.x;
-    const bool more = next < ntiles;
-    const ColInfo cn = col_info(p, more ? next : tile, lane);
-    if (more) xf32_load_raw(p, cn, wave, raw);
-    xf32_body<DIN, DOUT>(p, c, wave, lane, lds, ra);
-    if (!more) break;
-    tile = next;
-    c = cn;
-  }
-}
-
-template <int DIN, int DOUT>
-__global__ __launch_bounds__(256, 2) void xform32_kernel(const XformParams p) {
-  __shared__ uint4 lds[kXfLdsSlots * 4 * kXfLanes];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t col = static_cast<uint64_t>(blockIdx.x) * kXfLanes + lane;
-  const bool active = col < p.total_columns;
-  const uint64_t colc = active ? col : p.total_columns - 1;  // idle lanes redo the last column
-  const uint64_t blk = colc / p.chunks_per_shard;
-  const uint64_t chunk_off = (colc - blk * p.chunks_per_shard) * 64;
-
-  Regs8 ra;
-  {
-    const uint8_t* base = p.in + blk * p.in_block_stride + chunk_off;
-    static_for<8>([&](auto T) {
-      constexpr int t = decltype(T)::value;
-      const uint32_t s = 8 * wave + t;  // wave-uniform condition
-      if (s < p.n_in) {
-        dev::load_chunk(base + s * p.in_shard_stride, ra[t]);
-      } else {
-        static_for<16>([&](auto P) { ra[t][decltype(P)::value] = 0; });
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = 8 * wave + t;  // wave-uniform
+    if (s < p.n_out) {
+      uint32_t qmask = out_io.valid;  // chunk exists and (with a mask) shard s is selected
+      if (p.out_mask) {
+        static_for<4>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          const uint64_t pat = p.pattern_per_block ? out_io.blk[q] : 0;
+          if (!p.out_mask[pat * p.out_mask_stride + s]) qmask &= ~(1u << q);
+        });
       }
-    });
-    static_for<8>([&](auto T) { dev::planes_from_raw(ra[decltype(T)::value]); });
-  }
-
-  xf32_pass_a<DIN>(wave, ra);
-
-  // exchange A -> B: round rho moves pass-A slots 4rho..4rho+3 (shard bit 2 == rho)
-  Regs8 rb;
-  static_for<2>([&](auto Rho) {
-    constexpr int rho = decltype(Rho)::value;
-    static_for<4>([&](auto U) {
-      constexpr int u = decltype(U)::value;
-      lds_put(lds, 4 * wave + u, lane, ra[4 * rho + u]);
-    });
-    __syncthreads();
-    static_for<4>([&](auto W2) {
-      constexpr int w2 = decltype(W2)::value;
-      lds_get(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
-    });
-    __syncthreads();
-  });
-
-  xf32_pass_b<DIN, DOUT>(rb);
-
-  // exchange B -> C (inverse mapping)
-  static_for<2>([&](auto Rho) {
-    constexpr int rho = decltype(Rho)::value;
-    static_for<4>([&](auto W2) {
-      constexpr int w2 = decltype(W2)::value;
-      lds_put(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
-    });
-    __syncthreads();
-    static_for<4>([&](auto U) {
-      constexpr int u = decltype(U)::value;
-      lds_get(lds, 4 * wave + u, lane, ra[4 * rho + u]);
-    });
-    __syncthreads();
-  });
-
-  xf32_pass_c<DOUT>(wave, ra);
-
-  if (active) {
-    uint8_t* base = p.out + blk * p.out_block_stride + chunk_off;
-    const uint8_t* mask = nullptr;
-    if (p.out_mask) {
-      const uint64_t pat = p.pattern_per_block ? blk : 0;
-      mask = p.out_mask + pat * p.out_mask_stride;
+      store_shard(p.out + s * p.out_shard_stride, out_io, qmask, ra[t]);
     }
-    static_for<8>([&](auto T) {
-      constexpr int t = decltype(T)::value;
-      const uint32_t s = 8 * wave + t;
-      if (s < p.n_out && (mask == nullptr || mask[s])) dev::store_chunk(base + s * p.out_shard_stride, ra[t]);
-    });
-  }
+  });
 }
+
+// One 64-chunk tile per workgroup: 64 KiB LDS (ROUNDS = 2), two workgroups per CU.
+template <int DIN, int DOUT, int ROUNDS, int LB>
+__global__ __launch_bounds__(256, LB) void xform32_kernel(const XformParams p) {
+  __shared__ uint4 lds[(ROUNDS == 2 ? 16 : 8) * 4 * kXfLanes];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  Regs8 ra;
+  xf32_load_raw(p, tile_io(p, blockIdx.x, lane, p.in_block_stride), wave, ra);
+  xf32_body<DIN, DOUT, ROUNDS>(p, tile_io(p, blockIdx.x, lane, p.out_block_stride), wave, lane, lds, ra);
+}
+
 
 // =====================================================================================
 // Generic kernels: one thread per (block, symbol position); the crate's algorithm with
@@ -512,44 +540,18 @@ __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* dst, uint64
 // ---- launchers ----------------------------------------------------------------------
 bool xform_supported(unsigned n) { return n == 32; }
 
-static int g_xform_variant = -1;  // -1: default; 0: one tile per workgroup; 1: persistent
-
-static int xform_variant() {
-  if (g_xform_variant < 0) {
-    const char* e = getenv("AG_RS_XFORM_VARIANT");
-    g_xform_variant = e ? atoi(e) : 0;
-  }
-  return g_xform_variant;
-}
-
 hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream) {
   if (p.total_columns == 0) return hipSuccess;
   const uint64_t groups = (p.total_columns + kXfLanes - 1) / kXfLanes;
   if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const dim3 block(256);
-  if (xform_variant() == 1) {
-    int dev = 0, cus = 256;
-    if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    const dim3 pgrid(static_cast<unsigned>(groups < static_cast<uint64_t>(cus) ? groups : cus));
-    switch (kind) {
-      case XformKind::kEncode32:
-        hipLaunchKernelGGL((xform32_persist_kernel<32, 0>), pgrid, block, 0, stream, p);
-        break;
-      case XformKind::kDecode32:
-        hipLaunchKernelGGL((xform32_persist_kernel<0, 32>), pgrid, block, 0, stream, p);
-        break;
-      default:
-        return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
   const dim3 grid(static_cast<unsigned>(groups));
   switch (kind) {
     case XformKind::kEncode32:
-      hipLaunchKernelGGL((xform32_kernel<32, 0>), grid, block, 0, stream, p);
+      hipLaunchKernelGGL((xform32_kernel<32, 0, 2, 2>), grid, block, 0, stream, p);
       break;
     case XformKind::kDecode32:
-      hipLaunchKernelGGL((xform32_kernel<0, 32>), grid, block, 0, stream, p);
+      hipLaunchKernelGGL((xform32_kernel<0, 32, 2, 2>), grid, block, 0, stream, p);
       break;
     default:
       return hipErrorInvalidValue;
@@ -588,12 +590,4 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nblocks, uint64_t block_b
   return hipGetLastError();
 }
 
-void set_xform_variant(int v) { g_xform_variant = v; }
-
 }  // namespace ag
-
-// internal A/B hook (not part of the public header)
-extern "C" int ag_rs_internal_set_xform_variant(int v) {
-  ag::set_xform_variant(v);
-  return 0;
-}

@@ -24,7 +24,8 @@ import ctypes
 import os
 from dataclasses import dataclass
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "libalpenglow_rs.so")
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                        os.environ.get("AG_RS_LIB_NAME", "libalpenglow_rs.so"))
 
 MEM_DEVICE = 0
 MEM_HOST = 1

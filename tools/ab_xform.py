@@ -20,13 +20,18 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--nblocks", type=int, default=4096)
     ap.add_argument("--shard", type=int, default=32768)
+    ap.add_argument("--no-check", action="store_true", help="diagnostic builds with wrong output")
     args = ap.parse_args()
     import torch
     from alpenglow_amd import rs
 
     lib = rs.load()
-    setv = lib.ag_rs_internal_set_xform_variant
-    setv.argtypes = [ctypes.c_int]
+    if hasattr(lib, "ag_rs_internal_set_xform_variant"):
+        setv = lib.ag_rs_internal_set_xform_variant
+        setv.argtypes = [ctypes.c_int]
+    else:  # single-variant build: time the default kernel
+        def setv(v):
+            return 0
     dev = torch.device("cuda:0")
     ctx = rs.Context(0)
     st = torch.cuda.Stream(dev)
@@ -61,7 +66,7 @@ def main():
             chk = cw.sum(dtype=torch.int64).item()
             if ref is None:
                 ref = chk
-            assert chk == ref, "variant changed the output"
+            assert args.no_check or chk == ref, "variant changed the output"
     B = k * S
     out = {}
     for v in variants:

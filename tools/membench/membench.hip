@@ -1,0 +1,138 @@
+// Memory-pattern microbenchmark (diagnostic): HBM copy throughput with
+//  (a) coalesced 16 B/lane loads+stores (lane i at base + 16 i, 1 KiB per instruction)
+//  (b) the transform kernel's pattern: lane owns a 64-byte chunk, 4 x 16 B per chunk
+//      (lane stride 64 B), 8 chunks per lane from 8 "shards" (stride = shard bytes)
+// Usage: membench [bytes_GiB]
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+
+__global__ __launch_bounds__(256) void copy_coalesced(const uint4* __restrict__ in, uint4* __restrict__ out, size_t n16) {
+  size_t i = (size_t)blockIdx.x * 256 * 8 + threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    size_t j = i + (size_t)k * 256;
+    if (j < n16) out[j] = in[j];
+  }
+}
+
+// tile = 64 columns x 8 shards per wave; shard stride S bytes; block = 32 shards
+template <int CHUNKS>
+__global__ __launch_bounds__(256, 2) void copy_chunks(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                      size_t S, size_t nblocks) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t cps = S / 64;
+  const size_t col = (size_t)blockIdx.x * 64 + lane;
+  const size_t blk = col / cps, ch = col % cps;
+  if (blk >= nblocks) return;
+  uint4 v[CHUNKS][4];
+#pragma unroll
+  for (int t = 0; t < CHUNKS; ++t) {
+    const uint4* s = (const uint4*)(in + blk * 32 * S + (size_t)(8 * wave + t) * S + ch * 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[t][q] = s[q];
+  }
+#pragma unroll
+  for (int t = 0; t < CHUNKS; ++t) {
+    uint4* d = (uint4*)(out + blk * 32 * S + (size_t)(8 * wave + t) * S + ch * 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q] = v[t][q];
+  }
+}
+
+// same tile shape, but each wave-instruction covers 1 KiB contiguous (lane-linear)
+template <int CHUNKS>
+__global__ __launch_bounds__(256, 2) void copy_chunks_lin(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                          size_t S, size_t nblocks) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t cps = S / 64;
+  const size_t col0 = (size_t)blockIdx.x * 64;
+  const size_t blk = col0 / cps, ch0 = col0 % cps;  // assumes cps % 64 == 0
+  if (blk >= nblocks) return;
+  uint4 v[CHUNKS][4];
+#pragma unroll
+  for (int t = 0; t < CHUNKS; ++t) {
+    const uint4* s = (const uint4*)(in + blk * 32 * S + (size_t)(8 * wave + t) * S + ch0 * 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[t][q] = s[q * 64 + lane];
+  }
+#pragma unroll
+  for (int t = 0; t < CHUNKS; ++t) {
+    uint4* d = (uint4*)(out + blk * 32 * S + (size_t)(8 * wave + t) * S + ch0 * 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) d[q * 64 + lane] = v[t][q];
+  }
+}
+
+// "half-coalesced": instruction q covers the lo (q<2) or hi (q>=2) 32-byte halves of 32
+// chunks; lanes 2i, 2i+1 take the two 16-byte pieces of chunk half i.  A lane ends up
+// with lo+hi bytes of symbols 0-15 (even lanes) or 16-31 (odd lanes) of 2 chunks.
+template <int CHUNKS>
+__global__ __launch_bounds__(256, 2) void copy_chunks_half(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                           size_t S, size_t nblocks) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t cps = S / 64;
+  const size_t col0 = (size_t)blockIdx.x * 64;
+  const size_t blk = col0 / cps, ch0 = col0 % cps;
+  if (blk >= nblocks) return;
+  const int i = lane >> 1, h = lane & 1;
+  uint4 v[CHUNKS][4];
+#pragma unroll
+  for (int t = 0; t < CHUNKS; ++t) {
+    const uint8_t* s = in + blk * 32 * S + (size_t)(8 * wave + t) * S + ch0 * 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[t][q] = *(const uint4*)(s + (size_t)((q & 1) * 32 + i) * 64 + (q >> 1) * 32 + h * 16);
+  }
+#pragma unroll
+  for (int t = 0; t < CHUNKS; ++t) {
+    uint8_t* d = out + blk * 32 * S + (size_t)(8 * wave + t) * S + ch0 * 64;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) *(uint4*)(d + (size_t)((q & 1) * 32 + i) * 64 + (q >> 1) * 32 + h * 16) = v[t][q];
+  }
+}
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+int main(int argc, char** argv) {
+  double gib = argc > 1 ? atof(argv[1]) : 4.0;
+  size_t bytes = (size_t)(gib * (1ull << 30));
+  const size_t S = 32768, blockb = 32 * S;
+  size_t nblocks = bytes / blockb;
+  bytes = nblocks * blockb;
+  uint8_t *a, *b;
+  CK(hipMalloc(&a, bytes));
+  CK(hipMalloc(&b, bytes));
+  CK(hipMemset(a, 1, bytes));
+  CK(hipMemset(b, 0, bytes));
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  const size_t cols = nblocks * (S / 64);
+  const int reps = 10;
+  for (int variant = 0; variant < 4; ++variant) {
+    for (int rep = 0; rep < 2; ++rep) {
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < reps; ++r) {
+        if (variant == 0) {
+          size_t n16 = bytes / 16;
+          hipLaunchKernelGGL(copy_coalesced, dim3((n16 + 2047) / 2048), dim3(256), 0, 0, (const uint4*)a, (uint4*)b, n16);
+        } else if (variant == 1) {
+          hipLaunchKernelGGL(copy_chunks<8>, dim3((cols + 63) / 64), dim3(256), 0, 0, a, b, S, nblocks);
+        } else if (variant == 2) {
+          hipLaunchKernelGGL(copy_chunks_lin<8>, dim3((cols + 63) / 64), dim3(256), 0, 0, a, b, S, nblocks);
+        } else {
+          hipLaunchKernelGGL(copy_chunks_half<8>, dim3((cols + 63) / 64), dim3(256), 0, 0, a, b, S, nblocks);
+        }
+      }
+      CK(hipEventRecord(e1));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      if (rep == 1)
+        printf("%s: %.3f ms per copy of %.2f GiB, %.0f GB/s (read+write)\n",
+               variant == 0 ? "coalesced 16B/lane   " : variant == 1 ? "chunk 64B/lane strided" : variant == 2 ? "chunk tile lane-linear" : "chunk tile half-coalesced",
+               ms / reps, bytes / double(1ull << 30), 2.0 * bytes / (ms / reps * 1e-3) / 1e9);
+    }
+  }
+  return 0;
+}
