@@ -83,7 +83,7 @@ struct ag_rs_ctx {
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf stage_in, stage_out;             // host-memory calls
   DevBuf one_in, one_out;                 // crate-API single codeword
-  std::vector<uint8_t> mask_host;         // last store mask uploaded to d_mask
+  std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
 
   int enter() { return hipSetDevice(device) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE; }
 
@@ -212,17 +212,18 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   }
   int st;
   if (any_fast) {
-    // store mask: restore original i of a block iff its pattern is fast and i is absent
-    std::vector<uint8_t> mask(npat * k, 0);
+    // store mask word per pattern: restore original i iff the pattern is fast and i is absent
+    std::vector<uint64_t> mask(npat, 0);
     for (size_t p = 0; p < npat; ++p)
       if (cls[p] == 1)
-        for (size_t i = 0; i < k; ++i) mask[p * k + i] = opres[p * k + i] ? 0 : 1;
+        for (size_t i = 0; i < k; ++i)
+          if (!opres[p * k + i]) mask[p] |= uint64_t{1} << i;
     // upload only when the pattern set changed (steady-state batches reuse it, no sync)
     if (mask != c->mask_host) {
       AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read mask_host
-      if ((st = c->d_mask.ensure(mask.size(), c->stream))) return st;
+      if ((st = c->d_mask.ensure(mask.size() * 8, c->stream))) return st;
       c->mask_host = mask;
-      AG_HIP(hipMemcpyAsync(c->d_mask.ptr, c->mask_host.data(), mask.size(), hipMemcpyHostToDevice, c->stream));
+      AG_HIP(hipMemcpyAsync(c->d_mask.ptr, c->mask_host.data(), mask.size() * 8, hipMemcpyHostToDevice, c->stream));
     }
     ag::XformParams p{};
     p.in = rec;
@@ -231,8 +232,7 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     p.out = orig;
     p.out_block_stride = ostride;
     p.out_shard_stride = S;
-    p.out_mask = c->d_mask.as<uint8_t>();
-    p.out_mask_stride = k;
+    p.out_mask = c->d_mask.as<uint64_t>();
     p.pattern_per_block = npat > 1 ? 1u : 0u;
     p.n_in = static_cast<uint32_t>(m);
     p.n_out = static_cast<uint32_t>(k);

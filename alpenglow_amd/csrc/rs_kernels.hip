@@ -293,36 +293,15 @@ __device__ __forceinline__ void xf32_exchange_bc(int wave, int lane, uint4* lds,
   }
 }
 
-// Everything after the loads: half swap + transposes, the three passes with their two
-// LDS exchanges, inverse transposes and the masked stores of this wave's pass-C shards.
-template <int DIN, int DOUT, int ROUNDS>
-__device__ __forceinline__ void xf32_body(const XformParams& p, const TileIO& out_io, int wave, int lane, uint4* lds,
-                                          Regs8& ra) {
-  static_for<8>([&](auto T) {
-    swap_halves(ra[decltype(T)::value]);
-    dev::planes_from_raw(ra[decltype(T)::value]);
+// Store predicate of this wave's shard s for the four chunk slices of the tile: chunk
+// exists and, with a mask, bit s of its block's pattern word is set.
+__device__ __forceinline__ uint32_t store_qmask(const TileIO& io, const uint64_t* mask, uint32_t s) {
+  uint32_t qm = io.valid;
+  static_for<4>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    if (!((mask[q] >> s) & 1)) qm &= ~(1u << q);
   });
-  xf32_pass_a<DIN>(wave, ra);
-  Regs8 rb;
-  xf32_exchange_ab<ROUNDS>(wave, lane, lds, ra, rb);
-  xf32_pass_b<DIN, DOUT>(rb);
-  xf32_exchange_bc<ROUNDS>(wave, lane, lds, rb, ra);
-  xf32_pass_c<DOUT>(wave, ra);
-  static_for<8>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    const uint32_t s = 8 * wave + t;  // wave-uniform
-    if (s < p.n_out) {
-      uint32_t qmask = out_io.valid;  // chunk exists and (with a mask) shard s is selected
-      if (p.out_mask) {
-        static_for<4>([&](auto Q) {
-          constexpr int q = decltype(Q)::value;
-          const uint64_t pat = p.pattern_per_block ? out_io.blk[q] : 0;
-          if (!p.out_mask[pat * p.out_mask_stride + s]) qmask &= ~(1u << q);
-        });
-      }
-      store_shard(p.out + s * p.out_shard_stride, out_io, qmask, ra[t]);
-    }
-  });
+  return qm;
 }
 
 // One 64-chunk tile per workgroup: 64 KiB LDS (ROUNDS = 2), two workgroups per CU.
@@ -333,9 +312,49 @@ __global__ __launch_bounds__(256, LB) void xform32_kernel(const XformParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   Regs8 ra;
   xf32_load_raw(p, tile_io(p, blockIdx.x, lane, p.in_block_stride), wave, ra);
-  xf32_body<DIN, DOUT, ROUNDS>(p, tile_io(p, blockIdx.x, lane, p.out_block_stride), wave, lane, lds, ra);
-}
+  // Store-mask words, fetched now so their latency hides under the data loads.  With
+  // one pattern for the batch the word is wave-uniform (scalar load).
+  uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  if (p.out_mask) {
+    if (!p.pattern_per_block) {
+      const uint64_t m = p.out_mask[0];
+      mask[0] = mask[1] = mask[2] = mask[3] = m;
+    } else {
+      const TileIO io = tile_io(p, blockIdx.x, lane, p.out_block_stride);
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        mask[q] = p.out_mask[io.blk[q]];
+      });
+    }
+  }
 
+  static_for<8>([&](auto T) {
+    swap_halves(ra[decltype(T)::value]);
+    dev::planes_from_raw(ra[decltype(T)::value]);
+  });
+  xf32_pass_a<DIN>(wave, ra);
+  Regs8 rb;
+  xf32_exchange_ab<ROUNDS>(wave, lane, lds, ra, rb);
+  xf32_pass_b<DIN, DOUT>(rb);
+  xf32_exchange_bc<ROUNDS>(wave, lane, lds, rb, ra);
+
+  // pass C only where some lane of the wave stores one of its 8 shards (a decode restores
+  // only the erased originals)
+  const TileIO out_io = tile_io(p, blockIdx.x, lane, p.out_block_stride);
+  uint32_t need = 0;
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = 8 * wave + t;
+    if (s < p.n_out && store_qmask(out_io, mask, s)) need = 1;
+  });
+  if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+  xf32_pass_c<DOUT>(wave, ra);
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = 8 * wave + t;  // wave-uniform
+    if (s < p.n_out) store_shard(p.out + s * p.out_shard_stride, out_io, store_qmask(out_io, mask, s), ra[t]);
+  });
+}
 
 // =====================================================================================
 // Generic kernels: one thread per (block, symbol position); the crate's algorithm with

@@ -17,8 +17,7 @@ struct XformParams {
   uint8_t* out;
   uint64_t out_block_stride;
   uint64_t out_shard_stride;
-  const uint8_t* out_mask;  // device: out_mask[pattern(b) * out_mask_stride + s] != 0 => store
-  uint64_t out_mask_stride;
+  const uint64_t* out_mask;    // device, one word per pattern: bit s set => store shard s
   uint32_t pattern_per_block;  // pattern(b) = pattern_per_block ? b : 0
   uint32_t n_in;               // shards 0..n_in-1 are loaded, the rest are zero
   uint32_t n_out;              // shards 0..n_out-1 may be stored
