@@ -38,7 +38,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--nblocks", type=int, default=4096, help="blocks per GPU")
+    ap.add_argument("--nblocks", type=int, default=4096, help="blocks per GPU (weak scaling)")
+    ap.add_argument("--stream-blocks", type=int, default=0,
+                    help="strong scaling: split one stream of this many blocks over the GPUs "
+                         "(BASELINE configs[4]: 65536)")
     ap.add_argument("--block-bytes", type=int, default=1 << 20)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--m", type=int, default=32)
@@ -69,7 +72,15 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    k, m, B, n = args.k, args.m, args.block_bytes, args.nblocks
+    from alpenglow_amd.shard import block_range, max_over_ranks
+
+    k, m, B = args.k, args.m, args.block_bytes
+    if args.stream_blocks:
+        first, last = block_range(rank, world, args.stream_blocks)
+        n = last - first
+    else:
+        n = args.nblocks
+        first = rank * n  # rank-disjoint blocks of one stream
     if B % k or (B // k) % 2:
         raise SystemExit("block bytes must split into k even-sized shards")
     S = B // k
@@ -83,7 +94,7 @@ def main():
 
     # codeword buffer: block b = k data shards then m coding shards (HBM-resident)
     cw = torch.empty((n, cw_stride), dtype=torch.uint8, device=dev)
-    seed_base = 0x5EED_A19E_0000_0000 + rank * n  # rank-disjoint blocks of one stream
+    seed_base = 0x5EED_A19E_0000_0000 + first
     rs.fill_splitmix(ctx, cw, n, k * S, cw_stride, seed_base)
     data_ptr, par_ptr = cw.data_ptr(), cw.data_ptr() + k * S
     opres = [0] * e + [1] * (k - e)
@@ -127,10 +138,7 @@ def main():
     enc_ms = sum(ev[s][0].elapsed_time(ev[s][1]) for s in range(args.steps)) / args.steps
     dec_ms = sum(ev[s][1].elapsed_time(ev[s][2]) for s in range(args.steps)) / args.steps
 
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
+    wall_max = max_over_ranks(wall, dist if world > 1 else None, dev)
     ms_per_step = wall_max * 1e3 / args.steps
 
     # full-size property check: zero the erased shards, reconstruct, compare with a fresh
@@ -148,7 +156,8 @@ def main():
 
     line = None
     if rank == 0:
-        processed = world * n * B  # each byte went through encode and reconstruct
+        # each byte went through encode and reconstruct
+        processed = (args.stream_blocks if args.stream_blocks else world * n) * B
         enc_bytes = n * B * (1 + m / k)
         dec_bytes = n * B * (1 + e / k)
         kern = {
@@ -169,12 +178,13 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.stream_blocks else "weak",
             "vs_baseline": None,
             "dtype": "u8 (GF(2^16) symbols, bitsliced u32 planes)",
             "data": "synthetic (splitmix64 random blocks, device-generated)",
-            "config": {"workload": f"{n} x {B >> 20} MiB blocks per GPU, {k}:{m} encode + "
-                                   f"reconstruct with {e}/{k} data shreds erased",
+            "config": {"workload": (f"{args.stream_blocks} x {B >> 20} MiB block stream over {world} GPU(s)"
+                                    if args.stream_blocks else f"{n} x {B >> 20} MiB blocks per GPU")
+                                   + f", {k}:{m} encode + reconstruct with {e}/{k} data shreds erased",
                        "blocks_per_gpu": n, "block_bytes": B, "shard_bytes": S,
                        "data_shreds": k, "coding_shreds": m, "erased_data_shreds": e,
                        "parallelism": f"blocks sharded over {world} GPU(s), no collective",

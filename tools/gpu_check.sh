@@ -22,7 +22,7 @@ timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > $OUT/bench.json 2> $OUT/benc
 rc=$?; echo "bench exit $rc"; cat $OUT/bench.json; tail -3 $OUT/bench.err; stop_on_fatal $rc
 [ "${SKIP_PROF:-0}" = 1 ] && exit 0
 timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $OUT/prof -o kt --output-format csv -- \
-  python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline --no-verify > $OUT/prof_bench.json 2> $OUT/prof.err
+  python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-verify > $OUT/prof_bench.json 2> $OUT/prof.err
 rc=$?; echo "rocprof exit $rc"; stop_on_fatal $rc
 find $OUT/prof -name "*stats*" | head
 exit 0
