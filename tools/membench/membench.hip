@@ -64,6 +64,47 @@ __global__ __launch_bounds__(256, 2) void copy_chunks_lin(const uint8_t* __restr
   }
 }
 
+// decode-shaped copy: every wave reads 8 shards, only waves < STORE_WAVES write theirs
+// (BAL: spread the same 16 stored shards over all 4 waves instead)
+template <int STORE_WAVES, bool BAL>
+__global__ __launch_bounds__(256, 2) void copy_decode_shape(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
+                                                            size_t S, size_t nblocks) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const size_t cps = S / 64;
+  const size_t col0 = (size_t)blockIdx.x * 64;
+  const size_t blk = col0 / cps, ch0 = col0 % cps;
+  if (blk >= nblocks) return;
+  uint4 v[8][4];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const uint4* s = (const uint4*)(in + blk * 32 * S + (size_t)(8 * wave + t) * S + ch0 * 64);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[t][q] = s[q * 64 + lane];
+  }
+  if (BAL) {
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      uint4* d = (uint4*)(out + blk * 32 * S + (size_t)(4 * wave + t) * S + ch0 * 64);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q * 64 + lane] = v[t][q] ^ v[t + 4][q];
+    }
+  } else if (wave < STORE_WAVES) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      uint4* d = (uint4*)(out + blk * 32 * S + (size_t)(8 * wave + t) * S + ch0 * 64);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) d[q * 64 + lane] = v[t][q];
+    }
+  } else {
+    uint4 acc = v[0][0];
+#pragma unroll
+    for (int t = 0; t < 8; ++t)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc ^= v[t][q];
+    if (acc.x == 0x12345678u) out[0] = 1;
+  }
+}
+
 // "half-coalesced": instruction q covers the lo (q<2) or hi (q>=2) 32-byte halves of 32
 // chunks; lanes 2i, 2i+1 take the two 16-byte pieces of chunk half i.  A lane ends up
 // with lo+hi bytes of symbols 0-15 (even lanes) or 16-31 (odd lanes) of 2 chunks.
@@ -109,7 +150,7 @@ int main(int argc, char** argv) {
   CK(hipEventCreate(&e1));
   const size_t cols = nblocks * (S / 64);
   const int reps = 10;
-  for (int variant = 0; variant < 4; ++variant) {
+  for (int variant = 0; variant < 6; ++variant) {
     for (int rep = 0; rep < 2; ++rep) {
       CK(hipEventRecord(e0));
       for (int r = 0; r < reps; ++r) {
@@ -120,18 +161,23 @@ int main(int argc, char** argv) {
           hipLaunchKernelGGL(copy_chunks<8>, dim3((cols + 63) / 64), dim3(256), 0, 0, a, b, S, nblocks);
         } else if (variant == 2) {
           hipLaunchKernelGGL(copy_chunks_lin<8>, dim3((cols + 63) / 64), dim3(256), 0, 0, a, b, S, nblocks);
-        } else {
+        } else if (variant == 3) {
           hipLaunchKernelGGL(copy_chunks_half<8>, dim3((cols + 63) / 64), dim3(256), 0, 0, a, b, S, nblocks);
+        } else if (variant == 4) {
+          hipLaunchKernelGGL((copy_decode_shape<2, false>), dim3((cols + 63) / 64), dim3(256), 0, 0, a, b, S, nblocks);
+        } else {
+          hipLaunchKernelGGL((copy_decode_shape<2, true>), dim3((cols + 63) / 64), dim3(256), 0, 0, a, b, S, nblocks);
         }
       }
       CK(hipEventRecord(e1));
       CK(hipEventSynchronize(e1));
       float ms;
       CK(hipEventElapsedTime(&ms, e0, e1));
+      const double moved = variant >= 4 ? 1.5 * bytes : 2.0 * bytes;
       if (rep == 1)
-        printf("%s: %.3f ms per copy of %.2f GiB, %.0f GB/s (read+write)\n",
-               variant == 0 ? "coalesced 16B/lane   " : variant == 1 ? "chunk 64B/lane strided" : variant == 2 ? "chunk tile lane-linear" : "chunk tile half-coalesced",
-               ms / reps, bytes / double(1ull << 30), 2.0 * bytes / (ms / reps * 1e-3) / 1e9);
+        printf("%s: %.3f ms per pass over %.2f GiB, %.0f GB/s (read+write)\n",
+               variant == 0 ? "coalesced 16B/lane   " : variant == 1 ? "chunk 64B/lane strided" : variant == 2 ? "chunk tile lane-linear" : variant == 3 ? "chunk tile half-coalesced" : variant == 4 ? "decode shape (2 storing waves)" : "decode shape (balanced stores)",
+               ms / reps, bytes / double(1ull << 30), moved / (ms / reps * 1e-3) / 1e9);
     }
   }
   return 0;
