@@ -66,9 +66,21 @@ int check_geometry(size_t k, size_t m, size_t S) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-// Single-chunk HighRate with a 32-point transform: k <= m, next_pow2(m) == 32.
-bool fast32_geometry(size_t k, size_t m, size_t S) {
-  return ag::use_high_rate(k, m) == 1 && next_pow2(m) == 32 && k <= 32 && S % 64 == 0;
+// Single-chunk HighRate geometries served by the bitsliced N-point transform kernel:
+// k <= N, next_pow2(m) == N, N in {32, 64}, whole 64-byte chunks.  Returns N or 0.
+// (HighRate with a single chunk implies next_pow2(k) == N and k <= m.)
+unsigned xform_points(size_t k, size_t m, size_t S) {
+  if (S == 0 || S % 64 || ag::use_high_rate(k, m) != 1) return 0;
+  const size_t n = next_pow2(m);
+  return (n == 32 || n == 64) && k <= n ? static_cast<unsigned>(n) : 0;
+}
+
+// Multi-chunk HighRate encode with a small recovery chunk (encode_mc kernel): returns the
+// chunk next_pow2(m) in {1, 2, 4} when k > chunk, k <= 64, whole 64-byte chunks; else 0.
+unsigned mc_chunk(size_t k, size_t m, size_t S) {
+  if (S == 0 || S % 64 || ag::use_high_rate(k, m) != 1 || k > 64) return 0;
+  const size_t c = next_pow2(m);
+  return c <= 4 && k > c ? static_cast<unsigned>(c) : 0;
 }
 
 }  // namespace
@@ -138,7 +150,9 @@ constexpr size_t kGenericScratchBytes = size_t{512} << 20;
 int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
                   size_t ostride, uint8_t* rec, size_t rstride) {
   if (nblocks == 0) return AG_RS_OK;
-  if (fast32_geometry(k, m, S) && aligned16(orig) && aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0) {
+  const unsigned npts = xform_points(k, m, S);
+  const unsigned mc = mc_chunk(k, m, S);
+  if ((npts || mc) && aligned16(orig) && aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0) {
     ag::XformParams p{};
     p.in = orig;
     p.in_block_stride = ostride;
@@ -150,7 +164,12 @@ int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
     p.n_out = static_cast<uint32_t>(m);
     p.chunks_per_shard = static_cast<uint32_t>(S / 64);
     p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
-    return ag::launch_xform(ag::XformKind::kEncode32, p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+    hipError_t e;
+    if (npts)
+      e = ag::launch_xform(npts == 32 ? ag::XformKind::kEncode32 : ag::XformKind::kEncode64, p, c->stream);
+    else
+      e = ag::launch_encode_mc(mc, p, c->stream);
+    return e == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
   }
   int st = c->ensure_tables();
   if (st) return st;
@@ -190,9 +209,12 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
                   int mode) {
   if (nblocks == 0) return AG_RS_OK;
   const int hr = ag::use_high_rate(k, m);
-  // classify patterns: 0 = nothing to restore, 1 = bitsliced (full recovery set), 2 = generic
+  // classify patterns: 0 = nothing to restore, 1 = bitsliced (full recovery set), 2 = generic.
+  // The transform inverts the encoder only when all N recovery points exist (m == N):
+  // with m < N the points m..N-1 were never stored.
   std::vector<uint8_t> cls(npat);
-  const bool fast_geo = mode == AG_RS_DECODE_ANY_K && fast32_geometry(k, m, S) && aligned16(orig) &&
+  const unsigned npts = xform_points(k, m, S);
+  const bool fast_geo = mode == AG_RS_DECODE_ANY_K && npts != 0 && m == npts && aligned16(orig) &&
                         aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0;
   bool any_fast = false, any_generic = false;
   for (size_t p = 0; p < npat; ++p) {
@@ -238,7 +260,8 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     p.n_out = static_cast<uint32_t>(k);
     p.chunks_per_shard = static_cast<uint32_t>(S / 64);
     p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
-    if (ag::launch_xform(ag::XformKind::kDecode32, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    const auto kind = npts == 32 ? ag::XformKind::kDecode32 : ag::XformKind::kDecode64;
+    if (ag::launch_xform(kind, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   }
   if (!any_generic) return AG_RS_OK;
 
@@ -407,7 +430,7 @@ int ag_rs_use_high_rate(size_t k, size_t m) {
   return hr < 0 ? -AG_RS_ERR_UNSUPPORTED_SHARD_COUNT : hr;
 }
 
-int ag_rs_has_fast_path(size_t k, size_t m, size_t S) { return fast32_geometry(k, m, S) ? 1 : 0; }
+int ag_rs_has_fast_path(size_t k, size_t m, size_t S) { return xform_points(k, m, S) || mc_chunk(k, m, S) ? 1 : 0; }
 
 int ag_rs_encode_batch(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
                        size_t ostride, uint8_t* rec, size_t rstride, int memory) {

@@ -5,8 +5,9 @@
 // :211-231 re-encode).  Arithmetic: GF(2^16) Leopard additive FFT.
 //
 // Kernels
-//   xform32_kernel    bitsliced IFFT-32 + FFT-32 over one 32-point block; HighRate encode
-//                     (k <= m = 32) and decode-from-a-full-recovery-set.  HBM-bound.
+//   xform_kernel<NW>  bitsliced IFFT-N + FFT-N over one N = 32 or 64 point block; HighRate
+//                     encode (k <= m, next_pow2(m) = N) and decode-from-a-full-recovery-set
+//                     (m = N).  HBM-bound.
 //   generic_*         table-driven crate algorithm for every geometry (correctness path:
 //                     multi-chunk HighRate, LowRate, exact decode with any erasures).
 //   locator_kernel    erasure-locator logs (crate eval_poly: FWHT over 65536 in LDS).
@@ -22,87 +23,116 @@ namespace {
 using dev::static_for;
 
 // =====================================================================================
-// xform32: 4 waves x 64 lanes; lane = one 64-byte column (32 symbols) of one block,
-// each lane owns 8 of the 32 shards in each of three passes:
-//   pass A  (wave w: shards 8w+t)      IFFT layers dist 1, 2, 4      (skew delta DIN)
-//   pass B  (wave w: shards w+4t)      IFFT dist 8, 16; FFT dist 16, 8 (DIN / DOUT)
-//   pass C  (wave w: shards 8w+t)      FFT layers dist 4, 2, 1       (skew delta DOUT)
-// Shards change owner between passes through LDS (2 rounds x 64 KiB per exchange).
+// xform<NW>: N = 8 * NW point transform (NW = 4 -> 32, NW = 8 -> 64); NW waves x 64
+// lanes; lane = one 64-byte column (32 symbols) of one block, each lane owns 8 of the N
+// shards in each of three passes:
+//   pass A  (wave w: shards 8w+t)       IFFT layers dist 1, 2, 4        (skew delta DIN)
+//   pass B  (wave w: shards w+NW*t)     IFFT dist 8 .. N/2; FFT N/2 .. 8 (DIN / DOUT)
+//   pass C  (wave w: shards 8w+t)       FFT layers dist 4, 2, 1         (skew delta DOUT)
+// Shards change owner between passes through LDS (2 rounds per exchange: 64 KiB per
+// round for N = 32, 128 KiB for N = 64).
 // Skew index of a layer of distance d on the group starting at g: g + d + delta - 1.
+// In pass B the group start depends only on shard bits >= 4, i.e. on the slot index, so
+// that code is wave-independent; passes A and C branch once per butterfly on the
+// (scalar) wave id.
 // =====================================================================================
 
 constexpr int kXfLanes = 64;
-constexpr int kXfLdsSlots = 16;  // 16 shards x 16 planes x 64 lanes x 4 B = 64 KiB
 
 using Regs8 = uint32_t[8][16];
 
 // butterfly whose skew index is BASE + 8 * wave (wave-uniform, runtime)
-template <int BASE, bool INV>
+template <int S, bool INV>
+__device__ __forceinline__ void bfly(uint32_t* x, uint32_t* y) {
+  if constexpr (INV) dev::ifft_bfly<S>(x, y); else dev::fft_bfly<S>(x, y);
+}
+template <int BASE, bool INV, int NW>
 __device__ __forceinline__ void bfly_w(int wave, uint32_t* x, uint32_t* y) {
 #ifdef AG_XF_DIAG_ONE_ROLE
   wave = 0;  // diagnostic build only: every wave runs role 0's code (wrong output)
 #endif
-  switch (wave) {
-    case 0: if constexpr (INV) dev::ifft_bfly<BASE>(x, y); else dev::fft_bfly<BASE>(x, y); break;
-    case 1: if constexpr (INV) dev::ifft_bfly<BASE + 8>(x, y); else dev::fft_bfly<BASE + 8>(x, y); break;
-    case 2: if constexpr (INV) dev::ifft_bfly<BASE + 16>(x, y); else dev::fft_bfly<BASE + 16>(x, y); break;
-    default: if constexpr (INV) dev::ifft_bfly<BASE + 24>(x, y); else dev::fft_bfly<BASE + 24>(x, y); break;
+  if constexpr (NW == 4) {
+    switch (wave) {
+      case 0: bfly<BASE, INV>(x, y); break;
+      case 1: bfly<BASE + 8, INV>(x, y); break;
+      case 2: bfly<BASE + 16, INV>(x, y); break;
+      default: bfly<BASE + 24, INV>(x, y); break;
+    }
+  } else {
+    switch (wave) {
+      case 0: bfly<BASE, INV>(x, y); break;
+      case 1: bfly<BASE + 8, INV>(x, y); break;
+      case 2: bfly<BASE + 16, INV>(x, y); break;
+      case 3: bfly<BASE + 24, INV>(x, y); break;
+      case 4: bfly<BASE + 32, INV>(x, y); break;
+      case 5: bfly<BASE + 40, INV>(x, y); break;
+      case 6: bfly<BASE + 48, INV>(x, y); break;
+      default: bfly<BASE + 56, INV>(x, y); break;
+    }
   }
 }
-template <int DIN>
-__device__ __forceinline__ void xf32_pass_a(int wave, Regs8& r) {
+template <int NW, int DIN>
+__device__ __forceinline__ void xf_pass_a(int wave, Regs8& r) {
   static_for<4>([&](auto I) {  // dist 1
     constexpr int t = 2 * decltype(I)::value;
-    bfly_w<t + 1 + DIN - 1, true>(wave, r[t], r[t + 1]);
+    bfly_w<t + 1 + DIN - 1, true, NW>(wave, r[t], r[t + 1]);
   });
   static_for<4>([&](auto I) {  // dist 2
     constexpr int g = 4 * (decltype(I)::value >> 1);
     constexpr int u = g + (decltype(I)::value & 1);
-    bfly_w<g + 2 + DIN - 1, true>(wave, r[u], r[u + 2]);
+    bfly_w<g + 2 + DIN - 1, true, NW>(wave, r[u], r[u + 2]);
   });
   static_for<4>([&](auto I) {  // dist 4
     constexpr int u = decltype(I)::value;
-    bfly_w<4 + DIN - 1, true>(wave, r[u], r[u + 4]);
+    bfly_w<4 + DIN - 1, true, NW>(wave, r[u], r[u + 4]);
   });
 }
 
-// Slot t holds shard w + 4t: bit 2 <- t0, bit 3 <- t1, bit 4 <- t2.  The layers touched
-// here have group starts that depend only on bit 4, so the code is wave-independent.
-template <int DIN, int DOUT>
-__device__ __forceinline__ void xf32_pass_b(Regs8& r) {
-  constexpr int kPairs8[4] = {0, 1, 4, 5};
-  static_for<4>([&](auto I) {  // IFFT dist 8 (bit 3)
-    constexpr int t = kPairs8[decltype(I)::value];
-    dev::ifft_bfly<16 * (t >> 2) + 8 + DIN - 1>(r[t], r[t + 2]);
+// Pass B: slot t holds shard w + NW*t.  Layer on shard bit sb (dist 2^sb, sb >= 3) pairs
+// slots t, t + 2^tb with tb = sb - log2(NW); group start (NW*t) & ~(2d - 1).
+template <int NW>
+struct PassB {
+  static constexpr int kLogNw = NW == 4 ? 2 : 3;
+  static constexpr int kLayers = NW == 4 ? 2 : 3;  // shard bits 3 .. 3 + kLayers - 1
+  template <int L, int I>
+  struct Pair {
+    static constexpr int sb = 3 + L, tb = sb - kLogNw, d = 1 << sb;
+    static constexpr int t = ((I >> tb) << (tb + 1)) | (I & ((1 << tb) - 1));
+    static constexpr int u = t + (1 << tb);
+    static constexpr int g = (NW * t) & ~(2 * d - 1);
+  };
+};
+template <int NW, int DIN, int DOUT>
+__device__ __forceinline__ void xf_pass_b(Regs8& r) {
+  constexpr int NL = PassB<NW>::kLayers;
+  static_for<NL>([&](auto L) {  // IFFT, ascending distance
+    static_for<4>([&](auto I) {
+      using P = typename PassB<NW>::template Pair<decltype(L)::value, decltype(I)::value>;
+      dev::ifft_bfly<P::g + P::d + DIN - 1>(r[P::t], r[P::u]);
+    });
   });
-  static_for<4>([&](auto I) {  // IFFT dist 16 (bit 4)
-    constexpr int t = decltype(I)::value;
-    dev::ifft_bfly<16 + DIN - 1>(r[t], r[t + 4]);
-  });
-  static_for<4>([&](auto I) {  // FFT dist 16
-    constexpr int t = decltype(I)::value;
-    dev::fft_bfly<16 + DOUT - 1>(r[t], r[t + 4]);
-  });
-  static_for<4>([&](auto I) {  // FFT dist 8
-    constexpr int t = kPairs8[decltype(I)::value];
-    dev::fft_bfly<16 * (t >> 2) + 8 + DOUT - 1>(r[t], r[t + 2]);
+  static_for<NL>([&](auto L) {  // FFT, descending distance
+    static_for<4>([&](auto I) {
+      using P = typename PassB<NW>::template Pair<NL - 1 - decltype(L)::value, decltype(I)::value>;
+      dev::fft_bfly<P::g + P::d + DOUT - 1>(r[P::t], r[P::u]);
+    });
   });
 }
 
-template <int DOUT>
-__device__ __forceinline__ void xf32_pass_c(int wave, Regs8& r) {
+template <int NW, int DOUT>
+__device__ __forceinline__ void xf_pass_c(int wave, Regs8& r) {
   static_for<4>([&](auto I) {  // dist 4
     constexpr int u = decltype(I)::value;
-    bfly_w<4 + DOUT - 1, false>(wave, r[u], r[u + 4]);
+    bfly_w<4 + DOUT - 1, false, NW>(wave, r[u], r[u + 4]);
   });
   static_for<4>([&](auto I) {  // dist 2
     constexpr int g = 4 * (decltype(I)::value >> 1);
     constexpr int u = g + (decltype(I)::value & 1);
-    bfly_w<g + 2 + DOUT - 1, false>(wave, r[u], r[u + 2]);
+    bfly_w<g + 2 + DOUT - 1, false, NW>(wave, r[u], r[u + 2]);
   });
   static_for<4>([&](auto I) {  // dist 1
     constexpr int t = 2 * decltype(I)::value;
-    bfly_w<t + 1 + DOUT - 1, false>(wave, r[t], r[t + 1]);
+    bfly_w<t + 1 + DOUT - 1, false, NW>(wave, r[t], r[t + 1]);
   });
 }
 
@@ -164,7 +194,7 @@ __device__ __forceinline__ void swap_halves(uint32_t* v) {
 }
 
 // Raw 16-byte pieces of this wave's pass-A shards 8*wave + t (before swap / transpose).
-__device__ __forceinline__ void xf32_load_raw(const XformParams& p, const TileIO& io, int wave, Regs8& raw) {
+__device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& io, int wave, Regs8& raw) {
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = 8 * wave + t;  // wave-uniform condition
@@ -202,95 +232,59 @@ __device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const Ti
   });
 }
 
-// LDS exchange between passes.  Pass A/C slot t of wave w holds shard 8w+t; pass B slot
-// t' of wave w' holds shard w'+4t' (so A-slot t of wave w <-> B-slot 2w+(t>>2) of wave t&3).
-// ROUNDS = 2: each round moves 4 slots per wave through 64 KiB.  (ROUNDS = 4, 32 KiB per
-// round with wave-dependent slot pairing, is kept for experiments: it spills, because the
-// slot indices then depend on the runtime wave id.)
-template <int ROUNDS>
-__device__ __forceinline__ void xf32_exchange_ab(int wave, int lane, uint4* lds, Regs8& ra, Regs8& rb) {
-  if constexpr (ROUNDS == 2) {
-    static_for<2>([&](auto Rho) {
-      constexpr int rho = decltype(Rho)::value;
-      static_for<4>([&](auto U) {
-        constexpr int u = decltype(U)::value;
-        lds_put(lds, 4 * wave + u, lane, ra[4 * rho + u]);
-      });
-      __syncthreads();
+// LDS exchange between passes (2 rounds, 4 A-slots per wave per round).
+//   NW = 4: A-slot t of wave w (shard 8w+t) <-> B-slot 2w+(t>>2) of wave t&3
+//   NW = 8: A-slot t of wave w (shard 8w+t) <-> B-slot w of wave t
+template <int NW>
+__device__ __forceinline__ void xf_exchange_ab(int wave, int lane, uint4* lds, Regs8& ra, Regs8& rb) {
+  static_for<2>([&](auto Rho) {
+    constexpr int rho = decltype(Rho)::value;
+    static_for<4>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      lds_put(lds, 4 * wave + u, lane, ra[4 * rho + u]);
+    });
+    __syncthreads();
+    if constexpr (NW == 4) {
       static_for<4>([&](auto W2) {
         constexpr int w2 = decltype(W2)::value;
         lds_get(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
       });
-      __syncthreads();
-    });
-  } else {
-    static_for<4>([&](auto Rho) {
-      constexpr int rho = decltype(Rho)::value;
-      // writer w sends A-slots t0, t0+4 with t0 = (w+rho)&3 to wave t0
-      static_for<4>([&](auto Wc) {
-        constexpr int w = decltype(Wc)::value;
-        if (wave == w) {
-          constexpr int t0 = (w + rho) & 3;
-          lds_put(lds, 2 * w + 0, lane, ra[t0]);
-          lds_put(lds, 2 * w + 1, lane, ra[t0 + 4]);
-        }
-      });
-      __syncthreads();
-      // reader w' receives from writer w = (w'-rho)&3 into B-slots 2w, 2w+1
-      static_for<4>([&](auto Wc) {
-        constexpr int wr = decltype(Wc)::value;
-        if (wave == wr) {
-          constexpr int w = (wr - rho) & 3;
-          lds_get(lds, 2 * w + 0, lane, rb[2 * w + 0]);
-          lds_get(lds, 2 * w + 1, lane, rb[2 * w + 1]);
-        }
-      });
-      __syncthreads();
-    });
-  }
+    } else {
+      if ((wave >> 2) == rho) {
+        static_for<8>([&](auto W2) {
+          constexpr int w2 = decltype(W2)::value;
+          lds_get(lds, 4 * w2 + (wave & 3), lane, rb[w2]);
+        });
+      }
+    }
+    __syncthreads();
+  });
 }
 
-template <int ROUNDS>
-__device__ __forceinline__ void xf32_exchange_bc(int wave, int lane, uint4* lds, Regs8& rb, Regs8& ra) {
-  if constexpr (ROUNDS == 2) {
-    static_for<2>([&](auto Rho) {
-      constexpr int rho = decltype(Rho)::value;
+template <int NW>
+__device__ __forceinline__ void xf_exchange_bc(int wave, int lane, uint4* lds, Regs8& rb, Regs8& ra) {
+  static_for<2>([&](auto Rho) {
+    constexpr int rho = decltype(Rho)::value;
+    if constexpr (NW == 4) {
       static_for<4>([&](auto W2) {
         constexpr int w2 = decltype(W2)::value;
         lds_put(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
       });
-      __syncthreads();
-      static_for<4>([&](auto U) {
-        constexpr int u = decltype(U)::value;
-        lds_get(lds, 4 * wave + u, lane, ra[4 * rho + u]);
-      });
-      __syncthreads();
+    } else {
+      if ((wave >> 2) == rho) {
+        static_for<8>([&](auto W2) {
+          constexpr int w2 = decltype(W2)::value;
+          lds_put(lds, 4 * w2 + (wave & 3), lane, rb[w2]);
+        });
+      }
+    }
+    __syncthreads();
+    static_for<4>([&](auto U) {
+      constexpr int u = decltype(U)::value;
+      lds_get(lds, 4 * wave + u, lane, ra[4 * rho + u]);
     });
-  } else {
-    static_for<4>([&](auto Rho) {
-      constexpr int rho = decltype(Rho)::value;
-      // writer w' sends B-slots 2w, 2w+1 to pass-C wave w = (w'-rho)&3
-      static_for<4>([&](auto Wc) {
-        constexpr int wp = decltype(Wc)::value;
-        if (wave == wp) {
-          constexpr int w = (wp - rho) & 3;
-          lds_put(lds, 2 * wp + 0, lane, rb[2 * w + 0]);
-          lds_put(lds, 2 * wp + 1, lane, rb[2 * w + 1]);
-        }
-      });
-      __syncthreads();
-      // reader w receives from w' = (w+rho)&3 into C-slots w', w'+4
-      static_for<4>([&](auto Wc) {
-        constexpr int w = decltype(Wc)::value;
-        if (wave == w) {
-          constexpr int wp = (w + rho) & 3;
-          lds_get(lds, 2 * wp + 0, lane, ra[wp]);
-          lds_get(lds, 2 * wp + 1, lane, ra[wp + 4]);
-        }
-      });
-      __syncthreads();
-    });
-  }
+    __syncthreads();
+  });
 }
 
 // Store predicate of this wave's shard s for the four chunk slices of the tile: chunk
@@ -304,14 +298,15 @@ __device__ __forceinline__ uint32_t store_qmask(const TileIO& io, const uint64_t
   return qm;
 }
 
-// One 64-chunk tile per workgroup: 64 KiB LDS (ROUNDS = 2), two workgroups per CU.
-template <int DIN, int DOUT, int ROUNDS, int LB>
-__global__ __launch_bounds__(256, LB) void xform32_kernel(const XformParams p) {
-  __shared__ uint4 lds[(ROUNDS == 2 ? 16 : 8) * 4 * kXfLanes];
+// One 64-chunk tile per workgroup of NW waves.  N = 32: 64 KiB LDS, two workgroups per
+// CU; N = 64: 128 KiB LDS, one workgroup (8 waves) per CU.
+template <int NW, int DIN, int DOUT>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const XformParams p) {
+  __shared__ uint4 lds[4 * NW * 4 * kXfLanes];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   Regs8 ra;
-  xf32_load_raw(p, tile_io(p, blockIdx.x, lane, p.in_block_stride), wave, ra);
+  xf_load_raw(p, tile_io(p, blockIdx.x, lane, p.in_block_stride), wave, ra);
   // Store-mask words, fetched now so their latency hides under the data loads.  With
   // one pattern for the batch the word is wave-uniform (scalar load).
   uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
@@ -332,11 +327,11 @@ __global__ __launch_bounds__(256, LB) void xform32_kernel(const XformParams p) {
     swap_halves(ra[decltype(T)::value]);
     dev::planes_from_raw(ra[decltype(T)::value]);
   });
-  xf32_pass_a<DIN>(wave, ra);
+  xf_pass_a<NW, DIN>(wave, ra);
   Regs8 rb;
-  xf32_exchange_ab<ROUNDS>(wave, lane, lds, ra, rb);
-  xf32_pass_b<DIN, DOUT>(rb);
-  xf32_exchange_bc<ROUNDS>(wave, lane, lds, rb, ra);
+  xf_exchange_ab<NW>(wave, lane, lds, ra, rb);
+  xf_pass_b<NW, DIN, DOUT>(rb);
+  xf_exchange_bc<NW>(wave, lane, lds, rb, ra);
 
   // pass C only where some lane of the wave stores one of its 8 shards (a decode restores
   // only the erased originals)
@@ -348,11 +343,96 @@ __global__ __launch_bounds__(256, LB) void xform32_kernel(const XformParams p) {
     if (s < p.n_out && store_qmask(out_io, mask, s)) need = 1;
   });
   if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
-  xf32_pass_c<DOUT>(wave, ra);
+  xf_pass_c<NW, DOUT>(wave, ra);
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = 8 * wave + t;  // wave-uniform
     if (s < p.n_out) store_shard(p.out + s * p.out_shard_stride, out_io, store_qmask(out_io, mask, s), ra[t]);
+  });
+}
+
+// =====================================================================================
+// encode_mc<C>: multi-chunk HighRate encode for small recovery sets (chunk C = next_pow2(m)
+// in {1, 2, 4}, k <= kMcMaxK).  One wave per 64-column tile, no LDS: the wave streams the
+// k/C original chunks (next chunk's loads issued before this chunk's math), runs each
+// chunk's in-lane IFFT_C (skew delta C*(c+1)), XOR-accumulates, and ends with FFT_C (delta
+// 0) on the accumulator -- the crate's HighRate encoder.
+// =====================================================================================
+constexpr int kMcMaxK = 64;
+
+template <int C>
+constexpr int ilog2c() { return C <= 1 ? 0 : 1 + ilog2c<C / 2>(); }
+
+template <int C, int DELTA, bool INV>
+__device__ __forceinline__ void xform_lane(uint32_t (&r)[C][16]) {
+  constexpr int LC = ilog2c<C>();
+  static_for<LC>([&](auto Lx) {
+    constexpr int L = INV ? decltype(Lx)::value : LC - 1 - decltype(Lx)::value;  // IFFT ascending
+    constexpr int d = 1 << L;
+    static_for<C / 2>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      constexpr int g = (i / d) * 2 * d;
+      constexpr int u = g + i % d;
+      bfly<g + d + DELTA - 1, INV>(r[u], r[u + d]);
+    });
+  });
+}
+
+template <int C>
+__device__ __forceinline__ void mc_load(const XformParams& p, const TileIO& io, uint32_t s0, uint32_t (&raw)[C][16]) {
+  static_for<C>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    if (s0 + t < p.n_in) {  // wave-uniform
+      const uint8_t* base = p.in + (s0 + t) * p.in_shard_stride;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        raw[t][4 * q] = x.x;
+        raw[t][4 * q + 1] = x.y;
+        raw[t][4 * q + 2] = x.z;
+        raw[t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { raw[t][decltype(P)::value] = 0; });
+    }
+  });
+}
+
+template <int C>
+__global__ __launch_bounds__(256, 2) void encode_mc_kernel(const XformParams p) {
+  constexpr int NCMAX = kMcMaxK / C;
+  const int lane = threadIdx.x & 63;
+  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (tile * kXfLanes >= p.total_columns) return;  // whole wave
+  const TileIO io = tile_io(p, tile, lane, p.in_block_stride);
+  const uint32_t nc = (p.n_in + C - 1) / C;
+  uint32_t acc[C][16];
+  uint32_t raw[2][C][16];
+  mc_load<C>(p, io, 0, raw[0]);
+  static_for<NCMAX>([&](auto Cc) {
+    constexpr int c = decltype(Cc)::value;
+    if (c < nc) {
+      if (c + 1 < nc) mc_load<C>(p, io, (c + 1) * C, raw[(c + 1) & 1]);
+      auto& cur = raw[c & 1];
+      static_for<C>([&](auto T) {
+        swap_halves(cur[decltype(T)::value]);
+        dev::planes_from_raw(cur[decltype(T)::value]);
+      });
+      xform_lane<C, C * (c + 1), true>(cur);
+      static_for<C>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        static_for<16>([&](auto P) {
+          constexpr int q = decltype(P)::value;
+          if constexpr (c == 0) acc[t][q] = cur[t][q]; else acc[t][q] ^= cur[t][q];
+        });
+      });
+    }
+  });
+  xform_lane<C, 0, false>(acc);
+  const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
+  static_for<C>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    if (t < p.n_out) store_shard(p.out + t * p.out_shard_stride, out_io, out_io.valid, acc[t]);
   });
 }
 
@@ -557,20 +637,41 @@ __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* dst, uint64
 }  // namespace
 
 // ---- launchers ----------------------------------------------------------------------
-bool xform_supported(unsigned n) { return n == 32; }
+bool xform_supported(unsigned n) { return n == 32 || n == 64; }
+
+hipError_t launch_encode_mc(unsigned chunk, const XformParams& p, hipStream_t stream) {
+  if (p.total_columns == 0) return hipSuccess;
+  if (p.n_in > static_cast<uint32_t>(kMcMaxK) || p.n_out > chunk) return hipErrorInvalidValue;
+  const uint64_t tiles = (p.total_columns + kXfLanes - 1) / kXfLanes;
+  const uint64_t groups = (tiles + 3) / 4;
+  if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<unsigned>(groups));
+  switch (chunk) {
+    case 1: hipLaunchKernelGGL((encode_mc_kernel<1>), grid, dim3(256), 0, stream, p); break;
+    case 2: hipLaunchKernelGGL((encode_mc_kernel<2>), grid, dim3(256), 0, stream, p); break;
+    case 4: hipLaunchKernelGGL((encode_mc_kernel<4>), grid, dim3(256), 0, stream, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream) {
   if (p.total_columns == 0) return hipSuccess;
   const uint64_t groups = (p.total_columns + kXfLanes - 1) / kXfLanes;
   if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  const dim3 block(256);
   const dim3 grid(static_cast<unsigned>(groups));
   switch (kind) {
     case XformKind::kEncode32:
-      hipLaunchKernelGGL((xform32_kernel<32, 0, 2, 2>), grid, block, 0, stream, p);
+      hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);
       break;
     case XformKind::kDecode32:
-      hipLaunchKernelGGL((xform32_kernel<0, 32, 2, 2>), grid, block, 0, stream, p);
+      hipLaunchKernelGGL((xform_kernel<4, 0, 32>), grid, dim3(256), 0, stream, p);
+      break;
+    case XformKind::kEncode64:
+      hipLaunchKernelGGL((xform_kernel<8, 64, 0>), grid, dim3(512), 0, stream, p);
+      break;
+    case XformKind::kDecode64:
+      hipLaunchKernelGGL((xform_kernel<8, 0, 64>), grid, dim3(512), 0, stream, p);
       break;
     default:
       return hipErrorInvalidValue;

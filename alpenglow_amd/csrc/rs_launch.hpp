@@ -30,6 +30,9 @@ enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };
 hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream);
 // True when the bitsliced transform exists for this transform size.
 bool xform_supported(unsigned n);
+// Multi-chunk HighRate encode with chunk = next_pow2(m) in {1, 2, 4} and k <= 64:
+// in = originals (n_in = k), out = recovery (n_out = m).  out_mask unused.
+hipError_t launch_encode_mc(unsigned chunk, const XformParams& p, hipStream_t stream);
 
 // Generic (any geometry) table-driven kernels.  One thread per (block, symbol).
 struct GfDeviceTables {

@@ -45,7 +45,8 @@ def parse():
     ap.add_argument("--block-bytes", type=int, default=1 << 20)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--m", type=int, default=32)
-    ap.add_argument("--erase", type=int, default=16, help="data shards erased per block")
+    ap.add_argument("--erase", type=int, default=-1,
+                    help="data shards erased per block (default: k/2, at most m)")
     ap.add_argument("--only", choices=["both", "encode", "decode"], default="both",
                     help="profiling aid: time only one of the two kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -84,7 +85,7 @@ def main():
     if B % k or (B // k) % 2:
         raise SystemExit("block bytes must split into k even-sized shards")
     S = B // k
-    e = args.erase
+    e = args.erase if args.erase >= 0 else min(k // 2, m)
     cw_stride = (k + m) * S
 
     ctx = rs.Context(local)

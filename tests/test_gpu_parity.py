@@ -111,7 +111,29 @@ def test_encode_into_codeword_buffer(ctx, dev):
     assert np.array_equal(host[:, k:], ro_c.encode_blocks(host[:, :k], m))
 
 
-@pytest.mark.parametrize("k,m,S", [(16, 4, 1024), (64, 64, 256), (32, 64, 1024), (32, 33, 1024), (32, 32, 1000)])
+@pytest.mark.parametrize("k,m", [(64, 64), (33, 64), (40, 41), (48, 60)])
+def test_fast_encode_64_point(ctx, dev, k, m):
+    """Single-chunk HighRate with next_pow2(m) = 64: the 8-wave 64-point transform."""
+    S = 4096 if k == 64 else 192
+    assert rs.has_fast_path(k, m, S)
+    n = 5
+    blocks = np.stack([np.frombuffer(o.block_bytes(300 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    got = gpu_encode(ctx, dev, blocks, m)
+    want = ro_c.encode_blocks(blocks, m, threads=8)
+    assert np.array_equal(got, want)
+
+
+@pytest.mark.parametrize("k,m,S", [(16, 4, 4096), (16, 3, 640), (13, 4, 128), (64, 4, 1024), (5, 2, 64),
+                                   (9, 1, 192), (17, 2, 4096)])
+def test_multichunk_small_encode(ctx, dev, k, m, S):
+    """HighRate with next_pow2(m) <= 4 < k (BASELINE C4 16:4): the streaming encode_mc kernel."""
+    assert rs.has_fast_path(k, m, S)
+    n = 9
+    blocks = np.stack([np.frombuffer(o.block_bytes(600 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    assert np.array_equal(gpu_encode(ctx, dev, blocks, m), ro_c.encode_blocks(blocks, m, threads=8))
+
+
+@pytest.mark.parametrize("k,m,S", [(16, 4, 1000), (64, 64, 200), (32, 64, 1024), (32, 33, 1024), (32, 32, 1000)])
 def test_generic_encode_multi_block(ctx, dev, k, m, S):
     blocks = np.stack([np.frombuffer(o.block_bytes(7 + b, k * S), np.uint8).reshape(k, S) for b in range(3)])
     assert np.array_equal(gpu_encode(ctx, dev, blocks, m), ro_c.encode_blocks(blocks, m))
@@ -156,6 +178,35 @@ def test_fast_decode_from_recovery_set(ctx, dev, erased):
     op = [0 if i in erased else 1 for i in range(k)]
     got = gpu_decode(ctx, dev, damaged, rec, op, [1] * m, rs.DECODE_ANY_K)
     assert np.array_equal(got, blocks)
+
+
+@pytest.mark.parametrize("erased", [list(range(32)), list(range(64)), [0, 5, 63]])
+def test_fast_decode_64_point(ctx, dev, erased):
+    """64:64 with the full recovery set: 64-point transform restores the erased data."""
+    k, m, S, n = 64, 64, 2048, 7
+    blocks = np.stack([np.frombuffer(o.block_bytes(400 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    damaged = blocks.copy()
+    damaged[:, erased] = 0x33
+    op = [0 if i in erased else 1 for i in range(k)]
+    got = gpu_decode(ctx, dev, damaged, rec, op, [1] * m, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
+
+
+@pytest.mark.parametrize("k,m", [(20, 30), (17, 24), (40, 50)])
+def test_any_k_decode_partial_recovery_block(ctx, dev, k, m):
+    """m < next_pow2(m): all recovery shards present is NOT a full transform set (points
+    m..N-1 were never stored); the decode must still restore the originals exactly."""
+    S, n = 256, 4
+    blocks = np.stack([np.frombuffer(o.block_bytes(500 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    erased = list(range(0, k, 3))
+    damaged = blocks.copy()
+    damaged[:, erased] = 0
+    op = [0 if i in erased else 1 for i in range(k)]
+    for mode in (rs.DECODE_ANY_K, rs.DECODE_EXACT):
+        got = gpu_decode(ctx, dev, damaged, rec, op, [1] * m, mode)
+        assert np.array_equal(got, blocks), mode
 
 
 def test_decode_per_block_patterns(ctx, dev):

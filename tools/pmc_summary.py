@@ -22,8 +22,8 @@ vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(args.dir, "p*", "pmc_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        short = "encode" if "xform32_kernel<32, 0" in name else \
-                "reconstruct" if "xform32_kernel<0, 32" in name else \
+        short = "encode" if "xform_kernel<4, 32, 0" in name else \
+                "reconstruct" if "xform_kernel<4, 0, 32" in name else \
                 name.split("(")[0][-40:]
         vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 summary = {}
