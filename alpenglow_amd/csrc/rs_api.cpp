@@ -93,9 +93,12 @@ struct ag_rs_ctx {
   DevBuf d_exp, d_log, d_skew, d_log_walsh;
   DevBuf scratch;                         // generic-kernel work rows
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
+  DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
   DevBuf stage_in, stage_out;             // host-memory calls
   DevBuf one_in, one_out;                 // crate-API single codeword
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
+  std::vector<uint64_t> xmask_host;       // last general-decode masks (d_xmask), W = xmask_w
+  size_t xmask_w = 0;
 
   int enter() { return hipSetDevice(device) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE; }
 
@@ -136,7 +139,7 @@ struct ag_rs_ctx {
       (void)hipStreamSynchronize(own_stream);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &stage_in, &stage_out, &one_in, &one_out})
+                      &d_xmask, &d_rows, &d_xblocks, &stage_in, &stage_out, &one_in, &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
@@ -209,14 +212,21 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
                   int mode) {
   if (nblocks == 0) return AG_RS_OK;
   const int hr = ag::use_high_rate(k, m);
-  // classify patterns: 0 = nothing to restore, 1 = bitsliced (full recovery set), 2 = generic.
+  // classify patterns: 0 = nothing to restore, 1 = transform kernel (full recovery set),
+  // 3 = bitsliced general decoder, 2 = table-driven generic kernel.
   // The transform inverts the encoder only when all N recovery points exist (m == N):
   // with m < N the points m..N-1 were never stored.
   std::vector<uint8_t> cls(npat);
+  const bool aligned = aligned16(orig) && aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0;
   const unsigned npts = xform_points(k, m, S);
-  const bool fast_geo = mode == AG_RS_DECODE_ANY_K && npts != 0 && m == npts && aligned16(orig) &&
-                        aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0;
-  bool any_fast = false, any_generic = false;
+  const bool fast_geo = mode == AG_RS_DECODE_ANY_K && npts != 0 && m == npts && aligned;
+  const size_t xchunk = hr == 1 ? next_pow2(m) : 0;
+  const size_t xw = hr == 1 ? next_pow2(xchunk + k) : 0;
+  const size_t cps = S / 64;
+  // decode_x: HighRate, W in {32, 64}; one pattern per tile (single pattern, or tiles
+  // that never straddle blocks)
+  const bool x_geo = hr == 1 && S % 64 == 0 && (xw == 32 || xw == 64) && aligned && (npat == 1 || cps % 64 == 0);
+  bool any_fast = false, any_generic = false, any_x = false;
   for (size_t p = 0; p < npat; ++p) {
     size_t no = 0, nr = 0;
     for (size_t i = 0; i < k; ++i) no += opres[p * k + i] != 0;
@@ -227,6 +237,9 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     } else if (fast_geo && nr == m) {
       cls[p] = 1;
       any_fast = true;
+    } else if (x_geo) {
+      cls[p] = 3;
+      any_x = true;
     } else {
       cls[p] = 2;
       any_generic = true;
@@ -262,6 +275,70 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
     const auto kind = npts == 32 ? ag::XformKind::kDecode32 : ag::XformKind::kDecode64;
     if (ag::launch_xform(kind, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
+  if (any_x) {
+    if ((st = c->ensure_tables())) return st;
+    // per pattern: [erased (locator) | present (loaded) | restored] position bits
+    std::vector<uint64_t> xm(3 * npat, 0);
+    for (size_t p = 0; p < npat; ++p) {
+      if (cls[p] != 3) continue;
+      uint64_t e = 0, in = 0, out = 0;
+      for (size_t j = 0; j < xchunk; ++j) {
+        if (j < m && rpres[p * m + j]) in |= uint64_t{1} << j;
+        else e |= uint64_t{1} << j;  // lost recovery or virtual point m..chunk-1
+      }
+      for (size_t i = 0; i < k; ++i) {
+        const uint64_t bit = uint64_t{1} << (xchunk + i);
+        if (opres[p * k + i]) in |= bit; else { e |= bit; out |= bit; }
+      }
+      xm[p] = e;
+      xm[npat + 2 * p] = in;
+      xm[npat + 2 * p + 1] = out;
+    }
+    if (xm != c->xmask_host || xw != c->xmask_w) {
+      AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read xmask_host
+      if ((st = c->d_xmask.ensure(xm.size() * 8, c->stream))) return st;
+      if ((st = c->d_rows.ensure(npat * xw * 16 * 4, c->stream))) return st;
+      c->xmask_host = xm;
+      c->xmask_w = xw;
+      AG_HIP(hipMemcpyAsync(c->d_xmask.ptr, c->xmask_host.data(), xm.size() * 8, hipMemcpyHostToDevice, c->stream));
+      const uint64_t* dx = c->d_xmask.as<uint64_t>();
+      if (ag::launch_decode_rows(dx, dx + npat, static_cast<uint32_t>(npat), static_cast<uint32_t>(xw), c->dtables(),
+                                 c->d_rows.as<uint32_t>(), c->stream) != hipSuccess)
+        return AG_RS_ERR_DEVICE;
+    }
+    ag::DecodeXParams p{};
+    p.rec = rec;
+    p.rec_block_stride = rstride;
+    p.rec_shard_stride = S;
+    p.orig = orig;
+    p.orig_block_stride = ostride;
+    p.orig_shard_stride = S;
+    p.pmask = c->d_xmask.as<uint64_t>() + npat;
+    p.rows = c->d_rows.as<uint32_t>();
+    p.k = static_cast<uint32_t>(k);
+    p.m = static_cast<uint32_t>(m);
+    p.chunk = static_cast<uint32_t>(xchunk);
+    p.chunks_per_shard = static_cast<uint32_t>(cps);
+    p.total_columns = static_cast<uint64_t>(nblocks) * cps;
+    uint64_t ntiles;
+    if (npat == 1) {
+      ntiles = (p.total_columns + 63) / 64;
+    } else {
+      p.per_block = 1;
+      p.tiles_per_block = static_cast<uint32_t>(cps / 64);
+      std::vector<uint32_t> ids;
+      for (size_t b = 0; b < nblocks; ++b)
+        if (cls[b] == 3) ids.push_back(static_cast<uint32_t>(b));
+      if (ids.size() != nblocks) {
+        AG_HIP(hipStreamSynchronize(c->stream));  // a previous id upload may be pending
+        if ((st = c->d_xblocks.ensure(ids.size() * 4, c->stream))) return st;
+        AG_HIP(hipMemcpy(c->d_xblocks.ptr, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+        p.block_ids = c->d_xblocks.as<uint32_t>();
+      }
+      ntiles = static_cast<uint64_t>(ids.size()) * p.tiles_per_block;
+    }
+    if (ag::launch_decode_x(static_cast<unsigned>(xw), p, ntiles, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   }
   if (!any_generic) return AG_RS_OK;
 

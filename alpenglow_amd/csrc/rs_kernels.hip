@@ -102,21 +102,30 @@ struct PassB {
     static constexpr int g = (NW * t) & ~(2 * d - 1);
   };
 };
-template <int NW, int DIN, int DOUT>
-__device__ __forceinline__ void xf_pass_b(Regs8& r) {
+template <int NW, int DIN>
+__device__ __forceinline__ void xf_pass_b_ifft(Regs8& r) {
   constexpr int NL = PassB<NW>::kLayers;
-  static_for<NL>([&](auto L) {  // IFFT, ascending distance
+  static_for<NL>([&](auto L) {  // ascending distance
     static_for<4>([&](auto I) {
       using P = typename PassB<NW>::template Pair<decltype(L)::value, decltype(I)::value>;
       dev::ifft_bfly<P::g + P::d + DIN - 1>(r[P::t], r[P::u]);
     });
   });
-  static_for<NL>([&](auto L) {  // FFT, descending distance
+}
+template <int NW, int DOUT>
+__device__ __forceinline__ void xf_pass_b_fft(Regs8& r) {
+  constexpr int NL = PassB<NW>::kLayers;
+  static_for<NL>([&](auto L) {  // descending distance
     static_for<4>([&](auto I) {
       using P = typename PassB<NW>::template Pair<NL - 1 - decltype(L)::value, decltype(I)::value>;
       dev::fft_bfly<P::g + P::d + DOUT - 1>(r[P::t], r[P::u]);
     });
   });
+}
+template <int NW, int DIN, int DOUT>
+__device__ __forceinline__ void xf_pass_b(Regs8& r) {
+  xf_pass_b_ifft<NW, DIN>(r);
+  xf_pass_b_fft<NW, DOUT>(r);
 }
 
 template <int NW, int DOUT>
@@ -166,21 +175,25 @@ struct TileIO {
   uint64_t blk[4];  // block of chunk q (for the per-block store mask)
   uint32_t valid;   // bit q: chunk q exists (idle pieces re-read the last chunk, never store)
 };
-__device__ __forceinline__ TileIO tile_io(const XformParams& p, uint64_t tile, int lane, uint64_t block_stride) {
+__device__ __forceinline__ TileIO tile_io_g(uint64_t total_columns, uint32_t chunks_per_shard, uint64_t tile, int lane,
+                                           uint64_t block_stride) {
   TileIO io;
   io.valid = 0;
   const uint32_t quarter = ((lane >> 5) << 1) | (lane & 1);
   static_for<4>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
     const uint64_t g = tile * kXfLanes + 16 * q + ((lane & 31) >> 1);
-    const bool ok = g < p.total_columns;
-    const uint64_t gc = ok ? g : p.total_columns - 1;
-    const uint64_t blk = gc / p.chunks_per_shard;
+    const bool ok = g < total_columns;
+    const uint64_t gc = ok ? g : total_columns - 1;
+    const uint64_t blk = gc / chunks_per_shard;
     io.blk[q] = blk;
-    io.off[q] = blk * block_stride + (gc - blk * p.chunks_per_shard) * 64 + 16 * quarter;
+    io.off[q] = blk * block_stride + (gc - blk * chunks_per_shard) * 64 + 16 * quarter;
     io.valid |= ok ? (1u << q) : 0u;
   });
   return io;
+}
+__device__ __forceinline__ TileIO tile_io(const XformParams& p, uint64_t tile, int lane, uint64_t block_stride) {
+  return tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, block_stride);
 }
 
 // lanes l and l + 32 exchange register halves (see TileIO); an involution
@@ -349,6 +362,170 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
     const uint32_t s = 8 * wave + t;  // wave-uniform
     if (s < p.n_out) store_shard(p.out + s * p.out_shard_stride, out_io, store_qmask(out_io, mask, s), ra[t]);
   });
+}
+
+// =====================================================================================
+// decode_x<NW>: the crate's HighRate decoder for any erasure
+// pattern, bitsliced, over a W = 8*NW point window (W = next_pow2(chunk + k) in {32, 64}):
+//   pass A : load present positions (recovery j < chunk, original chunk + i), multiply by
+//            the pattern's locator constant (runtime 16x16 GF(2) matrix), IFFT dist 1..4
+//   pass B : IFFT dist 8.., formal derivative, FFT ..8
+//   pass C : FFT dist 4..1, multiply erased originals by the inverse locator, store
+// Position j sits where shard j sits in xform<NW>.  The formal derivative
+//   w'[j] = w[j] ^ XOR_{b : bit b of j clear} w[j | 2^b]     (all terms pre-derivative)
+// splits in layout B into slot bits (in-lane) and wave bits (partner waves through LDS).
+// Pattern constants come from decode_rows_kernel; one pattern per tile (either one
+// pattern for the batch, or tiles that never straddle blocks).
+// =====================================================================================
+
+// x <- M x for a runtime 16x16 GF(2) matrix, rows[o] bit i = M[o][i] (wave-uniform rows:
+// the row words and the 0/~0 masks live in SGPRs; 256 v_bitop3 per 32-symbol plane set).
+__device__ __forceinline__ void mul_rt(uint32_t* x, const uint32_t* __restrict__ rows) {
+  uint32_t y[16];
+  static_for<16>([&](auto O) {
+    constexpr int o = decltype(O)::value;
+    const uint32_t r = __builtin_amdgcn_readfirstlane(rows[o]);
+    uint32_t acc = 0;
+    static_for<16>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const uint32_t msk = static_cast<uint32_t>(static_cast<int32_t>(r << (31 - i)) >> 31);
+      acc = __builtin_amdgcn_bitop3_b32(acc, x[i], msk, 0x78);  // acc ^ (x & msk)
+    });
+    y[o] = acc;
+  });
+  static_for<16>([&](auto O) { x[decltype(O)::value] = y[decltype(O)::value]; });
+}
+
+__device__ __forceinline__ void lds_get_xor(const uint4* lds, int slot, int lane, uint32_t* v) {
+  static_for<4>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    const uint4 x = lds[(slot * 4 + q) * kXfLanes + lane];
+    v[4 * q] ^= x.x;
+    v[4 * q + 1] ^= x.y;
+    v[4 * q + 2] ^= x.z;
+    v[4 * q + 3] ^= x.w;
+  });
+}
+
+// Formal derivative in layout B (slot t of wave w = position w + NW*t).
+template <int NW>
+__device__ __forceinline__ void xf_derivative(int wave, int lane, uint4* lds, Regs8& r) {
+  constexpr int LNW = NW == 4 ? 2 : 3;
+  static_for<2>([&](auto Rho) {
+    constexpr int rho = decltype(Rho)::value;
+    static_for<4>([&](auto U) { lds_put(lds, 4 * wave + decltype(U)::value, lane, r[4 * rho + decltype(U)::value]); });
+    __syncthreads();
+    // slot bits, ascending t: partners t | 2^tb > t still hold pre-derivative values
+    static_for<4>([&](auto U) {
+      constexpr int t = 4 * rho + decltype(U)::value;
+      static_for<3>([&](auto TB) {
+        constexpr int tb = decltype(TB)::value;
+        if constexpr (!((t >> tb) & 1)) dev::xor_planes(r[t], r[t | (1 << tb)]);
+      });
+    });
+    // wave bits: partner waves' pre-derivative slots from LDS
+    static_for<LNW>([&](auto B) {
+      constexpr int b = decltype(B)::value;
+      if (!((wave >> b) & 1)) {
+        const int pw = wave | (1 << b);
+        static_for<4>([&](auto U) { lds_get_xor(lds, 4 * pw + decltype(U)::value, lane, r[4 * rho + decltype(U)::value]); });
+      }
+    });
+    __syncthreads();
+  });
+}
+
+template <int NW>
+__global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(const DecodeXParams p) {
+  constexpr int W = 8 * NW;
+  __shared__ uint4 lds[4 * NW * 4 * kXfLanes];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // tile -> (pattern, address tile)
+  uint64_t vtile = blockIdx.x, pat = 0;
+  if (p.per_block) {
+    const uint64_t bi = blockIdx.x / p.tiles_per_block;
+    const uint64_t blk = p.block_ids ? p.block_ids[bi] : bi;
+    vtile = blk * p.tiles_per_block + (blockIdx.x - bi * p.tiles_per_block);
+    pat = blk;
+  }
+  const uint64_t in_mask = p.pmask[2 * pat], out_mask = p.pmask[2 * pat + 1];
+  const uint32_t* rows = p.rows + pat * (W * 16);
+  const TileIO io_r = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.rec_block_stride);
+  const TileIO io_o = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.orig_block_stride);
+
+  Regs8 ra;
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = 8 * wave + t;  // wave-uniform
+    if ((in_mask >> j) & 1) {
+      const bool is_rec = j < p.chunk;
+      const uint8_t* base = is_rec ? p.rec + j * p.rec_shard_stride : p.orig + (j - p.chunk) * p.orig_shard_stride;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = *reinterpret_cast<const uint4*>(base + (is_rec ? io_r.off[q] : io_o.off[q]));
+        ra[t][4 * q] = x.x;
+        ra[t][4 * q + 1] = x.y;
+        ra[t][4 * q + 2] = x.z;
+        ra[t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { ra[t][decltype(P)::value] = 0; });
+    }
+  });
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = 8 * wave + t;
+    if ((in_mask >> j) & 1) {
+      swap_halves(ra[t]);
+      dev::planes_from_raw(ra[t]);
+      mul_rt(ra[t], rows + j * 16);
+    }
+  });
+  xf_pass_a<NW, 0>(wave, ra);
+  Regs8 rb;
+  xf_exchange_ab<NW>(wave, lane, lds, ra, rb);
+  xf_pass_b_ifft<NW, 0>(rb);
+  xf_derivative<NW>(wave, lane, lds, rb);
+  xf_pass_b_fft<NW, 0>(rb);
+  xf_exchange_bc<NW>(wave, lane, lds, rb, ra);
+  if (((out_mask >> (8 * wave)) & 0xFF) == 0) return;  // nothing to restore in this wave
+  xf_pass_c<NW, 0>(wave, ra);
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = 8 * wave + t;
+    if ((out_mask >> j) & 1) {
+      mul_rt(ra[t], rows + j * 16);
+      store_shard(p.orig + (j - p.chunk) * p.orig_shard_stride, io_o, io_o.valid, ra[t]);
+    }
+  });
+}
+
+// Per pattern and window position x: the decoder's locator constant as a bitsliced
+// multiply matrix.  loc(x) = sum_{e erased, e != x} log(x ^ e) (mod 65535) -- the crate's
+// eval_poly over the window up to one constant factor, which cancels between the input
+// multiply (present x: exp(loc)) and the output multiply (restored x: exp(-loc)).
+__global__ __launch_bounds__(64) void decode_rows_kernel(const uint64_t* __restrict__ emask,
+                                                         const uint64_t* __restrict__ pmask, uint32_t W,
+                                                         const uint16_t* __restrict__ log_t,
+                                                         const uint16_t* __restrict__ exp_t, uint32_t* rows) {
+  const uint64_t pat = blockIdx.x;
+  const uint32_t x = threadIdx.x;
+  if (x >= W) return;
+  const uint64_t e = emask[pat], in = pmask[2 * pat], out = pmask[2 * pat + 1];
+  const bool is_in = (in >> x) & 1, is_out = (out >> x) & 1;
+  uint32_t* dst = rows + (pat * W + x) * 16;
+  if (!is_in && !is_out) return;
+  uint32_t acc = 0;
+  for (uint32_t y = 0; y < W; ++y)
+    if (((e >> y) & 1) && y != x) acc = dev::add_mod(acc, log_t[x ^ y]);
+  const uint16_t lg = is_in ? static_cast<uint16_t>(acc) : static_cast<uint16_t>(65535 - acc);
+  uint32_t r[16] = {};
+  for (int i = 0; i < 16; ++i) {
+    const uint16_t prod = dev::gmul(exp_t, log_t, static_cast<uint16_t>(1u << i), lg);
+    for (int o = 0; o < 16; ++o) r[o] |= ((prod >> o) & 1u) << i;
+  }
+  for (int o = 0; o < 16; ++o) dst[o] = r[o];
 }
 
 // =====================================================================================
@@ -638,6 +815,26 @@ __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* dst, uint64
 
 // ---- launchers ----------------------------------------------------------------------
 bool xform_supported(unsigned n) { return n == 32 || n == 64; }
+
+hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
+  if (ntiles == 0) return hipSuccess;
+  if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  if (p.k + p.chunk > W || p.m > p.chunk) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<unsigned>(ntiles));
+  switch (W) {
+    case 32: hipLaunchKernelGGL((decode_x_kernel<4>), grid, dim3(256), 0, stream, p); break;
+    case 64: hipLaunchKernelGGL((decode_x_kernel<8>), grid, dim3(512), 0, stream, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_rows(const uint64_t* emask, const uint64_t* pmask, uint32_t npat, uint32_t W,
+                              const GfDeviceTables& t, uint32_t* rows, hipStream_t stream) {
+  if (npat == 0) return hipSuccess;
+  hipLaunchKernelGGL(decode_rows_kernel, dim3(npat), dim3(64), 0, stream, emask, pmask, W, t.log, t.exp, rows);
+  return hipGetLastError();
+}
 
 hipError_t launch_encode_mc(unsigned chunk, const XformParams& p, hipStream_t stream) {
   if (p.total_columns == 0) return hipSuccess;

@@ -34,13 +34,37 @@ bool xform_supported(unsigned n);
 // in = originals (n_in = k), out = recovery (n_out = m).  out_mask unused.
 hipError_t launch_encode_mc(unsigned chunk, const XformParams& p, hipStream_t stream);
 
-// Generic (any geometry) table-driven kernels.  One thread per (block, symbol).
 struct GfDeviceTables {
   const uint16_t* exp;
   const uint16_t* log;
   const uint16_t* skew;
   const uint16_t* log_walsh;
 };
+
+// Bitsliced HighRate decode for any erasure pattern over a W = 32 / 64 point window.
+// Positions: recovery j < chunk (shard j), originals chunk + i (shard i).
+struct DecodeXParams {
+  const uint8_t* rec;
+  uint64_t rec_block_stride;
+  uint64_t rec_shard_stride;
+  uint8_t* orig;  // present originals are read, restored ones written here
+  uint64_t orig_block_stride;
+  uint64_t orig_shard_stride;
+  const uint64_t* pmask;      // [pattern][2]: positions present (loaded), positions restored
+  const uint32_t* rows;       // [pattern][W][16] multiply matrices (decode_rows_kernel)
+  const uint32_t* block_ids;  // per_block: blocks processed (null = 0..)
+  uint32_t per_block;         // 1: pattern = block, tiles_per_block tiles per block
+  uint32_t tiles_per_block;   // chunks_per_shard / 64 (per_block mode)
+  uint32_t k, m, chunk;
+  uint32_t chunks_per_shard;
+  uint64_t total_columns;  // batch blocks * chunks_per_shard
+};
+hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream);
+// rows for npat patterns: emask[p] = erased positions (locator), pmask as above.
+hipError_t launch_decode_rows(const uint64_t* emask, const uint64_t* pmask, uint32_t npat, uint32_t W,
+                              const GfDeviceTables& t, uint32_t* rows, hipStream_t stream);
+
+// Generic (any geometry) table-driven kernels.  One thread per (block, symbol).
 
 struct GenericEncodeParams {
   const uint8_t* orig;

@@ -47,6 +47,10 @@ def parse():
     ap.add_argument("--m", type=int, default=32)
     ap.add_argument("--erase", type=int, default=-1,
                     help="data shards erased per block (default: k/2, at most m)")
+    ap.add_argument("--lose-coding", type=int, default=0,
+                    help="coding shreds also lost per block (forces the general decoder)")
+    ap.add_argument("--random-patterns", action="store_true",
+                    help="seeded random erasure pattern per block instead of the first e data shreds")
     ap.add_argument("--only", choices=["both", "encode", "decode"], default="both",
                     help="profiling aid: time only one of the two kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -86,6 +90,9 @@ def main():
         raise SystemExit("block bytes must split into k even-sized shards")
     S = B // k
     e = args.erase if args.erase >= 0 else min(k // 2, m)
+    lc = args.lose_coding
+    if e + lc > m:
+        raise SystemExit("erased data + lost coding shreds must not exceed m")
     cw_stride = (k + m) * S
 
     ctx = rs.Context(local)
@@ -98,8 +105,18 @@ def main():
     seed_base = 0x5EED_A19E_0000_0000 + first
     rs.fill_splitmix(ctx, cw, n, k * S, cw_stride, seed_base)
     data_ptr, par_ptr = cw.data_ptr(), cw.data_ptr() + k * S
-    opres = [0] * e + [1] * (k - e)
-    rpres = [1] * m
+    if args.random_patterns:  # per block: e random data shreds and lc random coding shreds lost
+        import random as _random
+
+        rng = _random.Random(0xA1 + first)
+        opres, rpres = [], []
+        for _ in range(n):
+            lost, lost_r = set(rng.sample(range(k), e)), set(rng.sample(range(m), lc))
+            opres += [0 if i in lost else 1 for i in range(k)]
+            rpres += [0 if j in lost_r else 1 for j in range(m)]
+    else:
+        opres = [0] * e + [1] * (k - e)
+        rpres = [0] * lc + [1] * (m - lc)
 
     def encode():
         rs.encode_batch(ctx, k, m, S, n, data_ptr, cw_stride, par_ptr, cw_stride)
@@ -147,7 +164,8 @@ def main():
     verify = None
     if not args.no_verify:
         view = cw.view(n, k + m, S)
-        view[:, :e].zero_()
+        lost = torch.tensor(opres, dtype=torch.uint8).view(-1, k)[: n if args.random_patterns else 1] == 0
+        view[:, :k][lost.to(dev).expand(n, k)] = 0
         reconstruct()
         ref = torch.empty((n, k * S), dtype=torch.uint8, device=dev)
         rs.fill_splitmix(ctx, ref, n, k * S, k * S, seed_base)
@@ -185,9 +203,12 @@ def main():
             "data": "synthetic (splitmix64 random blocks, device-generated)",
             "config": {"workload": (f"{args.stream_blocks} x {B >> 20} MiB block stream over {world} GPU(s)"
                                     if args.stream_blocks else f"{n} x {B >> 20} MiB blocks per GPU")
-                                   + f", {k}:{m} encode + reconstruct with {e}/{k} data shreds erased",
+                                   + f", {k}:{m} encode + reconstruct with {e}/{k} data shreds erased"
+                                   + (f" and {lc}/{m} coding shreds lost" if lc else "")
+                                   + (" (random pattern per block)" if args.random_patterns else ""),
                        "blocks_per_gpu": n, "block_bytes": B, "shard_bytes": S,
                        "data_shreds": k, "coding_shreds": m, "erased_data_shreds": e,
+                       "lost_coding_shreds": lc, "random_patterns": bool(args.random_patterns),
                        "parallelism": f"blocks sharded over {world} GPU(s), no collective",
                        "only": args.only},
             "roofline": {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBPS,
@@ -243,7 +264,7 @@ def _cpu_baseline(args, cw, k, m, S, e):
     rec = ro_c.encode_blocks(data, m, threads=threads)
     te = time.perf_counter() - t
     op = np.array([0] * e + [1] * (k - e), np.uint8)
-    rp = np.ones(m, np.uint8)
+    rp = np.array([0] * args.lose_coding + [1] * (m - args.lose_coding), np.uint8)
     cwh = np.concatenate([data, rec], axis=1)
     t = time.perf_counter()
     out = ro_c.decode_blocks(cwh, k, op, rp, threads=threads)

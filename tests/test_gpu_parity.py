@@ -209,6 +209,65 @@ def test_any_k_decode_partial_recovery_block(ctx, dev, k, m):
         assert np.array_equal(got, blocks), mode
 
 
+def _random_pattern_case(rng, k, m, S, n, seed, lose_rec):
+    blocks = np.stack([np.frombuffer(o.block_bytes(seed + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    op, rp, damaged = [], [], blocks.copy()
+    for b in range(n):
+        lr = rng.randrange(0, lose_rec + 1)
+        e = rng.randrange(1, m - lr + 1)
+        lost, lost_r = rng.sample(range(k), min(e, k)), rng.sample(range(m), lr)
+        damaged[b, lost] = 0xC3
+        op += [0 if i in lost else 1 for i in range(k)]
+        rp += [0 if j in lost_r else 1 for j in range(m)]
+    return blocks, rec, damaged, op, rp
+
+
+@pytest.mark.parametrize("k,m,S,n", [(16, 4, 4096, 6), (16, 4, 640, 11), (24, 8, 1024, 5), (20, 12, 192, 7),
+                                     (32, 32, 1024, 13), (32, 16, 4096, 3), (48, 16, 2048, 4), (17, 15, 64, 9)])
+@pytest.mark.parametrize("mode", [rs.DECODE_EXACT, rs.DECODE_ANY_K])
+def test_general_decode_one_pattern(ctx, dev, k, m, S, n, mode):
+    """Bitsliced general decoder (decode_x, W = 32 / 64), one erasure pattern for the
+    batch including lost recovery shards; tiles may straddle blocks."""
+    rng = random.Random(k * 1000 + m + S)
+    blocks = np.stack([np.frombuffer(o.block_bytes(700 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    lr = rng.randrange(0, m // 2 + 1)
+    e = max(1, min(k, m - lr))
+    lost, lost_r = rng.sample(range(k), e), rng.sample(range(m), lr)
+    damaged = blocks.copy()
+    damaged[:, lost] = 0x99
+    op = [0 if i in lost else 1 for i in range(k)]
+    rp = [0 if j in lost_r else 1 for j in range(m)]
+    got = gpu_decode(ctx, dev, damaged, rec, op, rp, mode)
+    assert np.array_equal(got, blocks)
+
+
+@pytest.mark.parametrize("k,m,S,n", [(32, 32, 4096, 12), (16, 4, 8192, 9), (32, 16, 4096, 6)])
+def test_general_decode_per_block_patterns(ctx, dev, k, m, S, n):
+    """Random pattern per block (per-block tiles, S a multiple of 4 KiB), some blocks with
+    the full recovery set (transform kernel), others with lost recovery shards."""
+    rng = random.Random(k + m + n)
+    blocks, rec, damaged, op, rp = _random_pattern_case(rng, k, m, S, n, 800, lose_rec=m // 2)
+    for mode in (rs.DECODE_ANY_K, rs.DECODE_EXACT):
+        got = gpu_decode(ctx, dev, damaged, rec, op, rp, mode)
+        assert np.array_equal(got, blocks), mode
+
+
+def test_general_decode_pattern_cache(ctx, dev):
+    """Back-to-back calls with different patterns of the same shape must not reuse stale
+    per-pattern matrices."""
+    k, m, S, n = 32, 32, 4096, 4
+    blocks = np.stack([np.frombuffer(o.block_bytes(900 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    for lost, lost_r in [([0, 1, 2], [5]), ([7, 8], [0, 1, 2]), ([0, 1, 2], [5]), ([31], [31])]:
+        damaged = blocks.copy()
+        damaged[:, lost] = 0
+        op = [0 if i in lost else 1 for i in range(k)]
+        rp = [0 if j in lost_r else 1 for j in range(m)]
+        assert np.array_equal(gpu_decode(ctx, dev, damaged, rec, op, rp, rs.DECODE_ANY_K), blocks)
+
+
 def test_decode_per_block_patterns(ctx, dev):
     """Random per-block patterns: some blocks have the full recovery set (bitsliced
     kernel), others lost recovery shards too (generic kernel)."""
