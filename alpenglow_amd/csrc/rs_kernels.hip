@@ -17,6 +17,12 @@
 #include "rs_device.hpp"
 #include "rs_launch.hpp"
 
+// Diagnostic builds only (wrong output): bit 0 skips decode_x's input multiply, bit 1 its
+// output multiply, bit 2 the formal derivative.
+#ifndef AG_DX_DIAG
+#define AG_DX_DIAG 0
+#endif
+
 namespace ag {
 namespace {
 
@@ -365,6 +371,223 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
 }
 
 // =====================================================================================
+// xform64h: 64-point transform with two workgroups per CU.  4 waves; a tile is 32
+// columns; lane half h (lane >> 5) is position bit 0 in passes A and C:
+//   pass A/C  position (w << 4) | (t << 1) | h : layers dist 2, 4, 8 in-lane; dist 1
+//             pairs the two lane halves (v_permlane32_swap gives every lane both x and
+//             y, both halves run the butterfly, each keeps its own output)
+//   pass B    position h | (w << 1) | (t << 3) : layers dist 16, 32 in-lane
+// The A<->B slot mapping is the 32-point kernel's, lane-local, so the LDS exchanges are
+// shared with xform<4>.  Skew constants never depend on h: the dist-1 group start is the
+// even position of the pair.
+// =====================================================================================
+
+// butterfly whose skew index is BASE + 16 * wave
+template <int BASE, bool INV>
+__device__ __forceinline__ void bfly_w16(int wave, uint32_t* x, uint32_t* y) {
+  switch (wave) {
+    case 0: bfly<BASE, INV>(x, y); break;
+    case 1: bfly<BASE + 16, INV>(x, y); break;
+    case 2: bfly<BASE + 32, INV>(x, y); break;
+    default: bfly<BASE + 48, INV>(x, y); break;
+  }
+}
+
+// dist-1 butterfly across lane halves: half 0 holds x, half 1 holds y (same register).
+template <int S, bool INV>
+__device__ __forceinline__ void cross_bfly(uint32_t* r, uint32_t hmask) {
+  uint32_t X[16], Y[16];
+  static_for<16>([&](auto P) {
+    constexpr int q = decltype(P)::value;
+    const auto sw = __builtin_amdgcn_permlane32_swap(r[q], r[q], false, false);
+    X[q] = sw[0];  // lanes of both halves: x
+    Y[q] = sw[1];  // y
+  });
+  if constexpr (INV) {
+    dev::xor_planes(Y, X);
+    if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(X, Y);
+  } else {
+    if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(X, Y);
+    dev::xor_planes(Y, X);
+  }
+  static_for<16>([&](auto P) {
+    constexpr int q = decltype(P)::value;
+    r[q] = dev::bfi(hmask, Y[q], X[q]);
+  });
+}
+template <int BASE, bool INV>
+__device__ __forceinline__ void cross_bfly_w16(int wave, uint32_t* r, uint32_t hmask) {
+  switch (wave) {
+    case 0: cross_bfly<BASE, INV>(r, hmask); break;
+    case 1: cross_bfly<BASE + 16, INV>(r, hmask); break;
+    case 2: cross_bfly<BASE + 32, INV>(r, hmask); break;
+    default: cross_bfly<BASE + 48, INV>(r, hmask); break;
+  }
+}
+
+// in-lane layers of pass A / C: layer bit b (1..3) <-> slot bit b-1
+template <int B, int DELTA, bool INV>
+__device__ __forceinline__ void x64h_inlane_layer(int wave, Regs8& r) {
+  constexpr int d = 1 << B, tb = B - 1;
+  static_for<4>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    constexpr int t = ((i >> tb) << (tb + 1)) | (i & ((1 << tb) - 1));
+    constexpr int g = (2 * t) & ~(2 * d - 1);
+    bfly_w16<g + d + DELTA - 1, INV>(wave, r[t], r[t + (1 << tb)]);
+  });
+}
+template <int DIN>
+__device__ __forceinline__ void x64h_pass_a(int wave, uint32_t hmask, Regs8& r) {
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    cross_bfly_w16<2 * t + DIN, true>(wave, r[t], hmask);
+  });
+  x64h_inlane_layer<1, DIN, true>(wave, r);
+  x64h_inlane_layer<2, DIN, true>(wave, r);
+  x64h_inlane_layer<3, DIN, true>(wave, r);
+}
+template <int DOUT>
+__device__ __forceinline__ void x64h_pass_c(int wave, uint32_t hmask, Regs8& r) {
+  x64h_inlane_layer<3, DOUT, false>(wave, r);
+  x64h_inlane_layer<2, DOUT, false>(wave, r);
+  x64h_inlane_layer<1, DOUT, false>(wave, r);
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    cross_bfly_w16<2 * t + DOUT, false>(wave, r[t], hmask);
+  });
+}
+// pass B: slot t <-> position bits 3..5; layers bit 4 (slot bit 1), bit 5 (slot bit 2)
+template <int DIN>
+__device__ __forceinline__ void x64h_pass_b_ifft(Regs8& r) {
+  static_for<4>([&](auto I) {
+    constexpr int t = ((decltype(I)::value >> 1) << 2) | (decltype(I)::value & 1);
+    dev::ifft_bfly<32 * (t >> 2) + 16 + DIN - 1>(r[t], r[t + 2]);
+  });
+  static_for<4>([&](auto I) {
+    constexpr int t = decltype(I)::value;
+    dev::ifft_bfly<32 + DIN - 1>(r[t], r[t + 4]);
+  });
+}
+template <int DOUT>
+__device__ __forceinline__ void x64h_pass_b_fft(Regs8& r) {
+  static_for<4>([&](auto I) {
+    constexpr int t = decltype(I)::value;
+    dev::fft_bfly<32 + DOUT - 1>(r[t], r[t + 4]);
+  });
+  static_for<4>([&](auto I) {
+    constexpr int t = ((decltype(I)::value >> 1) << 2) | (decltype(I)::value & 1);
+    dev::fft_bfly<32 * (t >> 2) + 16 + DOUT - 1>(r[t], r[t + 2]);
+  });
+}
+
+// Half-wave tile I/O: a tile is 32 chunks; instruction q covers chunks 8q .. 8q+7 of the
+// tile per lane half (512 B lane-linear); half-lane c = 16a + b takes quarter (b & 1) of
+// chunk 8q + (b >> 1), low bytes for a = 0, high bytes for a = 1.  v_permlane16_swap then
+// pairs low and high bytes (lanes b and b + 16 of a half): a = 0 keeps chunks q = 0, 1,
+// a = 1 chunks q = 2, 3.
+__device__ __forceinline__ TileIO tile_io_h(uint64_t total_columns, uint32_t chunks_per_shard, uint64_t tile,
+                                            int lane, uint64_t block_stride) {
+  TileIO io;
+  io.valid = 0;
+  const int c = lane & 31, a = c >> 4, b = c & 15;
+  static_for<4>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    const uint64_t g = tile * 32 + 8 * q + (b >> 1);
+    const bool ok = g < total_columns;
+    const uint64_t gc = ok ? g : total_columns - 1;
+    const uint64_t blk = gc / chunks_per_shard;
+    io.blk[q] = blk;
+    io.off[q] = blk * block_stride + (gc - blk * chunks_per_shard) * 64 + 32 * a + 16 * (b & 1);
+    io.valid |= ok ? (1u << q) : 0u;
+  });
+  return io;
+}
+__device__ __forceinline__ void swap_rows16(uint32_t* v) {
+  static_for<8>([&](auto K) {
+    constexpr int k = decltype(K)::value;
+    const auto r = __builtin_amdgcn_permlane16_swap(v[k], v[k + 8], false, false);
+    v[k] = r[0];
+    v[k + 8] = r[1];
+  });
+}
+__device__ __forceinline__ void store_shard_h(uint8_t* __restrict__ base, const TileIO& io, uint32_t qmask,
+                                              const uint32_t* planes) {
+  uint32_t v[16];
+  static_for<16>([&](auto P) { v[decltype(P)::value] = planes[decltype(P)::value]; });
+  dev::transpose8(v);
+  dev::transpose8(v + 8);
+  swap_rows16(v);
+  static_for<4>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    if (qmask & (1u << q))
+      *reinterpret_cast<uint4*>(base + io.off[q]) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+  });
+}
+
+template <int DIN, int DOUT>
+__global__ __launch_bounds__(256, 2) void xform64h_kernel(const XformParams p) {
+  __shared__ uint4 lds[16 * 4 * kXfLanes];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t h = lane >> 5;
+  const uint32_t hmask = 0u - h;
+  const TileIO io = tile_io_h(p.total_columns, p.chunks_per_shard, blockIdx.x, lane, p.in_block_stride);
+  Regs8 ra;
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = (wave << 4) | (t << 1) | h;  // this lane's shard (differs per half)
+    if (s < p.n_in) {
+      const uint8_t* base = p.in + s * p.in_shard_stride;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        ra[t][4 * q] = x.x;
+        ra[t][4 * q + 1] = x.y;
+        ra[t][4 * q + 2] = x.z;
+        ra[t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { ra[t][decltype(P)::value] = 0; });
+    }
+  });
+  uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  if (p.out_mask) {
+    if (!p.pattern_per_block) {
+      const uint64_t m = p.out_mask[0];
+      mask[0] = mask[1] = mask[2] = mask[3] = m;
+    } else {
+      const TileIO oi = tile_io_h(p.total_columns, p.chunks_per_shard, blockIdx.x, lane, p.out_block_stride);
+      static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[oi.blk[decltype(Q)::value]]; });
+    }
+  }
+  static_for<8>([&](auto T) {
+    swap_rows16(ra[decltype(T)::value]);
+    dev::planes_from_raw(ra[decltype(T)::value]);
+  });
+  x64h_pass_a<DIN>(wave, hmask, ra);
+  Regs8 rb;
+  xf_exchange_ab<4>(wave, lane, lds, ra, rb);
+  x64h_pass_b_ifft<DIN>(rb);
+  x64h_pass_b_fft<DOUT>(rb);
+  xf_exchange_bc<4>(wave, lane, lds, rb, ra);
+
+  const TileIO out_io = tile_io_h(p.total_columns, p.chunks_per_shard, blockIdx.x, lane, p.out_block_stride);
+  uint32_t need = 0;
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = (wave << 4) | (t << 1) | h;
+    if (s < p.n_out && store_qmask(out_io, mask, s)) need = 1;
+  });
+  if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+  x64h_pass_c<DOUT>(wave, hmask, ra);
+  static_for<8>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = (wave << 4) | (t << 1) | h;
+    if (s < p.n_out) store_shard_h(p.out + s * p.out_shard_stride, out_io, store_qmask(out_io, mask, s), ra[t]);
+  });
+}
+
+// =====================================================================================
 // decode_x<NW>: the crate's HighRate decoder for any erasure
 // pattern, bitsliced, over a W = 8*NW point window (W = next_pow2(chunk + k) in {32, 64}):
 //   pass A : load present positions (recovery j < chunk, original chunk + i), multiply by
@@ -479,14 +702,18 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     if ((in_mask >> j) & 1) {
       swap_halves(ra[t]);
       dev::planes_from_raw(ra[t]);
+#if !(AG_DX_DIAG & 1)
       mul_rt(ra[t], rows + j * 16);
+#endif
     }
   });
   xf_pass_a<NW, 0>(wave, ra);
   Regs8 rb;
   xf_exchange_ab<NW>(wave, lane, lds, ra, rb);
   xf_pass_b_ifft<NW, 0>(rb);
+#if !(AG_DX_DIAG & 4)
   xf_derivative<NW>(wave, lane, lds, rb);
+#endif
   xf_pass_b_fft<NW, 0>(rb);
   xf_exchange_bc<NW>(wave, lane, lds, rb, ra);
   if (((out_mask >> (8 * wave)) & 0xFF) == 0) return;  // nothing to restore in this wave
@@ -495,7 +722,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     constexpr int t = decltype(T)::value;
     const uint32_t j = 8 * wave + t;
     if ((out_mask >> j) & 1) {
+#if !(AG_DX_DIAG & 2)
       mul_rt(ra[t], rows + j * 16);
+#endif
       store_shard(p.orig + (j - p.chunk) * p.orig_shard_stride, io_o, io_o.valid, ra[t]);
     }
   });
@@ -814,6 +1043,9 @@ __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* dst, uint64
 }  // namespace
 
 // ---- launchers ----------------------------------------------------------------------
+// Kernel variant selector for in-process A/B timing (tools/ab_xform.py); 0 = default.
+int g_xform_variant = 0;
+int xform_variant() { return g_xform_variant; }
 bool xform_supported(unsigned n) { return n == 32 || n == 64; }
 
 hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
@@ -865,10 +1097,18 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
       hipLaunchKernelGGL((xform_kernel<4, 0, 32>), grid, dim3(256), 0, stream, p);
       break;
     case XformKind::kEncode64:
-      hipLaunchKernelGGL((xform_kernel<8, 64, 0>), grid, dim3(512), 0, stream, p);
+      if (xform_variant() == 1)
+        hipLaunchKernelGGL((xform_kernel<8, 64, 0>), grid, dim3(512), 0, stream, p);
+      else
+        hipLaunchKernelGGL((xform64h_kernel<64, 0>), dim3(static_cast<unsigned>((p.total_columns + 31) / 32)),
+                           dim3(256), 0, stream, p);
       break;
     case XformKind::kDecode64:
-      hipLaunchKernelGGL((xform_kernel<8, 0, 64>), grid, dim3(512), 0, stream, p);
+      if (xform_variant() == 1)
+        hipLaunchKernelGGL((xform_kernel<8, 0, 64>), grid, dim3(512), 0, stream, p);
+      else
+        hipLaunchKernelGGL((xform64h_kernel<0, 64>), dim3(static_cast<unsigned>((p.total_columns + 31) / 32)),
+                           dim3(256), 0, stream, p);
       break;
     default:
       return hipErrorInvalidValue;
@@ -908,3 +1148,8 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nblocks, uint64_t block_b
 }
 
 }  // namespace ag
+
+extern "C" int ag_rs_internal_set_xform_variant(int v) {
+  ag::g_xform_variant = v;
+  return 0;
+}

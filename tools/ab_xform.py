@@ -19,7 +19,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--nblocks", type=int, default=4096)
-    ap.add_argument("--shard", type=int, default=32768)
+    ap.add_argument("--shard", type=int, default=0, help="shard bytes (default: 1 MiB / k)")
+    ap.add_argument("--k", type=int, default=32)
+    ap.add_argument("--m", type=int, default=32)
+    ap.add_argument("--erase", type=int, default=-1, help="data shards erased (default k/2, at most m)")
+    ap.add_argument("--lose-coding", type=int, default=0)
     ap.add_argument("--no-check", action="store_true", help="diagnostic builds with wrong output")
     args = ap.parse_args()
     import torch
@@ -37,13 +41,14 @@ def main():
     st = torch.cuda.Stream(dev)
     torch.cuda.set_stream(st)
     ctx.set_stream(st.cuda_stream)
-    k = m = 32
-    S, n = args.shard, args.nblocks
+    k, m = args.k, args.m
+    S, n = args.shard or (1 << 20) // k, args.nblocks
     stride = (k + m) * S
     cw = torch.empty((n, stride), dtype=torch.uint8, device=dev)
     rs.fill_splitmix(ctx, cw, n, k * S, stride, 0x5EED_A19E_0000_0000)
     dp, pp = cw.data_ptr(), cw.data_ptr() + k * S
-    op, rp = [0] * 16 + [1] * 16, [1] * 32
+    e = args.erase if args.erase >= 0 else min(k // 2, m)
+    op, rp = [0] * e + [1] * (k - e), [0] * args.lose_coding + [1] * (m - args.lose_coding)
     variants = [int(v) for v in args.variants.split(",")]
     res = {v: {"enc": [], "dec": []} for v in variants}
     ref = None
@@ -68,11 +73,13 @@ def main():
                 ref = chk
             assert args.no_check or chk == ref, "variant changed the output"
     B = k * S
+    ne = op.count(0)
     out = {}
     for v in variants:
         e = sorted(res[v]["enc"])[len(res[v]["enc"]) // 2]
         d = sorted(res[v]["dec"])[len(res[v]["dec"]) // 2]
-        out[v] = {"enc_ms": e, "dec_ms": d, "enc_GBps": n * B * 2 / e / 1e6, "dec_GBps": n * B * 1.5 / d / 1e6,
+        out[v] = {"enc_ms": e, "dec_ms": d, "enc_GBps": n * B * (1 + m / k) / e / 1e6,
+                  "dec_GBps": n * B * (1 + ne / k) / d / 1e6,
                   "enc_min_ms": min(res[v]["enc"]), "dec_min_ms": min(res[v]["dec"])}
     print(json.dumps(out, indent=1))
 
