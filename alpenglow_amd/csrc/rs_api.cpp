@@ -83,6 +83,17 @@ unsigned mc_chunk(size_t k, size_t m, size_t S) {
   return c <= 4 && k > c ? static_cast<unsigned>(c) : 0;
 }
 
+// LowRate encode through the transform kernel, one launch per recovery chunk: returns the
+// chunk next_pow2(k) in {32, 64} when the recovery chunks fit the launcher, else 0.
+unsigned lowrate_chunk(size_t k, size_t m, size_t S) {
+  if (S == 0 || S % 64 || ag::use_high_rate(k, m) != 0) return 0;
+  const size_t c = next_pow2(k);
+  const size_t chunks = (m + c - 1) / c;
+  if (c == 32 && chunks <= 4) return 32;
+  if (c == 64 && chunks <= 3) return 64;
+  return 0;
+}
+
 }  // namespace
 
 struct ag_rs_ctx {
@@ -94,6 +105,7 @@ struct ag_rs_ctx {
   DevBuf scratch;                         // generic-kernel work rows
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
+  DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf stage_in, stage_out;             // host-memory calls
   DevBuf one_in, one_out;                 // crate-API single codeword
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
@@ -139,7 +151,8 @@ struct ag_rs_ctx {
       (void)hipStreamSynchronize(own_stream);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &stage_in, &stage_out, &one_in, &one_out})
+                      &d_xmask, &d_rows, &d_xblocks, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
+                      &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
@@ -155,7 +168,8 @@ int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
   if (nblocks == 0) return AG_RS_OK;
   const unsigned npts = xform_points(k, m, S);
   const unsigned mc = mc_chunk(k, m, S);
-  if ((npts || mc) && aligned16(orig) && aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0) {
+  const unsigned lr = lowrate_chunk(k, m, S);
+  if ((npts || mc || lr) && aligned16(orig) && aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0) {
     ag::XformParams p{};
     p.in = orig;
     p.in_block_stride = ostride;
@@ -167,11 +181,19 @@ int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
     p.n_out = static_cast<uint32_t>(m);
     p.chunks_per_shard = static_cast<uint32_t>(S / 64);
     p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
-    hipError_t e;
-    if (npts)
+    hipError_t e = hipSuccess;
+    if (npts) {
       e = ag::launch_xform(npts == 32 ? ag::XformKind::kEncode32 : ag::XformKind::kEncode64, p, c->stream);
-    else
+    } else if (mc) {
       e = ag::launch_encode_mc(mc, p, c->stream);
+    } else {
+      for (size_t j = 0; j * lr < m && e == hipSuccess; ++j) {  // one launch per recovery chunk
+        ag::XformParams pj = p;
+        pj.out = rec + j * lr * S;
+        pj.n_out = static_cast<uint32_t>(std::min<size_t>(lr, m - j * lr));
+        e = ag::launch_xform_lowrate(lr, static_cast<unsigned>(j), pj, c->stream);
+      }
+    }
     return e == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
   }
   int st = c->ensure_tables();
@@ -507,7 +529,9 @@ int ag_rs_use_high_rate(size_t k, size_t m) {
   return hr < 0 ? -AG_RS_ERR_UNSUPPORTED_SHARD_COUNT : hr;
 }
 
-int ag_rs_has_fast_path(size_t k, size_t m, size_t S) { return xform_points(k, m, S) || mc_chunk(k, m, S) ? 1 : 0; }
+int ag_rs_has_fast_path(size_t k, size_t m, size_t S) {
+  return xform_points(k, m, S) || mc_chunk(k, m, S) || lowrate_chunk(k, m, S) ? 1 : 0;
+}
 
 int ag_rs_encode_batch(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
                        size_t ostride, uint8_t* rec, size_t rstride, int memory) {
@@ -902,6 +926,90 @@ int ag_rs_coder_deshred(ag_rs_coder* c, size_t data_shreds, const uint8_t* const
   std::memcpy(data_out, data.data(), data.size());
   std::memcpy(coding_out, coding.data(), coding.size());
   *shred_bytes = S;
+  return AG_RS_OK;
+}
+
+int ag_rs_coder_shred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, const uint8_t* payloads,
+                            size_t payload_stride, const uint32_t* lens, uint8_t* cw, size_t cw_stride) {
+  if (!c || (n && (!lens || !cw))) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (m == 0 || m > kTotalShreds) return AG_RS_ERR_UNSUPPORTED_SHARD_COUNT;
+  if (S == 0 || S % 2 || S > AG_RS_MAX_DATA_PER_SHRED) return AG_RS_ERR_INVALID_SHARD_SIZE;
+  if (cw_stride < (kDataShreds + m) * S) return AG_RS_ERR_INVALID_ARGUMENT;
+  for (size_t b = 0; b < n; ++b) {
+    if (lens[b] > kMaxPayload) return AG_RS_ERR_TOO_MUCH_DATA;
+    const size_t padded = lens[b] + 2 * kDataShreds - lens[b] % (2 * kDataShreds);  // reed_solomon.rs:94-95
+    if (padded / kDataShreds != S) return AG_RS_ERR_INVALID_ARGUMENT;
+  }
+  if (n == 0) return AG_RS_OK;
+  int st = c->enter();
+  if (st) return st;
+  // d_lens may still be read by a previous call's pad kernel
+  AG_HIP(hipStreamSynchronize(c->stream));
+  if ((st = c->d_lens.ensure(n * 4, c->stream))) return st;
+  AG_HIP(hipMemcpy(c->d_lens.ptr, lens, n * 4, hipMemcpyHostToDevice));
+  if (ag::launch_coder_pad(payloads, payload_stride, c->d_lens.as<uint32_t>(), cw, cw_stride,
+                           static_cast<uint32_t>(kDataShreds * S), n, c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  return encode_device(c, kDataShreds, m, S, n, cw, cw_stride, cw + kDataShreds * S, cw_stride);
+}
+
+int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
+                              const uint8_t* dpres, const uint8_t* cpres, int mode, int64_t* out) {
+  if (!c || (n && (!cw || !dpres || !cpres || !out))) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (m == 0 || m > kTotalShreds) return AG_RS_ERR_UNSUPPORTED_SHARD_COUNT;
+  if (mode != AG_RS_DECODE_EXACT && mode != AG_RS_DECODE_ANY_K) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (S == 0 || S % 2) return AG_RS_ERR_INVALID_SHARD_SIZE;
+  if (kDataShreds * S > kMaxAfterPadding) return AG_RS_ERR_TOO_MUCH_DATA;  // reed_solomon.rs:183
+  if (cw_stride < (kDataShreds + m) * S) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  int st = c->enter();
+  if (st) return st;
+  // slices with fewer than 32 shreds: reported, and decoded as "nothing missing" (untouched)
+  std::vector<uint8_t> op(dpres, dpres + n * kDataShreds);
+  std::vector<uint8_t> ok(n, 1);
+  for (size_t b = 0; b < n; ++b) {
+    size_t cnt = 0;
+    for (size_t i = 0; i < kDataShreds; ++i) cnt += dpres[b * kDataShreds + i] != 0;
+    for (size_t j = 0; j < m; ++j) cnt += cpres[b * m + j] != 0;
+    if (cnt < kDataShreds) {
+      ok[b] = 0;
+      out[b] = -AG_RS_ERR_NOT_ENOUGH_SHARDS;
+      std::fill(op.begin() + b * kDataShreds, op.begin() + (b + 1) * kDataShreds, uint8_t{1});
+    }
+  }
+  uint8_t* rec = cw + kDataShreds * S;
+  if ((st = decode_device(c, kDataShreds, m, S, n, cw, cw_stride, rec, cw_stride, op.data(), cpres, n, mode)))
+    return st;
+  if ((st = c->d_strip.ensure(n * 8, c->stream))) return st;
+  if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(kDataShreds * S), n, c->d_strip.as<int64_t>(),
+                             c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  std::vector<int64_t> lens(n);
+  AG_HIP(hipMemcpyAsync(lens.data(), c->d_strip.ptr, n * 8, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipStreamSynchronize(c->stream));
+  for (size_t b = 0; b < n; ++b) {
+    if (!ok[b]) continue;
+    if (lens[b] < 0) {
+      ok[b] = 0;
+      out[b] = -AG_RS_ERR_INVALID_PADDING;
+    } else {
+      out[b] = lens[b];
+    }
+  }
+  // re-encode all coding shards (encode_coding_from_data) of each run of good slices
+  for (size_t b = 0; b < n;) {
+    if (!ok[b]) {
+      ++b;
+      continue;
+    }
+    size_t e = b;
+    while (e < n && ok[e]) ++e;
+    if ((st = encode_device(c, kDataShreds, m, S, e - b, cw + b * cw_stride, cw_stride, rec + b * cw_stride,
+                            cw_stride)))
+      return st;
+    b = e;
+  }
+  AG_HIP(hipStreamSynchronize(c->stream));
   return AG_RS_OK;
 }
 

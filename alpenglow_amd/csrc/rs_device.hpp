@@ -47,13 +47,39 @@ __device__ __forceinline__ uint32_t xsum(uint32_t acc, const uint32_t* y) {
   }
 }
 
-// x ^= y * skew[S]   (bitsliced; S is a compile-time skew index)
+// acc ^ XOR_{i in MASK} s[i] over a 64-bit signal mask, 3-input XORs.
+template <uint64_t MASK>
+__device__ __forceinline__ uint32_t xsum64(uint32_t acc, const uint32_t* s) {
+  if constexpr (MASK == 0) {
+    return acc;
+  } else {
+    constexpr int i = __builtin_ctzll(MASK);
+    constexpr uint64_t rest = MASK & (MASK - 1);
+    if constexpr (rest == 0) {
+      return acc ^ s[i];
+    } else {
+      constexpr int j = __builtin_ctzll(rest);
+      return xsum64<rest & (rest - 1)>(xor3(acc, s[i], s[j]), s);
+    }
+  }
+}
+
+// x ^= y * skew[S]   (bitsliced; S is a compile-time skew index).  Shared sub-sums of the
+// 16x16 network (kCse*, gen_consts.cpp) are computed once: ~36 VALU ops on average.
 template <int S>
 __device__ __forceinline__ void mul_acc(uint32_t* x, const uint32_t* y) {
   static_assert(S >= 0 && S < kSkewConstCount, "skew index outside generated table");
+  constexpr int NT = kCseNTemps[S];
+  uint32_t sig[16 + kCseMaxTemps];
+  static_for<16>([&](auto I) { sig[decltype(I)::value] = y[decltype(I)::value]; });
+  static_for<NT>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int a = kCseTemp[S][j][0], b = kCseTemp[S][j][1], c = kCseTemp[S][j][2];
+    if constexpr (c == 255) sig[16 + j] = sig[a] ^ sig[b]; else sig[16 + j] = xor3(sig[a], sig[b], sig[c]);
+  });
   static_for<16>([&](auto O) {
     constexpr int o = decltype(O)::value;
-    x[o] = xsum<kMulRow[S][o]>(x[o], y);
+    x[o] = xsum64<kCseRow[S][o]>(x[o], sig);
   });
 }
 

@@ -1019,6 +1019,62 @@ __global__ __launch_bounds__(1024) void locator_kernel(const uint8_t* erased, ui
 }
 
 // =====================================================================================
+// ReedSolomonCoder batch helpers (reed_solomon.rs:88-128 shred padding, :190-203 strip)
+// =====================================================================================
+// Data region of slice b (32 * S bytes at cw + b * cw_stride) := payload || 0x80 || 0...
+// (payload == null: the payload already sits in the data region; only the padding is
+// written).  One thread per 16 output bytes.
+__global__ __launch_bounds__(256) void coder_pad_kernel(const uint8_t* __restrict__ payload, uint64_t payload_stride,
+                                                        const uint32_t* __restrict__ lens, uint8_t* cw,
+                                                        uint64_t cw_stride, uint32_t data_bytes, uint64_t nslices) {
+  const uint64_t per = data_bytes / 16;
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (tid >= nslices * per) return;
+  const uint64_t b = tid / per;
+  const uint32_t j = static_cast<uint32_t>(tid - b * per) * 16;
+  const uint32_t len = lens[b];
+  uint8_t* dst = cw + b * cw_stride + j;
+  if (j + 16 <= len) {
+    if (payload) {
+      const uint8_t* src = payload + b * payload_stride + j;
+      if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+      } else {
+        for (int i = 0; i < 16; ++i) dst[i] = src[i];
+      }
+    }
+    return;
+  }
+  uint8_t v[16];
+  for (int i = 0; i < 16; ++i) {
+    const uint32_t pos = j + i;
+    v[i] = pos < len ? (payload ? payload[b * payload_stride + pos] : dst[i]) : (pos == len ? 0x80 : 0);
+  }
+  for (int i = 0; i < 16; ++i) dst[i] = v[i];
+}
+
+// Per slice: payload length after stripping the bit padding (trailing zeros, then a 0x80
+// marker), or -1 when the padding is invalid.  One workgroup per slice.
+__global__ __launch_bounds__(256) void coder_strip_kernel(const uint8_t* __restrict__ cw, uint64_t cw_stride,
+                                                          uint32_t data_bytes, int64_t* out) {
+  __shared__ int32_t best[256];
+  const uint8_t* d = cw + static_cast<uint64_t>(blockIdx.x) * cw_stride;
+  int32_t last = -1;
+  for (uint32_t i = threadIdx.x; i < data_bytes; i += blockDim.x)
+    if (d[i]) last = static_cast<int32_t>(i);
+  best[threadIdx.x] = last;
+  __syncthreads();
+  for (int w = 128; w > 0; w >>= 1) {
+    if (static_cast<int>(threadIdx.x) < w) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + w]);
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    const int32_t m = best[0];
+    out[blockIdx.x] = (m < 0 || d[m] != 0x80) ? -1 : m;
+  }
+}
+
+// =====================================================================================
 // splitmix64 fill (same generator as oracle/rs_oracle.py splitmix64_bytes)
 // =====================================================================================
 __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* dst, uint64_t nblocks, uint64_t words_per_block,
@@ -1047,6 +1103,32 @@ __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* dst, uint64
 int g_xform_variant = 0;
 int xform_variant() { return g_xform_variant; }
 bool xform_supported(unsigned n) { return n == 32 || n == 64; }
+
+hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hipStream_t stream) {
+  if (p.total_columns == 0) return hipSuccess;
+  const uint64_t tiles = (p.total_columns + (n == 32 ? 63 : 31)) / (n == 32 ? 64 : 32);
+  if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<unsigned>(tiles));
+  if (n == 32) {
+    switch (j) {
+      case 0: hipLaunchKernelGGL((xform_kernel<4, 0, 32>), grid, dim3(256), 0, stream, p); break;
+      case 1: hipLaunchKernelGGL((xform_kernel<4, 0, 64>), grid, dim3(256), 0, stream, p); break;
+      case 2: hipLaunchKernelGGL((xform_kernel<4, 0, 96>), grid, dim3(256), 0, stream, p); break;
+      case 3: hipLaunchKernelGGL((xform_kernel<4, 0, 128>), grid, dim3(256), 0, stream, p); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else if (n == 64) {
+    switch (j) {
+      case 0: hipLaunchKernelGGL((xform64h_kernel<0, 64>), grid, dim3(256), 0, stream, p); break;
+      case 1: hipLaunchKernelGGL((xform64h_kernel<0, 128>), grid, dim3(256), 0, stream, p); break;
+      case 2: hipLaunchKernelGGL((xform64h_kernel<0, 192>), grid, dim3(256), 0, stream, p); break;
+      default: return hipErrorInvalidValue;
+    }
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
@@ -1134,6 +1216,25 @@ hipError_t launch_locator(const uint8_t* erased, uint32_t npatterns, uint32_t W,
                           const uint16_t* log_walsh, uint16_t* loc, hipStream_t stream) {
   if (npatterns == 0) return hipSuccess;
   hipLaunchKernelGGL(locator_kernel, dim3(npatterns), dim3(1024), 0, stream, erased, W, fill_from, log_walsh, loc);
+  return hipGetLastError();
+}
+
+hipError_t launch_coder_pad(const uint8_t* payload, uint64_t payload_stride, const uint32_t* lens, uint8_t* cw,
+                            uint64_t cw_stride, uint32_t data_bytes, uint64_t nslices, hipStream_t stream) {
+  if (data_bytes % 16) return hipErrorInvalidValue;
+  const uint64_t n = nslices * (data_bytes / 16);
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(coder_pad_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream, payload,
+                     payload_stride, lens, cw, cw_stride, data_bytes, nslices);
+  return hipGetLastError();
+}
+
+hipError_t launch_coder_strip(const uint8_t* cw, uint64_t cw_stride, uint32_t data_bytes, uint64_t nslices,
+                              int64_t* out, hipStream_t stream) {
+  if (nslices == 0) return hipSuccess;
+  if (nslices > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(coder_strip_kernel, dim3(static_cast<unsigned>(nslices)), dim3(256), 0, stream, cw, cw_stride,
+                     data_bytes, out);
   return hipGetLastError();
 }
 

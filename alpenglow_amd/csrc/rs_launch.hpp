@@ -30,6 +30,9 @@ enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };
 hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream);
 // True when the bitsliced transform exists for this transform size.
 bool xform_supported(unsigned n);
+// LowRate encode, recovery chunk j: out = FFT_n(IFFT_n(in, 0), n * (j + 1)) for
+// n = next_pow2(k) in {32 (j < 4), 64 (j < 3)} -- the crate's LowRate encoder per chunk.
+hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hipStream_t stream);
 // Multi-chunk HighRate encode with chunk = next_pow2(m) in {1, 2, 4} and k <= 64:
 // in = originals (n_in = k), out = recovery (n_out = m).  out_mask unused.
 hipError_t launch_encode_mc(unsigned chunk, const XformParams& p, hipStream_t stream);
@@ -106,6 +109,13 @@ hipError_t launch_generic_decode(const GenericDecodeParams& p, hipStream_t strea
 // >= fill_from up to 65535 are also erased (LowRate virtual recovery); loc[p * W + x].
 hipError_t launch_locator(const uint8_t* erased, uint32_t npatterns, uint32_t W, uint32_t fill_from,
                           const uint16_t* log_walsh, uint16_t* loc, hipStream_t stream);
+
+// ReedSolomonCoder batches: padding writer (payload null = in place) and padding strip
+// (out[b] = payload length, or -1 for invalid padding).  data_bytes = 32 * S, % 16 == 0.
+hipError_t launch_coder_pad(const uint8_t* payload, uint64_t payload_stride, const uint32_t* lens, uint8_t* cw,
+                            uint64_t cw_stride, uint32_t data_bytes, uint64_t nslices, hipStream_t stream);
+hipError_t launch_coder_strip(const uint8_t* cw, uint64_t cw_stride, uint32_t data_bytes, uint64_t nslices,
+                              int64_t* out, hipStream_t stream);
 
 // Synthetic blocks: splitmix64 u64 little-endian words, block b seeded seed_base + b.
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nblocks, uint64_t block_bytes,

@@ -71,6 +71,7 @@ EXPORTS = (
     "ag_rs_decoder_add_recovery_shard", "ag_rs_decoder_decode",
     "ag_rs_decoder_restored_original", "ag_rs_decoder_free",
     "ag_rs_coder_new", "ag_rs_coder_free", "ag_rs_coder_shred", "ag_rs_coder_deshred",
+    "ag_rs_coder_shred_batch", "ag_rs_coder_deshred_batch",
 )
 
 
@@ -128,8 +129,12 @@ def load():
         "ag_rs_coder_free": ([p], None),
         "ag_rs_coder_shred": ([p, p, sz, p, p, psz], i),
         "ag_rs_coder_deshred": ([p, sz, p, p, p, p, psz, p, p, psz], i),
+        "ag_rs_coder_shred_batch": ([p, sz, sz, sz, p, sz, p, p, sz], i),
+        "ag_rs_coder_deshred_batch": ([p, sz, sz, sz, p, sz, p, p, i, p], i),
     }
     for name, (args, res) in sigs.items():
+        if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
+            continue              # check the shipped library exports everything
         f = getattr(L, name)
         f.argtypes = args
         f.restype = res
@@ -231,6 +236,33 @@ def decode_batch(ctx: Context, k: int, m: int, shard_bytes: int, nblocks: int, o
     _check(load().ag_rs_decode_batch(ctx.handle, k, m, shard_bytes, nblocks, _ptr(original),
                                      original_block_stride, _ptr(recovery), recovery_block_stride,
                                      op, rp, npat, mode, memory), "ag_rs_decode_batch")
+
+
+def coder_shred_batch(ctx: Context, num_coding: int, nslices: int, shred_bytes: int, payloads,
+                      payload_stride: int, payload_lens, codewords, codeword_stride: int):
+    """Batched ReedSolomonCoder::shred (device-resident): payload b (device) -> padded data
+    shards + num_coding coding shards in codeword b.  payloads None: already in place."""
+    lens = (ctypes.c_uint32 * nslices)(*payload_lens)
+    _check(load().ag_rs_coder_shred_batch(ctx.handle, num_coding, nslices, shred_bytes,
+                                          _ptr(payloads) if payloads is not None else None,
+                                          payload_stride, lens, _ptr(codewords), codeword_stride),
+           "ag_rs_coder_shred_batch")
+
+
+def coder_deshred_batch(ctx: Context, num_coding: int, nslices: int, shred_bytes: int, codewords,
+                        codeword_stride: int, data_present, coding_present,
+                        mode: int = DECODE_EXACT) -> list:
+    """Batched ReedSolomonCoder::deshred (device-resident, in place).  Returns per slice the
+    payload length or an RSError kind string ('NotEnoughShards' / 'InvalidPadding')."""
+    dp = bytes(bytearray(data_present))
+    cp = bytes(bytearray(coding_present))
+    if len(dp) != nslices * 32 or len(cp) != nslices * num_coding:
+        raise ValueError("present-flag arrays do not match the batch")
+    out = (ctypes.c_int64 * nslices)()
+    _check(load().ag_rs_coder_deshred_batch(ctx.handle, num_coding, nslices, shred_bytes,
+                                            _ptr(codewords), codeword_stride, dp, cp, mode, out),
+           "ag_rs_coder_deshred_batch")
+    return [v if v >= 0 else STATUS_KIND.get(-v, f"Status{-v}") for v in out]
 
 
 def fill_splitmix(ctx: Context, device_dst, nblocks: int, block_bytes: int, dst_block_stride: int,

@@ -183,6 +183,36 @@ int ag_rs_coder_deshred(ag_rs_coder* coder, size_t data_shreds, const uint8_t* c
                         uint8_t* payload_out, size_t* payload_len, uint8_t* data_out,
                         uint8_t* coding_out, size_t* shred_bytes);
 
+/* ---- 2b. ReedSolomonCoder over batches of slices (device-resident) -------------------
+ * All slices of a call share one shred size S (even, <= 1024).  Slice b's codeword is 32
+ * data shards then num_coding coding shards, contiguous, at codewords + b*codeword_stride
+ * (stride >= (32 + num_coding) * S).  A batch form of reed_solomon.rs:88-128 / :140-208 for
+ * callers holding many slices (block production, repair catch-up): the same bytes as
+ * ag_rs_coder_shred / ag_rs_coder_deshred per slice.
+ *
+ * shred_batch: payload_lens (HOST, nslices) must each pad to S (64-byte multiple / 32);
+ * payload b (device, payloads + b*payload_stride) is copied into the data region, padded
+ * with 0x80 00.., then the coding shards are encoded.  payloads NULL: the payloads already
+ * sit in the data regions.  Asynchronous on the context stream.
+ * Errors (nothing launched): TOO_MUCH_DATA (a length > 32767), INVALID_ARGUMENT. */
+int ag_rs_coder_shred_batch(ag_rs_ctx* ctx, size_t num_coding, size_t nslices, size_t shred_bytes,
+                            const uint8_t* payloads, size_t payload_stride,
+                            const uint32_t* payload_lens, uint8_t* codewords,
+                            size_t codeword_stride);
+
+/* deshred_batch: data_present [nslices][32] and coding_present [nslices][num_coding] are
+ * HOST 0/1 flags.  Restores the absent data shards in place, strips the padding and
+ * re-encodes all num_coding coding shards of every slice that succeeded (RawShreds of the
+ * reference).  payload_len_out (HOST, nslices): the payload length (the payload is the
+ * first len bytes of the slice's data region), or -AG_RS_ERR_NOT_ENOUGH_SHARDS /
+ * -AG_RS_ERR_INVALID_PADDING for a slice whose coding shards are left untouched.  mode:
+ * AG_RS_DECODE_EXACT (crate semantics) or AG_RS_DECODE_ANY_K.  Synchronous.  Whole-call
+ * errors: TOO_MUCH_DATA (S > 1024), INVALID_SHARD_SIZE. */
+int ag_rs_coder_deshred_batch(ag_rs_ctx* ctx, size_t num_coding, size_t nslices,
+                              size_t shred_bytes, uint8_t* codewords, size_t codeword_stride,
+                              const uint8_t* data_present, const uint8_t* coding_present,
+                              int mode, int64_t* payload_len_out);
+
 #ifdef __cplusplus
 }
 #endif

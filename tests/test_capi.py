@@ -70,11 +70,13 @@ def test_fast_path_geometry(lib):
     assert rs.has_fast_path(32, 32, 1024) and rs.has_fast_path(32, 32, 32768)
     assert rs.has_fast_path(20, 30, 64)
     assert not rs.has_fast_path(32, 32, 62)      # tail chunk -> generic kernel
-    assert not rs.has_fast_path(32, 64, 1024)    # LowRate -> generic kernel
+    assert rs.has_fast_path(32, 64, 1024)        # LowRate: one transform launch per chunk
+    assert rs.has_fast_path(32, 33, 1024)
+    assert not rs.has_fast_path(16, 64, 1024)    # LowRate chunk 16 -> generic kernel
     assert rs.has_fast_path(16, 4, 1024)          # multi-chunk small encode
     assert rs.has_fast_path(64, 64, 1024)         # 64-point transform
     assert not rs.has_fast_path(16, 8, 1024)      # chunk 8 -> generic kernel
-    assert not rs.has_fast_path(64, 33, 1024)     # tie with k > m: LowRate
+    assert rs.has_fast_path(64, 33, 1024)         # tie with k > m: LowRate, 64-point
 
 
 def test_generated_constants_match_oracle_skew():

@@ -133,7 +133,17 @@ def test_multichunk_small_encode(ctx, dev, k, m, S):
     assert np.array_equal(gpu_encode(ctx, dev, blocks, m), ro_c.encode_blocks(blocks, m, threads=8))
 
 
-@pytest.mark.parametrize("k,m,S", [(16, 4, 1000), (64, 64, 200), (32, 64, 1024), (32, 33, 1024), (32, 32, 1000)])
+@pytest.mark.parametrize("k,m,S", [(32, 64, 1024), (32, 33, 4096), (20, 100, 128), (32, 20, 192), (17, 128, 64),
+                                   (64, 33, 256), (40, 128, 128), (64, 192, 64)])
+def test_lowrate_encode_transform(ctx, dev, k, m, S):
+    """LowRate (CodingOnly 32:64, PETS 32:33, ...): one transform launch per recovery chunk."""
+    assert rs.has_fast_path(k, m, S) and not rs.use_high_rate(k, m)
+    n = 5
+    blocks = np.stack([np.frombuffer(o.block_bytes(1100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    assert np.array_equal(gpu_encode(ctx, dev, blocks, m), ro_c.encode_blocks(blocks, m, threads=8))
+
+
+@pytest.mark.parametrize("k,m,S", [(16, 4, 1000), (64, 64, 200), (32, 64, 1000), (32, 33, 1000), (32, 32, 1000)])
 def test_generic_encode_multi_block(ctx, dev, k, m, S):
     blocks = np.stack([np.frombuffer(o.block_bytes(7 + b, k * S), np.uint8).reshape(k, S) for b in range(3)])
     assert np.array_equal(gpu_encode(ctx, dev, blocks, m), ro_c.encode_blocks(blocks, m))
@@ -444,3 +454,103 @@ def test_coder_error_mapping(ctx):
     with pytest.raises(rs.RSError) as e:
         coder.deshred(odd)
     assert e.value.kind == "InvalidLayout"
+
+
+# ------------------------------------------------------------------ coder batches (§8 f1)
+
+def _payload_lens(rng, S, n):
+    """Payload lengths that all pad to shred size S (reed_solomon.rs:94-95)."""
+    return [rng.randrange(max(0, 32 * S - 64), 32 * S) for _ in range(n)]
+
+
+@pytest.mark.parametrize("S,n,inplace", [(1024, 6, False), (62, 5, False), (64, 9, True), (1024, 3, True)])
+def test_coder_shred_batch(ctx, dev, S, n, inplace):
+    rng = random.Random(S * 7 + n)
+    m = 32
+    lens = _payload_lens(rng, S, n)
+    payloads = [o.splitmix64_bytes(1000 + b, L) for b, L in enumerate(lens)]
+    stride = (32 + m) * S
+    cw = np.full((n, stride), 0xEE, np.uint8)
+    if inplace:
+        for b, p in enumerate(payloads):
+            cw[b, :len(p)] = np.frombuffer(p, np.uint8)
+        d_cw = to_dev(cw, dev)
+        rs.coder_shred_batch(ctx, m, n, S, None, 0, lens, d_cw, stride)
+    else:
+        P = (32 * S + 15) // 16 * 16
+        pay = np.zeros((n, P), np.uint8)
+        for b, p in enumerate(payloads):
+            pay[b, :len(p)] = np.frombuffer(p, np.uint8)
+        d_pay, d_cw = to_dev(pay, dev), to_dev(cw, dev)
+        rs.coder_shred_batch(ctx, m, n, S, d_pay, P, lens, d_cw, stride)
+    host = d_cw.cpu().numpy()
+    for b in range(n):
+        raw = o.coder_shred(payloads[b], m)
+        assert host[b, :32 * S].tobytes() == b"".join(raw.data)
+        assert host[b, 32 * S:].tobytes() == b"".join(raw.coding)
+
+
+def test_coder_shred_batch_errors(ctx, dev):
+    cw = torch.zeros((2, 64 * 64), dtype=torch.uint8, device=dev)
+    with pytest.raises(rs.RSError) as e:
+        rs.coder_shred_batch(ctx, 32, 2, 64, None, 0, [2000, 40000], cw, 64 * 64)
+    assert e.value.kind == "TooMuchData"
+    with pytest.raises(rs.RSError):  # 100 pads to S = 4, not 64
+        rs.coder_shred_batch(ctx, 32, 2, 64, None, 0, [2000, 100], cw, 64 * 64)
+
+
+@pytest.mark.parametrize("S", [1024, 96])
+@pytest.mark.parametrize("mode", [rs.DECODE_EXACT, rs.DECODE_ANY_K])
+def test_coder_deshred_batch(ctx, dev, S, mode):
+    """Batched deshred vs the oracle's ReedSolomonCoder::deshred: restored payload, all data
+    shards, re-encoded coding shards; NotEnoughShreds / InvalidPadding slices untouched."""
+    rng = random.Random(S + mode)
+    m, n = 32, 9
+    stride = (32 + m) * S
+    lens = _payload_lens(rng, S, n)
+    cw = np.zeros((n, stride), np.uint8)
+    for b in range(n):
+        if b == 6:    # all-zero data: consistent codeword, invalid padding
+            continue
+        if b == 7:    # random data without a 0x80 marker at the end of the nonzero bytes
+            data = bytearray(o.splitmix64_bytes(77, 32 * S))
+            data[-1] = 0x11
+            cw[b, :32 * S] = np.frombuffer(bytes(data), np.uint8)
+            cw[b, 32 * S:] = np.frombuffer(b"".join(o.encode([bytes(data[i * S:(i + 1) * S])
+                                                             for i in range(32)], m)), np.uint8)
+            continue
+        raw = o.coder_shred(o.splitmix64_bytes(2000 + b, lens[b]), m)
+        cw[b] = np.frombuffer(b"".join(raw.data) + b"".join(raw.coding), np.uint8)
+    present = []
+    for b in range(n):
+        if b == 0:
+            keep = set(range(64))
+        elif b == 1:
+            keep = set(range(32, 64))           # all data lost
+        elif b == 3:
+            keep = set(rng.sample(range(64), 31))  # not enough
+        else:
+            keep = set(rng.sample(range(64), rng.randrange(32, 64)))
+        present.append(keep)
+    damaged = cw.copy()
+    for b in range(n):
+        for i in range(64):
+            if i not in present[b]:
+                damaged[b, i * S:(i + 1) * S] = 0xAB
+    dp = [1 if i in present[b] else 0 for b in range(n) for i in range(32)]
+    cp = [1 if 32 + j in present[b] else 0 for b in range(n) for j in range(m)]
+    d_cw = to_dev(damaged, dev)
+    res = rs.coder_deshred_batch(ctx, m, n, S, d_cw, stride, dp, cp, mode)
+    host = d_cw.cpu().numpy()
+    for b in range(n):
+        shreds = [(i < 32, cw[b, i * S:(i + 1) * S].tobytes()) if i in present[b] else None for i in range(64)]
+        try:
+            payload, raw = o.coder_deshred(shreds, 32, m)
+        except o.RSError as err:  # wrapper NotEnoughShreds maps to the crate status code
+            assert res[b] == {"NotEnoughShreds": "NotEnoughShards"}.get(err.kind, err.kind), (b, res[b])
+            assert host[b, 32 * S:].tobytes() == damaged[b, 32 * S:].tobytes()  # coding untouched
+            continue
+        assert res[b] == len(payload), (b, res[b])
+        assert host[b, :len(payload)].tobytes() == payload
+        assert host[b, :32 * S].tobytes() == b"".join(raw.data)
+        assert host[b, 32 * S:].tobytes() == b"".join(raw.coding)
