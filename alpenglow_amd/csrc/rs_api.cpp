@@ -106,7 +106,13 @@ struct ag_rs_ctx {
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
-  DevBuf stage_in, stage_out;             // host-memory calls
+  DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
+  // host-memory calls: two staging slots, H2D / D2H streams next to the compute stream
+  struct Slot {
+    DevBuf in, out;
+    hipEvent_t up = nullptr, done = nullptr, down = nullptr;
+  } slot[2];
+  hipStream_t h2d = nullptr, d2h = nullptr;
   DevBuf one_in, one_out;                 // crate-API single codeword
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
   std::vector<uint64_t> xmask_host;       // last general-decode masks (d_xmask), W = xmask_w
@@ -145,10 +151,35 @@ struct ag_rs_ctx {
     return {d_exp.as<uint16_t>(), d_log.as<uint16_t>(), d_skew.as<uint16_t>(), d_log_walsh.as<uint16_t>()};
   }
 
+  int ensure_copy_streams() {
+    if (h2d) return AG_RS_OK;
+    AG_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
+    AG_HIP(hipStreamCreateWithFlags(&d2h, hipStreamNonBlocking));
+    for (Slot& s : slot) {
+      AG_HIP(hipEventCreateWithFlags(&s.up, hipEventDisableTiming));
+      AG_HIP(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+      AG_HIP(hipEventCreateWithFlags(&s.down, hipEventDisableTiming));
+      AG_HIP(hipEventRecord(s.down, d2h));  // slots start free
+    }
+    return AG_RS_OK;
+  }
+
   ~ag_rs_ctx() {
     if (own_stream) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(own_stream);
+    }
+    if (h2d) {
+      (void)hipStreamSynchronize(h2d);
+      (void)hipStreamSynchronize(d2h);
+      for (Slot& s : slot) {
+        s.in.release();
+        s.out.release();
+        for (hipEvent_t e : {s.up, s.done, s.down})
+          if (e) (void)hipEventDestroy(e);
+      }
+      (void)hipStreamDestroy(h2d);
+      (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
                       &d_xmask, &d_rows, &d_xblocks, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
@@ -159,6 +190,9 @@ struct ag_rs_ctx {
 };
 
 namespace {
+
+// Host-memory calls: bytes (in + out) per staging group; two groups in flight.
+constexpr size_t kStageGroupBytes = size_t{64} << 20;
 
 // Scratch budget of the generic kernels (per launch).
 constexpr size_t kGenericScratchBytes = size_t{512} << 20;
@@ -542,22 +576,29 @@ int ag_rs_encode_batch(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblock
   if ((st = c->enter())) return st;
   if (memory == AG_RS_MEM_DEVICE) return encode_device(c, k, m, S, nblocks, orig, ostride, rec, rstride);
   if (memory != AG_RS_MEM_HOST) return AG_RS_ERR_INVALID_ARGUMENT;
-  // host memory: stage groups of blocks through device buffers (packed strides)
+  // host memory: groups of blocks through two device staging slots, H2D / compute / D2H
+  // overlapped across groups (pinned host buffers give the full PCIe rate)
   const size_t in_b = k * S, out_b = m * S;
-  const size_t group = std::max<size_t>(1, (size_t{256} << 20) / (in_b + out_b));
-  for (size_t b0 = 0; b0 < nblocks; b0 += group) {
+  const size_t group = std::max<size_t>(1, kStageGroupBytes / (in_b + out_b));
+  if ((st = c->ensure_copy_streams())) return st;
+  size_t g = 0;
+  for (size_t b0 = 0; b0 < nblocks; b0 += group, ++g) {
     const size_t n = std::min(group, nblocks - b0);
-    if ((st = c->stage_in.ensure(n * in_b, c->stream)) || (st = c->stage_out.ensure(n * out_b, c->stream)))
-      return st;
-    AG_HIP(hipMemcpy2DAsync(c->stage_in.ptr, in_b, orig + b0 * ostride, ostride, in_b, n, hipMemcpyHostToDevice,
-                            c->stream));
-    if ((st = encode_device(c, k, m, S, n, c->stage_in.as<uint8_t>(), in_b, c->stage_out.as<uint8_t>(), out_b)))
-      return st;
-    AG_HIP(hipMemcpy2DAsync(rec + b0 * rstride, rstride, c->stage_out.ptr, out_b, out_b, n, hipMemcpyDeviceToHost,
-                            c->stream));
-    AG_HIP(hipStreamSynchronize(c->stream));
+    auto& sl = c->slot[g & 1];
+    AG_HIP(hipStreamWaitEvent(c->h2d, sl.down, 0));  // slot free: its previous download is done
+    if ((st = sl.in.ensure(group * in_b, c->h2d)) || (st = sl.out.ensure(group * out_b, c->h2d))) return st;
+    AG_HIP(hipMemcpy2DAsync(sl.in.ptr, in_b, orig + b0 * ostride, ostride, in_b, n, hipMemcpyHostToDevice, c->h2d));
+    AG_HIP(hipEventRecord(sl.up, c->h2d));
+    AG_HIP(hipStreamWaitEvent(c->stream, sl.up, 0));
+    if ((st = encode_device(c, k, m, S, n, sl.in.as<uint8_t>(), in_b, sl.out.as<uint8_t>(), out_b))) break;
+    AG_HIP(hipEventRecord(sl.done, c->stream));
+    AG_HIP(hipStreamWaitEvent(c->d2h, sl.done, 0));
+    AG_HIP(hipMemcpy2DAsync(rec + b0 * rstride, rstride, sl.out.ptr, out_b, out_b, n, hipMemcpyDeviceToHost, c->d2h));
+    AG_HIP(hipEventRecord(sl.down, c->d2h));
   }
-  return AG_RS_OK;
+  AG_HIP(hipStreamSynchronize(c->stream));
+  AG_HIP(hipStreamSynchronize(c->d2h));
+  return st;
 }
 
 int ag_rs_decode_batch(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
@@ -581,24 +622,57 @@ int ag_rs_decode_batch(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblock
     if (cnt < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
   }
   const size_t o_b = k * S, r_b = m * S;
-  const size_t group = std::max<size_t>(1, (size_t{256} << 20) / (o_b + r_b));
-  for (size_t b0 = 0; b0 < nblocks; b0 += group) {
+  const size_t group = std::max<size_t>(1, kStageGroupBytes / (o_b + r_b));
+  if ((st = c->ensure_copy_streams())) return st;
+  // One pattern: move only what the kernels read and write -- present originals up (none
+  // when the transform path restores from the full recovery set), erased originals down.
+  bool up_orig_all = npat > 1, down_all = npat > 1;
+  bool need_orig = true;
+  if (npat == 1) {
+    size_t nr = 0, no = 0;
+    for (size_t i = 0; i < m; ++i) nr += rpres[i] != 0;
+    for (size_t i = 0; i < k; ++i) no += opres[i] != 0;
+    if (no == k) return AG_RS_OK;  // nothing to restore
+    const unsigned npts = xform_points(k, m, S);
+    need_orig = !(mode == AG_RS_DECODE_ANY_K && npts && m == npts && nr == m);
+  }
+  size_t g = 0;
+  for (size_t b0 = 0; b0 < nblocks; b0 += group, ++g) {
     const size_t n = std::min(group, nblocks - b0);
-    if ((st = c->stage_in.ensure(n * r_b, c->stream)) || (st = c->stage_out.ensure(n * o_b, c->stream))) return st;
-    AG_HIP(hipMemcpy2DAsync(c->stage_in.ptr, r_b, rec + b0 * rstride, rstride, r_b, n, hipMemcpyHostToDevice,
-                            c->stream));
-    AG_HIP(hipMemcpy2DAsync(c->stage_out.ptr, o_b, orig + b0 * ostride, ostride, o_b, n, hipMemcpyHostToDevice,
-                            c->stream));
+    auto& sl = c->slot[g & 1];
+    AG_HIP(hipStreamWaitEvent(c->h2d, sl.down, 0));
+    if ((st = sl.in.ensure(group * r_b, c->h2d)) || (st = sl.out.ensure(group * o_b, c->h2d))) return st;
+    AG_HIP(hipMemcpy2DAsync(sl.in.ptr, r_b, rec + b0 * rstride, rstride, r_b, n, hipMemcpyHostToDevice, c->h2d));
+    if (up_orig_all) {
+      AG_HIP(hipMemcpy2DAsync(sl.out.ptr, o_b, orig + b0 * ostride, ostride, o_b, n, hipMemcpyHostToDevice, c->h2d));
+    } else if (need_orig) {
+      for (size_t i = 0; i < k; ++i)
+        if (opres[i])
+          AG_HIP(hipMemcpy2DAsync(sl.out.as<uint8_t>() + i * S, o_b, orig + b0 * ostride + i * S, ostride, S, n,
+                                  hipMemcpyHostToDevice, c->h2d));
+    }
+    AG_HIP(hipEventRecord(sl.up, c->h2d));
+    AG_HIP(hipStreamWaitEvent(c->stream, sl.up, 0));
     const uint8_t* op = npat > 1 ? opres + b0 * k : opres;
     const uint8_t* rp = npat > 1 ? rpres + b0 * m : rpres;
-    if ((st = decode_device(c, k, m, S, n, c->stage_out.as<uint8_t>(), o_b, c->stage_in.as<uint8_t>(), r_b, op, rp,
+    if ((st = decode_device(c, k, m, S, n, sl.out.as<uint8_t>(), o_b, sl.in.as<uint8_t>(), r_b, op, rp,
                             npat > 1 ? n : 1, mode)))
-      return st;
-    AG_HIP(hipMemcpy2DAsync(orig + b0 * ostride, ostride, c->stage_out.ptr, o_b, o_b, n, hipMemcpyDeviceToHost,
-                            c->stream));
-    AG_HIP(hipStreamSynchronize(c->stream));
+      break;
+    AG_HIP(hipEventRecord(sl.done, c->stream));
+    AG_HIP(hipStreamWaitEvent(c->d2h, sl.done, 0));
+    if (down_all) {
+      AG_HIP(hipMemcpy2DAsync(orig + b0 * ostride, ostride, sl.out.ptr, o_b, o_b, n, hipMemcpyDeviceToHost, c->d2h));
+    } else {
+      for (size_t i = 0; i < k; ++i)
+        if (!opres[i])
+          AG_HIP(hipMemcpy2DAsync(orig + b0 * ostride + i * S, ostride, sl.out.as<uint8_t>() + i * S, o_b, S, n,
+                                  hipMemcpyDeviceToHost, c->d2h));
+    }
+    AG_HIP(hipEventRecord(sl.down, c->d2h));
   }
-  return AG_RS_OK;
+  AG_HIP(hipStreamSynchronize(c->stream));
+  AG_HIP(hipStreamSynchronize(c->d2h));
+  return st;
 }
 
 int ag_rs_fill_splitmix(ag_rs_ctx* c, uint8_t* dst, size_t nblocks, size_t block_bytes, size_t dst_stride,

@@ -554,3 +554,45 @@ def test_coder_deshred_batch(ctx, dev, S, mode):
         assert host[b, :len(payload)].tobytes() == payload
         assert host[b, :32 * S].tobytes() == b"".join(raw.data)
         assert host[b, 32 * S:].tobytes() == b"".join(raw.coding)
+
+
+# --------------------------------------------------------- host-memory (PCIe) pipeline
+
+@pytest.mark.parametrize("k,m,S,n", [(32, 32, 32768, 70), (16, 4, 4096, 9), (32, 64, 1024, 5)])
+def test_host_memory_encode_pipeline(ctx, k, m, S, n):
+    """Host buffers, several staging groups (64 MiB each) in flight."""
+    blocks = np.stack([np.frombuffer(o.block_bytes(1300 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    want = ro_c.encode_blocks(blocks, m, threads=8)
+    orig = np.ascontiguousarray(blocks.reshape(n, k * S))
+    rec = np.zeros((n, m * S), np.uint8)
+    rs.encode_batch(ctx, k, m, S, n, orig.ctypes.data, k * S, rec.ctypes.data, m * S, memory=rs.MEM_HOST)
+    assert np.array_equal(rec.reshape(n, m, S), want)
+
+
+@pytest.mark.parametrize("case", ["full_recovery", "lost_coding", "per_block", "exact"])
+def test_host_memory_decode_pipeline(ctx, case):
+    k, m, S, n = 32, 32, 32768, 70
+    rng = random.Random(hash(case) & 0xFFFF)
+    blocks = np.stack([np.frombuffer(o.block_bytes(1400 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    if case == "per_block":
+        op, rp = [], []
+        for b in range(n):
+            lost = rng.sample(range(k), rng.randrange(1, 17))
+            lost_r = rng.sample(range(m), rng.randrange(0, 8))
+            op += [0 if i in lost else 1 for i in range(k)]
+            rp += [0 if j in lost_r else 1 for j in range(m)]
+        opa = np.array(op, np.uint8).reshape(n, k)
+    else:
+        lost = rng.sample(range(k), 16)
+        op = [0 if i in lost else 1 for i in range(k)]
+        rp = [1] * m if case in ("full_recovery", "exact") else [0 if j in (3, 9) else 1 for j in range(m)]
+        opa = np.tile(np.array(op, np.uint8), (n, 1))
+    damaged = blocks.copy()
+    damaged[opa == 0] = 0x6D
+    orig = np.ascontiguousarray(damaged.reshape(n, k * S))
+    recb = np.ascontiguousarray(rec.reshape(n, m * S))
+    mode = rs.DECODE_EXACT if case == "exact" else rs.DECODE_ANY_K
+    rs.decode_batch(ctx, k, m, S, n, orig.ctypes.data, k * S, recb.ctypes.data, m * S, op, rp, mode=mode,
+                    memory=rs.MEM_HOST)
+    assert np.array_equal(orig.reshape(n, k, S), blocks)
