@@ -19,6 +19,12 @@
 
 // Diagnostic builds only (wrong output): bit 0 skips decode_x's input multiply, bit 1 its
 // output multiply, bit 2 the formal derivative.
+// Diagnostic builds only (wrong output): AG_XF_DIAG bit 0 skips the transform's pass C, bit 1
+// keeps waves with nothing to store running through pass C, bit 2 skips the LDS exchanges,
+// bit 3 skips the pass A and B butterflies.
+#ifndef AG_XF_DIAG
+#define AG_XF_DIAG 0
+#endif
 #ifndef AG_DX_DIAG
 #define AG_DX_DIAG 0
 #endif
@@ -324,8 +330,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
   __shared__ uint4 lds[4 * NW * 4 * kXfLanes];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
   Regs8 ra;
-  xf_load_raw(p, tile_io(p, blockIdx.x, lane, p.in_block_stride), wave, ra);
+  xf_load_raw(p, tile_io(p, tile, lane, p.in_block_stride), wave, ra);
   // Store-mask words, fetched now so their latency hides under the data loads.  With
   // one pattern for the batch the word is wave-uniform (scalar load).
   uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
@@ -334,7 +341,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
       const uint64_t m = p.out_mask[0];
       mask[0] = mask[1] = mask[2] = mask[3] = m;
     } else {
-      const TileIO io = tile_io(p, blockIdx.x, lane, p.out_block_stride);
+      const TileIO io = tile_io(p, tile, lane, p.out_block_stride);
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
         mask[q] = p.out_mask[io.blk[q]];
@@ -346,27 +353,298 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
     swap_halves(ra[decltype(T)::value]);
     dev::planes_from_raw(ra[decltype(T)::value]);
   });
+#if !(AG_XF_DIAG & 8)
   xf_pass_a<NW, DIN>(wave, ra);
+#endif
+#if !(AG_XF_DIAG & 4)
   Regs8 rb;
   xf_exchange_ab<NW>(wave, lane, lds, ra, rb);
+#else
+  Regs8& rb = ra;
+#endif
+#if !(AG_XF_DIAG & 8)
   xf_pass_b<NW, DIN, DOUT>(rb);
+#endif
+#if !(AG_XF_DIAG & 4)
   xf_exchange_bc<NW>(wave, lane, lds, rb, ra);
+#endif
 
   // pass C only where some lane of the wave stores one of its 8 shards (a decode restores
   // only the erased originals)
-  const TileIO out_io = tile_io(p, blockIdx.x, lane, p.out_block_stride);
+  const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
   uint32_t need = 0;
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = 8 * wave + t;
     if (s < p.n_out && store_qmask(out_io, mask, s)) need = 1;
   });
+#if !(AG_XF_DIAG & 2)
   if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+#endif
+#if !(AG_XF_DIAG & 1)
   xf_pass_c<NW, DOUT>(wave, ra);
+#endif
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = 8 * wave + t;  // wave-uniform
     if (s < p.n_out) store_shard(p.out + s * p.out_shard_stride, out_io, store_qmask(out_io, mask, s), ra[t]);
+  });
+}
+
+// =====================================================================================
+// xform8: the 32-point transform with 8 waves per workgroup and 4 shard slots per lane.
+// Half the per-lane state of xform<4> (16 loads per lane in flight instead of 32, ~half
+// the VGPRs), so two 8-wave workgroups share a CU and each wave has half the arithmetic
+// between its loads and its stores (tools/membench/membench4.hip: 64-column tile copies
+// 5.57 -> 5.74 TB/s at 8 waves; xform<4> runs at its own load/store skeleton's speed).
+// Every position bit is a slot bit (2) or a wave bit (3), so a layer's skew constant
+// depends only on slot bits (compile time) and wave bits (a scalar switch over the wave
+// bits above the layer).  A layer needs its bit in a slot; between layers one slot bit
+// trades places with one wave bit (x8_swap: partner waves swap half their slots through
+// 64 KiB of LDS; the other half stay in place):
+//   L0 slots p0 p1 | waves p2 p3 p4   IFFT b0 b1            (loads, FFT b0, stores)
+//   L1 slots p2 p1 | waves p0 p3 p4   IFFT b2               (FFT b1)
+//   L2 slots p2 p3 | waves p0 p1 p4   IFFT b3               (FFT b2)
+//   L3 slots p4 p3 | waves p0 p1 p2   IFFT b4, FFT b4 b3
+// =====================================================================================
+using Regs4 = uint32_t[4][16];
+
+template <int L>
+struct X8Layout {  // position bit held by slot bit k (sb) and by wave bit k (wb)
+  static constexpr int sb[2] = {L == 0 ? 0 : L == 3 ? 4 : 2, L >= 2 ? 3 : 1};
+  static constexpr int wb[3] = {L == 0 ? 2 : 0, L == 0 || L == 1 ? 3 : 1, L == 3 ? 2 : 4};
+  static constexpr int pos(int w, int t) {
+    return (((t >> 0) & 1) << sb[0]) | (((t >> 1) & 1) << sb[1]) | (((w >> 0) & 1) << wb[0]) |
+           (((w >> 1) & 1) << wb[1]) | (((w >> 2) & 1) << wb[2]);
+  }
+  static constexpr int slot_of(int b) { return sb[0] == b ? 0 : sb[1] == b ? 1 : -1; }
+  // wave bits whose position bit exceeds b (the ones a layer-b constant depends on)
+  static constexpr int rel(int b) { return (wb[0] > b ? 1 : 0) | (wb[1] > b ? 2 : 0) | (wb[2] > b ? 4 : 0); }
+};
+
+constexpr int x8_popc(int m) { return (m & 1) + ((m >> 1) & 1) + ((m >> 2) & 1); }
+// wave bits selected by REL packed into the low bits, and back
+template <int REL>
+__device__ __forceinline__ int x8_compress(int w) {
+  int v = 0, k = 0;
+  if constexpr (REL & 1) v |= (w & 1) << k++;
+  if constexpr (REL & 2) v |= ((w >> 1) & 1) << k++;
+  if constexpr (REL & 4) v |= ((w >> 2) & 1) << k++;
+  return v;
+}
+constexpr int x8_expand(int v, int rel) {
+  int w = 0, k = 0;
+  for (int j = 0; j < 3; ++j)
+    if ((rel >> j) & 1) w |= ((v >> k++) & 1) << j;
+  return w;
+}
+
+// The butterfly on slots (T, T | 2^i) of layer bit B in layout L for the wave bits V.
+template <int L, int B, bool INV, int DELTA, int T, int V>
+__device__ __forceinline__ void x8_bfly(uint32_t* x, uint32_t* y) {
+  using Lay = X8Layout<L>;
+  constexpr int w = x8_expand(V, Lay::rel(B));
+  constexpr int S = (Lay::pos(w, T) & ~((2 << B) - 1)) + (1 << B) + DELTA - 1;
+  if constexpr (INV) dev::ifft_bfly<S>(x, y); else dev::fft_bfly<S>(x, y);
+}
+template <int L, int B, bool INV, int DELTA, int T>
+__device__ __forceinline__ void x8_bfly_w(int v, uint32_t* x, uint32_t* y) {
+  constexpr int n = 1 << x8_popc(X8Layout<L>::rel(B));
+  if constexpr (n == 1) {
+    x8_bfly<L, B, INV, DELTA, T, 0>(x, y);
+  } else if constexpr (n == 2) {
+    if (v == 0) x8_bfly<L, B, INV, DELTA, T, 0>(x, y); else x8_bfly<L, B, INV, DELTA, T, 1>(x, y);
+  } else if constexpr (n == 4) {
+    switch (v) {
+      case 0: x8_bfly<L, B, INV, DELTA, T, 0>(x, y); break;
+      case 1: x8_bfly<L, B, INV, DELTA, T, 1>(x, y); break;
+      case 2: x8_bfly<L, B, INV, DELTA, T, 2>(x, y); break;
+      default: x8_bfly<L, B, INV, DELTA, T, 3>(x, y); break;
+    }
+  } else {
+    switch (v) {
+      case 0: x8_bfly<L, B, INV, DELTA, T, 0>(x, y); break;
+      case 1: x8_bfly<L, B, INV, DELTA, T, 1>(x, y); break;
+      case 2: x8_bfly<L, B, INV, DELTA, T, 2>(x, y); break;
+      case 3: x8_bfly<L, B, INV, DELTA, T, 3>(x, y); break;
+      case 4: x8_bfly<L, B, INV, DELTA, T, 4>(x, y); break;
+      case 5: x8_bfly<L, B, INV, DELTA, T, 5>(x, y); break;
+      case 6: x8_bfly<L, B, INV, DELTA, T, 6>(x, y); break;
+      default: x8_bfly<L, B, INV, DELTA, T, 7>(x, y); break;
+    }
+  }
+}
+// One butterfly layer on position bit B in layout L (skew delta DELTA).
+template <int L, int B, bool INV, int DELTA>
+__device__ __forceinline__ void x8_layer(int wave, Regs4& r) {
+  constexpr int i = X8Layout<L>::slot_of(B);
+  static_assert(i >= 0, "layer bit must be a slot bit");
+  const int v = x8_compress<X8Layout<L>::rel(B)>(wave);
+  constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;  // the slots with bit i clear
+  x8_bfly_w<L, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)]);
+  x8_bfly_w<L, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)]);
+}
+
+// Slot bit I <-> wave bit J.  Slot t of wave w moves iff t_I != w_J: to slot t ^ 2^I of
+// wave w ^ 2^J, whose outgoing slots are exactly the incoming ones' registers.
+// The branches for t and t ^ 2^I have complementary conditions; the asm markers keep
+// LLVM from merging them into one access through a phi of register-array pointers
+// (which would send the whole slot array to scratch).
+// AG_X8_PAIRSYNC: partner waves synchronise through LDS epoch flags instead of workgroup
+// barriers (ready[w] = last swap whose data w has written, done[w] = last swap w has read).
+#ifndef AG_X8_PAIRSYNC
+#define AG_X8_PAIRSYNC 1
+#endif
+struct X8Flags {
+  uint32_t ready[8];
+  uint32_t done[8];
+};
+__device__ __forceinline__ void x8_wait_ge(const uint32_t* f, uint32_t e) {
+  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < e) __builtin_amdgcn_s_sleep(1);
+}
+__device__ __forceinline__ void x8_signal(uint32_t* f, uint32_t e, int lane) {
+  if (lane == 0) __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+template <int I, int J, int EP>
+__device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, X8Flags* fl, Regs4& r) {
+  const int wj = (wave >> J) & 1;
+  const int partner = wave ^ (1 << J);
+#if AG_X8_PAIRSYNC
+  // region `partner` was last read by the partner in swap EP - 1
+  if constexpr (EP > 1) x8_wait_ge(&fl->done[partner], EP - 1);
+#endif
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    constexpr int k = (t >> (1 - I)) & 1;  // the other slot bit: index within the pair
+    if (((t >> I) & 1) != wj) {
+      lds_put(lds, 2 * partner + k, lane, r[t]);
+      __asm__ volatile("; x8_swap put %0" ::"n"(t));
+    }
+  });
+#if AG_X8_PAIRSYNC
+  x8_signal(&fl->ready[wave], EP, lane);
+  x8_wait_ge(&fl->ready[partner], EP);
+#else
+  __syncthreads();
+#endif
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    constexpr int k = (t >> (1 - I)) & 1;
+    if (((t >> I) & 1) != wj) {
+      lds_get(lds, 2 * wave + k, lane, r[t]);
+      __asm__ volatile("; x8_swap get %0" ::"n"(t));
+    }
+  });
+#if AG_X8_PAIRSYNC
+  x8_signal(&fl->done[wave], EP, lane);
+#else
+  __syncthreads();
+#endif
+}
+
+#ifndef AG_X8_WAVES_PER_EU
+#define AG_X8_WAVES_PER_EU 4
+#endif
+template <int DIN, int DOUT>
+__global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const XformParams p) {
+  __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
+  __shared__ X8Flags flags;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if AG_X8_PAIRSYNC
+  if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
+  __syncthreads();
+#endif
+  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
+  const TileIO io = tile_io(p, tile, lane, p.in_block_stride);
+  Regs4 r;
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t sh = 4 * wave + t;  // LA: wave-uniform
+    if (sh < p.n_in) {
+      const uint8_t* base = p.in + sh * p.in_shard_stride;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        r[t][4 * q] = x.x;
+        r[t][4 * q + 1] = x.y;
+        r[t][4 * q + 2] = x.z;
+        r[t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { r[t][decltype(P)::value] = 0; });
+    }
+  });
+  uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  if (p.out_mask) {
+    if (!p.pattern_per_block) {
+      const uint64_t m = p.out_mask[0];
+      mask[0] = mask[1] = mask[2] = mask[3] = m;
+    } else {
+      const TileIO oi = tile_io(p, tile, lane, p.out_block_stride);
+      static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[oi.blk[decltype(Q)::value]]; });
+    }
+  }
+  static_for<4>([&](auto T) {
+    swap_halves(r[decltype(T)::value]);
+    dev::planes_from_raw(r[decltype(T)::value]);
+  });
+#if !(AG_XF_DIAG & 8)
+  x8_layer<0, 0, true, DIN>(wave, r);
+  x8_layer<0, 1, true, DIN>(wave, r);
+#endif
+#if !(AG_XF_DIAG & 4)
+  x8_swap<0, 0, 1>(wave, lane, lds, &flags, r);
+#endif
+#if !(AG_XF_DIAG & 8)
+  x8_layer<1, 2, true, DIN>(wave, r);
+#endif
+#if !(AG_XF_DIAG & 4)
+  x8_swap<1, 1, 2>(wave, lane, lds, &flags, r);
+#endif
+#if !(AG_XF_DIAG & 8)
+  x8_layer<2, 3, true, DIN>(wave, r);
+#endif
+#if !(AG_XF_DIAG & 4)
+  x8_swap<0, 2, 3>(wave, lane, lds, &flags, r);
+#endif
+#if !(AG_XF_DIAG & 8)
+  x8_layer<3, 4, true, DIN>(wave, r);
+  x8_layer<3, 4, false, DOUT>(wave, r);
+  x8_layer<3, 3, false, DOUT>(wave, r);
+#endif
+#if !(AG_XF_DIAG & 4)
+  x8_swap<0, 2, 4>(wave, lane, lds, &flags, r);
+#endif
+#if !(AG_XF_DIAG & 8)
+  x8_layer<2, 2, false, DOUT>(wave, r);
+#endif
+#if !(AG_XF_DIAG & 4)
+  x8_swap<1, 1, 5>(wave, lane, lds, &flags, r);
+#endif
+#if !(AG_XF_DIAG & 8)
+  x8_layer<1, 1, false, DOUT>(wave, r);
+#endif
+#if !(AG_XF_DIAG & 4)
+  x8_swap<0, 0, 6>(wave, lane, lds, &flags, r);
+#endif
+  const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
+  uint32_t need = 0;
+  static_for<4>([&](auto T) {
+    const uint32_t sh = 4 * wave + decltype(T)::value;
+    if (sh < p.n_out && store_qmask(out_io, mask, sh)) need = 1;
+  });
+#if !(AG_XF_DIAG & 2)
+  if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+#endif
+#if !(AG_XF_DIAG & 1)
+  x8_layer<0, 0, false, DOUT>(wave, r);
+#endif
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t sh = 4 * wave + t;  // wave-uniform
+    if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, store_qmask(out_io, mask, sh), r[t]);
   });
 }
 
@@ -531,7 +809,8 @@ __global__ __launch_bounds__(256, 2) void xform64h_kernel(const XformParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t h = lane >> 5;
   const uint32_t hmask = 0u - h;
-  const TileIO io = tile_io_h(p.total_columns, p.chunks_per_shard, blockIdx.x, lane, p.in_block_stride);
+  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
+  const TileIO io = tile_io_h(p.total_columns, p.chunks_per_shard, tile, lane, p.in_block_stride);
   Regs8 ra;
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
@@ -556,7 +835,7 @@ __global__ __launch_bounds__(256, 2) void xform64h_kernel(const XformParams p) {
       const uint64_t m = p.out_mask[0];
       mask[0] = mask[1] = mask[2] = mask[3] = m;
     } else {
-      const TileIO oi = tile_io_h(p.total_columns, p.chunks_per_shard, blockIdx.x, lane, p.out_block_stride);
+      const TileIO oi = tile_io_h(p.total_columns, p.chunks_per_shard, tile, lane, p.out_block_stride);
       static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[oi.blk[decltype(Q)::value]]; });
     }
   }
@@ -571,7 +850,7 @@ __global__ __launch_bounds__(256, 2) void xform64h_kernel(const XformParams p) {
   x64h_pass_b_fft<DOUT>(rb);
   xf_exchange_bc<4>(wave, lane, lds, rb, ra);
 
-  const TileIO out_io = tile_io_h(p.total_columns, p.chunks_per_shard, blockIdx.x, lane, p.out_block_stride);
+  const TileIO out_io = tile_io_h(p.total_columns, p.chunks_per_shard, tile, lane, p.out_block_stride);
   uint32_t need = 0;
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
@@ -665,11 +944,12 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   // tile -> (pattern, address tile)
-  uint64_t vtile = blockIdx.x, pat = 0;
+  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
+  uint64_t vtile = tile, pat = 0;
   if (p.per_block) {
-    const uint64_t bi = blockIdx.x / p.tiles_per_block;
+    const uint64_t bi = tile / p.tiles_per_block;
     const uint64_t blk = p.block_ids ? p.block_ids[bi] : bi;
-    vtile = blk * p.tiles_per_block + (blockIdx.x - bi * p.tiles_per_block);
+    vtile = blk * p.tiles_per_block + (tile - bi * p.tiles_per_block);
     pat = blk;
   }
   const uint64_t in_mask = p.pmask[2 * pat], out_mask = p.pmask[2 * pat + 1];
@@ -808,7 +1088,7 @@ template <int C>
 __global__ __launch_bounds__(256, 2) void encode_mc_kernel(const XformParams p) {
   constexpr int NCMAX = kMcMaxK / C;
   const int lane = threadIdx.x & 63;
-  const uint64_t tile = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const uint64_t tile = static_cast<uint64_t>(dev::xcd_tile(blockIdx.x, gridDim.x)) * 4 + (threadIdx.x >> 6);
   if (tile * kXfLanes >= p.total_columns) return;  // whole wave
   const TileIO io = tile_io(p, tile, lane, p.in_block_stride);
   const uint32_t nc = (p.n_in + C - 1) / C;
@@ -1172,11 +1452,20 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
   if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const dim3 grid(static_cast<unsigned>(groups));
   switch (kind) {
+    // 32-point: xform<4> encodes (it runs at its load/store skeleton's speed), xform8
+    // reconstructs (half the exposed arithmetic per wave: -8% time).  A/B: variant 3 = xform<4>
+    // for both, variant 4 = xform8 for both.
     case XformKind::kEncode32:
-      hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);
+      if (xform_variant() == 4)
+        hipLaunchKernelGGL((xform8_kernel<32, 0>), grid, dim3(512), 0, stream, p);
+      else
+        hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);
       break;
     case XformKind::kDecode32:
-      hipLaunchKernelGGL((xform_kernel<4, 0, 32>), grid, dim3(256), 0, stream, p);
+      if (xform_variant() == 3)
+        hipLaunchKernelGGL((xform_kernel<4, 0, 32>), grid, dim3(256), 0, stream, p);
+      else
+        hipLaunchKernelGGL((xform8_kernel<0, 32>), grid, dim3(512), 0, stream, p);
       break;
     case XformKind::kEncode64:
       if (xform_variant() == 1)
