@@ -2,7 +2,9 @@
 // engine/tables.rs: LFSR log table, conversion to the Cantor basis, FFT skew factors.
 #include "gf16.hpp"
 
+#include <algorithm>
 #include <memory>
+#include <vector>
 
 namespace ag {
 namespace {
@@ -55,6 +57,53 @@ std::unique_ptr<Gf16Tables> build() {
 const Gf16Tables& gf16_tables() {
   static const std::unique_ptr<Gf16Tables> tables = build();
   return *tables;
+}
+
+namespace {
+
+// The crate's additive FFT / IFFT over one symbol column (indices relative to pos, skew
+// index r + dist + delta - 1).
+void ifft_col(const Gf16Tables& t, uint16_t* w, size_t pos, size_t size, size_t trunc, size_t delta) {
+  for (size_t dist = 1; dist < size; dist <<= 1)
+    for (size_t r = 0; r < trunc; r += 2 * dist) {
+      const uint16_t lm = t.skew[r + dist + delta - 1];
+      for (size_t i = r; i < r + dist; ++i) {
+        uint16_t &x = w[pos + i], &y = w[pos + i + dist];
+        y ^= x;
+        if (lm != kGfModulus) x ^= gf_mul(t, y, lm);
+      }
+    }
+}
+void fft_col(const Gf16Tables& t, uint16_t* w, size_t pos, size_t size, size_t trunc, size_t delta) {
+  for (size_t dist = size >> 1; dist >= 1; dist >>= 1)
+    for (size_t r = 0; r < trunc; r += 2 * dist) {
+      const uint16_t lm = t.skew[r + dist + delta - 1];
+      for (size_t i = r; i < r + dist; ++i) {
+        uint16_t &x = w[pos + i], &y = w[pos + i + dist];
+        if (lm != kGfModulus) x ^= gf_mul(t, y, lm);
+        y ^= x;
+      }
+    }
+}
+
+}  // namespace
+
+void hr_generator(size_t k, size_t m, uint16_t* G) {
+  const Gf16Tables& t = gf16_tables();
+  const size_t chunk = next_pow2(m);
+  const size_t rows = std::max(chunk, (k + chunk - 1) / chunk * chunk);
+  std::vector<uint16_t> w(rows);
+  for (size_t i = 0; i < k; ++i) {
+    std::fill(w.begin(), w.end(), uint16_t{0});
+    w[i] = 1;
+    ifft_col(t, w.data(), 0, chunk, std::min(k, chunk), chunk);
+    for (size_t cs = chunk; cs < k; cs += chunk) {  // further (possibly partial) chunks
+      ifft_col(t, w.data(), cs, chunk, std::min(chunk, k - cs), cs + chunk);
+      for (size_t j = 0; j < chunk; ++j) w[j] ^= w[cs + j];
+    }
+    fft_col(t, w.data(), 0, chunk, m, 0);
+    for (size_t j = 0; j < m; ++j) G[j * k + i] = w[j];
+  }
 }
 
 int use_high_rate(size_t k, size_t m) {

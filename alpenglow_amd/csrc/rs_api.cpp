@@ -105,6 +105,7 @@ struct ag_rs_ctx {
   DevBuf scratch;                         // generic-kernel work rows
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
+  DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
   // host-memory calls: two staging slots, H2D / D2H streams next to the compute stream
@@ -117,6 +118,7 @@ struct ag_rs_ctx {
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
   std::vector<uint64_t> xmask_host;       // last general-decode masks (d_xmask), W = xmask_w
   size_t xmask_w = 0;
+  std::vector<uint8_t> syn_key;             // (k, m, present flags) of the patterns in d_syn
 
   int enter() { return hipSetDevice(device) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE; }
 
@@ -182,7 +184,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
                       &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -196,6 +198,53 @@ constexpr size_t kStageGroupBytes = size_t{64} << 20;
 
 // Scratch budget of the generic kernels (per launch).
 constexpr size_t kGenericScratchBytes = size_t{512} << 20;
+
+// Syndrome-decoder pattern (decode_syn_kernel): restore the erased originals from the
+// first e present recovery shards.  Returns false if the e x e system is singular (cannot
+// happen for an MDS code; the caller then takes another decoder).
+bool build_syn_pattern(size_t k, size_t m, const uint8_t* opres, const uint8_t* rpres, const uint16_t* G,
+                       ag::SynPattern* sp) {
+  const ag::Gf16Tables& t = ag::gf16_tables();
+  std::memset(sp, 0, sizeof *sp);
+  size_t e = 0, r = 0;
+  for (size_t i = 0; i < k; ++i) {
+    if (opres[i]) sp->dmask |= uint64_t{1} << i;
+    else if (e < 4) sp->out[e++] = static_cast<uint8_t>(i);
+    else return false;
+  }
+  for (size_t j = 0; j < m && r < e; ++j)
+    if (rpres[j]) sp->rec[r++] = static_cast<uint8_t>(j);
+  if (r < e) return false;
+  sp->e = static_cast<uint32_t>(e);
+  // A[b][a] = G[rec[b]][out[a]]; Gauss-Jordan inverse over GF(2^16)
+  uint16_t A[4][8] = {};
+  for (size_t b = 0; b < e; ++b) {
+    for (size_t a = 0; a < e; ++a) A[b][a] = G[sp->rec[b] * k + sp->out[a]];
+    A[b][e + b] = 1;
+  }
+  for (size_t col = 0; col < e; ++col) {
+    size_t piv = col;
+    while (piv < e && A[piv][col] == 0) ++piv;
+    if (piv == e) return false;
+    if (piv != col)
+      for (size_t x = 0; x < 2 * e; ++x) std::swap(A[piv][x], A[col][x]);
+    const uint16_t inv = ag::gf_inv(t, A[col][col]);
+    for (size_t x = 0; x < 2 * e; ++x) A[col][x] = ag::gf_mul_elem(t, A[col][x], inv);
+    for (size_t row = 0; row < e; ++row) {
+      if (row == col || A[row][col] == 0) continue;
+      const uint16_t f = A[row][col];
+      for (size_t x = 0; x < 2 * e; ++x) A[row][x] ^= ag::gf_mul_elem(t, f, A[col][x]);
+    }
+  }
+  // Minv[a][b] = A[a][e + b]; bitsliced matrix rows[o] bit i = bit o of (Minv * 2^i)
+  for (size_t a = 0; a < e; ++a)
+    for (size_t b = 0; b < e; ++b)
+      for (unsigned i = 0; i < 16; ++i) {
+        const uint16_t prod = ag::gf_mul_elem(t, A[a][e + b], static_cast<uint16_t>(1u << i));
+        for (unsigned o = 0; o < 16; ++o) sp->rows[a][b][o] |= ((prod >> o) & 1u) << i;
+      }
+  return true;
+}
 
 int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
                   size_t ostride, uint8_t* rec, size_t rstride) {
@@ -282,7 +331,17 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   // decode_x: HighRate, W in {32, 64}; one pattern per tile (single pattern, or tiles
   // that never straddle blocks)
   const bool x_geo = hr == 1 && S % 64 == 0 && (xw == 32 || xw == 64) && aligned && (npat == 1 || cps % 64 == 0);
-  bool any_fast = false, any_generic = false, any_x = false;
+  // decode_syn: the encode_mc geometries (chunk <= 4), any k survivors, same tiling rule
+  const unsigned syn_chunk = mode == AG_RS_DECODE_ANY_K && aligned && (npat == 1 || cps % 64 == 0)
+                                 ? mc_chunk(k, m, S) : 0;
+  std::vector<uint16_t> G;
+  if (syn_chunk) {
+    G.resize(m * k);
+    ag::hr_generator(k, m, G.data());
+  }
+  std::vector<ag::SynPattern> syn;
+  if (syn_chunk) syn.resize(npat);
+  bool any_fast = false, any_generic = false, any_x = false, any_syn = false;
   for (size_t p = 0; p < npat; ++p) {
     size_t no = 0, nr = 0;
     for (size_t i = 0; i < k; ++i) no += opres[p * k + i] != 0;
@@ -293,6 +352,9 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     } else if (fast_geo && nr == m) {
       cls[p] = 1;
       any_fast = true;
+    } else if (syn_chunk && build_syn_pattern(k, m, opres + p * k, rpres + p * m, G.data(), &syn[p])) {
+      cls[p] = 4;
+      any_syn = true;
     } else if (x_geo) {
       cls[p] = 3;
       any_x = true;
@@ -331,6 +393,53 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
     const auto kind = npts == 32 ? ag::XformKind::kDecode32 : ag::XformKind::kDecode64;
     if (ag::launch_xform(kind, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
+  if (any_syn) {
+    // pattern upload only when (k, m, flags) changed; non-syndrome patterns stay zeroed
+    std::vector<uint8_t> key(16 + npat * (k + m));
+    const uint64_t km[2] = {k, m};
+    std::memcpy(key.data(), km, 16);
+    for (size_t p = 0; p < npat; ++p) {
+      if (cls[p] != 4) continue;
+      std::memcpy(&key[16 + p * (k + m)], opres + p * k, k);
+      std::memcpy(&key[16 + p * (k + m) + k], rpres + p * m, m);
+    }
+    if (key != c->syn_key) {
+      for (size_t p = 0; p < npat; ++p)
+        if (cls[p] != 4) std::memset(&syn[p], 0, sizeof syn[p]);
+      AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read d_syn
+      if ((st = c->d_syn.ensure(npat * sizeof(ag::SynPattern), c->stream))) return st;
+      AG_HIP(hipMemcpy(c->d_syn.ptr, syn.data(), npat * sizeof(ag::SynPattern), hipMemcpyHostToDevice));
+      c->syn_key = key;
+    }
+    ag::DecodeSynParams p{};
+    p.rec = rec;
+    p.rec_block_stride = rstride;
+    p.rec_shard_stride = S;
+    p.orig = orig;
+    p.orig_block_stride = ostride;
+    p.orig_shard_stride = S;
+    p.pat = c->d_syn.as<ag::SynPattern>();
+    p.k = static_cast<uint32_t>(k);
+    p.chunks_per_shard = static_cast<uint32_t>(cps);
+    p.total_columns = static_cast<uint64_t>(nblocks) * cps;
+    if (npat == 1) {
+      p.ntiles = (p.total_columns + 63) / 64;
+    } else {
+      p.per_block = 1;
+      p.tiles_per_block = static_cast<uint32_t>(cps / 64);
+      std::vector<uint32_t> ids;
+      for (size_t b = 0; b < nblocks; ++b)
+        if (cls[b] == 4) ids.push_back(static_cast<uint32_t>(b));
+      if (ids.size() != nblocks) {
+        AG_HIP(hipStreamSynchronize(c->stream));  // a previous id upload may be pending
+        if ((st = c->d_synblocks.ensure(ids.size() * 4, c->stream))) return st;
+        AG_HIP(hipMemcpy(c->d_synblocks.ptr, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+        p.block_ids = c->d_synblocks.as<uint32_t>();
+      }
+      p.ntiles = static_cast<uint64_t>(ids.size()) * p.tiles_per_block;
+    }
+    if (ag::launch_decode_syn(syn_chunk, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   }
   if (any_x) {
     if ((st = c->ensure_tables())) return st;

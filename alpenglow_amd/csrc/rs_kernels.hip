@@ -25,6 +25,9 @@
 #ifndef AG_XF_DIAG
 #define AG_XF_DIAG 0
 #endif
+#ifndef AG_SYN_DIAG
+#define AG_SYN_DIAG 0
+#endif
 #ifndef AG_DX_DIAG
 #define AG_DX_DIAG 0
 #endif
@@ -1123,6 +1126,190 @@ __global__ __launch_bounds__(256, 2) void encode_mc_kernel(const XformParams p) 
 }
 
 // =====================================================================================
+// decode_syn<C>: syndrome decoder for small recovery sets (chunk C = next_pow2(m) <= 4,
+// k <= kMcMaxK).  One wave per 64-column tile, no LDS.  The wave re-encodes the present
+// originals exactly as encode_mc does (erased originals read as zero), adds e received
+// recovery shards (syndromes S_b = received_b ^ re-encoded_b = sum over erased a of
+// G[b][a] * original_a) and restores original E[a] = sum_b Minv[a][b] S_b with e^2 runtime
+// multiplies.  Any correct decoder returns the crate's originals on a valid codeword (MDS).
+// =====================================================================================
+typedef uint32_t u32x16 __attribute__((ext_vector_type(16)));
+
+// the 16 XOR combinations of planes x[0..3] (entry v = XOR of x[i] for the bits i of v)
+__device__ __forceinline__ u32x16 syn_table(const uint32_t* x) {
+  const uint32_t a = x[0], b = x[1], c = x[2], d = x[3];
+  const uint32_t ab = a ^ b, cd = c ^ d;
+  return u32x16{0u, a, b, ab, c, a ^ c, b ^ c, ab ^ c, d, a ^ d, b ^ d, ab ^ d, cd, a ^ cd, b ^ cd, ab ^ cd};
+}
+
+// acc ^= M x for a runtime 16x16 GF(2) matrix in (wave-uniform) global memory
+__device__ __forceinline__ void mul_rt_acc(uint32_t* acc, const uint32_t* x, const uint32_t* __restrict__ rows) {
+  static_for<16>([&](auto O) {
+    constexpr int o = decltype(O)::value;
+    const uint32_t r = __builtin_amdgcn_readfirstlane(rows[o]);
+    uint32_t a = acc[o];
+    static_for<16>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const uint32_t msk = static_cast<uint32_t>(static_cast<int32_t>(r << (31 - i)) >> 31);
+      a = __builtin_amdgcn_bitop3_b32(a, x[i], msk, 0x78);  // a ^ (x & msk)
+    });
+    acc[o] = a;
+  });
+}
+
+template <int C>
+__device__ __forceinline__ void syn_load(const DecodeSynParams& p, const TileIO& io, uint64_t dmask, uint32_t s0,
+                                         uint32_t (&raw)[C][16]) {
+  static_for<C>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = s0 + t;
+    if (s < p.k && ((dmask >> s) & 1)) {  // wave-uniform
+      const uint8_t* base = p.orig + s * p.orig_shard_stride;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        raw[t][4 * q] = x.x;
+        raw[t][4 * q + 1] = x.y;
+        raw[t][4 * q + 2] = x.z;
+        raw[t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { raw[t][decltype(P)::value] = 0; });
+    }
+  });
+}
+
+template <int C>
+__global__ __launch_bounds__(256, 2) void decode_syn_kernel(const DecodeSynParams p) {
+  constexpr int NCMAX = kMcMaxK / C;
+  __shared__ uint32_t stab[4][64 * 64];  // per wave: 4 groups x 16 entries x 64 lanes
+  const int lane = threadIdx.x & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  uint64_t tile = static_cast<uint64_t>(dev::xcd_tile(blockIdx.x, gridDim.x)) * 4 + wave;
+  if (tile >= p.ntiles) return;  // whole wave
+  uint64_t pat = 0;
+  if (p.per_block) {
+    const uint64_t bi = tile / p.tiles_per_block;
+    const uint64_t blk = p.block_ids ? p.block_ids[bi] : bi;
+    tile = blk * p.tiles_per_block + (tile - bi * p.tiles_per_block);
+    pat = blk;
+  }
+  const SynPattern* sp = p.pat + pat;
+  const uint64_t dmask = sp->dmask;
+  const uint32_t e = sp->e;
+  const TileIO io = tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, p.orig_block_stride);
+  const uint32_t nc = (p.k + C - 1) / C;
+  uint32_t acc[C][16];
+  uint32_t raw[2][C][16];
+  syn_load<C>(p, io, dmask, 0, raw[0]);
+  static_for<NCMAX>([&](auto Cc) {
+    constexpr int c = decltype(Cc)::value;
+    if (c < nc) {
+      if (c + 1 < nc) syn_load<C>(p, io, dmask, (c + 1) * C, raw[(c + 1) & 1]);
+      auto& cur = raw[c & 1];
+      static_for<C>([&](auto T) {
+        swap_halves(cur[decltype(T)::value]);
+        dev::planes_from_raw(cur[decltype(T)::value]);
+      });
+      xform_lane<C, C * (c + 1), true>(cur);
+      static_for<C>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        static_for<16>([&](auto P) {
+          constexpr int q = decltype(P)::value;
+          if constexpr (c == 0) acc[t][q] = cur[t][q]; else acc[t][q] ^= cur[t][q];
+        });
+      });
+    }
+  });
+  xform_lane<C, 0, false>(acc);  // re-encoded recovery shards 0..C-1
+  // syndromes S_b (b < e) into raw[0][b]
+  const TileIO rio = tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, p.rec_block_stride);
+  static_for<C>([&](auto B) {
+    constexpr int b = decltype(B)::value;
+    if (b < e) {
+      const uint32_t j = sp->rec[b];  // wave-uniform
+      const uint8_t* base = p.rec + j * p.rec_shard_stride;
+      uint32_t* sb = raw[0][b];
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = *reinterpret_cast<const uint4*>(base + rio.off[q]);
+        sb[4 * q] = x.x;
+        sb[4 * q + 1] = x.y;
+        sb[4 * q + 2] = x.z;
+        sb[4 * q + 3] = x.w;
+      });
+      swap_halves(sb);
+      dev::planes_from_raw(sb);
+      static_for<C>([&](auto J) {
+        constexpr int jj = decltype(J)::value;
+        if (j == jj) dev::xor_planes(sb, acc[jj]);
+      });
+    }
+  });
+#if AG_SYN_DIAG & 2  // bit-matrix form: one v_bitop3 per matrix entry
+  static_for<C>([&](auto A) {
+    constexpr int a = decltype(A)::value;
+    if (a < e) {
+      uint32_t out[16];
+      static_for<16>([&](auto P) { out[decltype(P)::value] = 0; });
+      static_for<C>([&](auto B) {
+        constexpr int b = decltype(B)::value;
+        if (b < e) mul_rt_acc(out, raw[0][b], sp->rows[a][b]);
+      });
+      store_shard(p.orig + sp->out[a] * p.orig_shard_stride, io, io.valid, out);
+    }
+  });
+#else
+  // Four Russians: per syndrome, the 16 XOR combinations of each 4-plane group go to this
+  // wave's LDS table (entry-major, lane-minor: conflict-free); output plane o of
+  // Minv[a][b] S_b is then 4 table reads at the nibbles of row o (wave-uniform offsets).
+  // Outputs go in pairs so that 2 x 16 accumulators and the syndromes fit the registers.
+  constexpr int NP = C >= 2 ? 2 : 1;
+  uint32_t* tb = stab[wave];
+  static_for<(C + NP - 1) / NP>([&](auto Pp) {
+    constexpr int a0 = NP * decltype(Pp)::value;
+    if (a0 < e) {
+      uint32_t out[NP][16];
+      static_for<NP>([&](auto A) { static_for<16>([&](auto P) { out[decltype(A)::value][decltype(P)::value] = 0; }); });
+      static_for<C>([&](auto B) {
+        constexpr int b = decltype(B)::value;
+        if (b < e) {
+          const uint32_t* x = raw[0][b];
+          static_for<4>([&](auto G) {
+            constexpr int g = decltype(G)::value;
+            const u32x16 t = syn_table(x + 4 * g);
+            static_for<16>([&](auto V) { tb[(16 * g + decltype(V)::value) * 64 + lane] = t[decltype(V)::value]; });
+          });
+          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+          static_for<NP>([&](auto A) {
+            constexpr int da = decltype(A)::value;
+            if (a0 + da < e) {
+              const uint32_t* rows = sp->rows[a0 + da][b];
+              static_for<16>([&](auto O) {
+                constexpr int o = decltype(O)::value;
+                const uint32_t r = __builtin_amdgcn_readfirstlane(rows[o]);
+                const uint32_t t0 = tb[(r & 15) * 64 + lane], t1 = tb[(16 + ((r >> 4) & 15)) * 64 + lane];
+                const uint32_t t2 = tb[(32 + ((r >> 8) & 15)) * 64 + lane];
+                const uint32_t t3 = tb[(48 + ((r >> 12) & 15)) * 64 + lane];
+                out[da][o] = dev::xor3(out[da][o], t0, t1) ^ dev::xor3(t2, t3, 0u);
+              });
+            }
+          });
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+          __builtin_amdgcn_wave_barrier();
+        }
+      });
+      static_for<NP>([&](auto A) {
+        constexpr int da = decltype(A)::value;
+        if (a0 + da < e) store_shard(p.orig + sp->out[a0 + da] * p.orig_shard_stride, io, io.valid, out[da]);
+      });
+    }
+  });
+#endif
+}
+
+// =====================================================================================
 // Generic kernels: one thread per (block, symbol position); the crate's algorithm with
 // log/exp tables, work rows in a global scratch column (stride nsym).
 // =====================================================================================
@@ -1441,6 +1628,21 @@ hipError_t launch_encode_mc(unsigned chunk, const XformParams& p, hipStream_t st
     case 1: hipLaunchKernelGGL((encode_mc_kernel<1>), grid, dim3(256), 0, stream, p); break;
     case 2: hipLaunchKernelGGL((encode_mc_kernel<2>), grid, dim3(256), 0, stream, p); break;
     case 4: hipLaunchKernelGGL((encode_mc_kernel<4>), grid, dim3(256), 0, stream, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_decode_syn(unsigned chunk, const DecodeSynParams& p, hipStream_t stream) {
+  if (p.ntiles == 0) return hipSuccess;
+  if (p.k > static_cast<uint32_t>(kMcMaxK)) return hipErrorInvalidValue;
+  const uint64_t groups = (p.ntiles + 3) / 4;
+  if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<unsigned>(groups));
+  switch (chunk) {
+    case 1: hipLaunchKernelGGL((decode_syn_kernel<1>), grid, dim3(256), 0, stream, p); break;
+    case 2: hipLaunchKernelGGL((decode_syn_kernel<2>), grid, dim3(256), 0, stream, p); break;
+    case 4: hipLaunchKernelGGL((decode_syn_kernel<4>), grid, dim3(256), 0, stream, p); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -37,6 +37,36 @@ hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hi
 // in = originals (n_in = k), out = recovery (n_out = m).  out_mask unused.
 hipError_t launch_encode_mc(unsigned chunk, const XformParams& p, hipStream_t stream);
 
+// Syndrome decoder for HighRate geometries with chunk = next_pow2(m) <= 4, k <= 64 (the
+// encode_mc domain), any k survivors: re-encode the present originals (erased ones read as
+// zero), XOR with e received recovery shards -> syndromes S, restore the e <= 4 erased
+// originals as Minv S (Minv = inverse of the generator's e x e erased/used submatrix).
+struct SynPattern {
+  uint64_t dmask;           // originals present (loaded)
+  uint32_t e;               // originals restored (<= 4)
+  uint8_t rec[4];           // recovery shards used for the syndromes
+  uint8_t out[4];           // erased originals
+  uint32_t pad;
+  uint32_t rows[4][4][16];  // Minv[a][b] as 16x16 GF(2) matrices (rows[o] bit i)
+};
+struct DecodeSynParams {
+  const uint8_t* rec;
+  uint64_t rec_block_stride;
+  uint64_t rec_shard_stride;
+  uint8_t* orig;  // present originals are read, restored ones written here
+  uint64_t orig_block_stride;
+  uint64_t orig_shard_stride;
+  const SynPattern* pat;      // [pattern]
+  const uint32_t* block_ids;  // per_block: blocks processed (null = 0..)
+  uint32_t per_block;         // 1: pattern = block; tiles_per_block 64-column tiles per block
+  uint32_t tiles_per_block;
+  uint32_t k;
+  uint32_t chunks_per_shard;
+  uint64_t total_columns;  // batch blocks * chunks_per_shard
+  uint64_t ntiles;         // 64-column tiles processed
+};
+hipError_t launch_decode_syn(unsigned chunk, const DecodeSynParams& p, hipStream_t stream);
+
 struct GfDeviceTables {
   const uint16_t* exp;
   const uint16_t* log;

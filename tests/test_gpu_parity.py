@@ -264,6 +264,47 @@ def test_general_decode_per_block_patterns(ctx, dev, k, m, S, n):
         assert np.array_equal(got, blocks), mode
 
 
+@pytest.mark.parametrize("k,m,S,n", [(16, 4, 4096, 6), (16, 3, 640, 5), (13, 4, 128, 7), (64, 4, 1024, 3),
+                                     (5, 2, 64, 9), (9, 1, 192, 4), (17, 2, 4096, 3), (16, 4, 64, 33)])
+def test_syndrome_decode_one_pattern(ctx, dev, k, m, S, n):
+    """Syndrome decoder (decode_syn: m <= 4, ANY_K): every erasure count 1..m - lost
+    recovery, lost recovery shards, tiles straddling blocks (S < 4 KiB)."""
+    rng = random.Random(k * 7 + m * 3 + S)
+    blocks = np.stack([np.frombuffer(o.block_bytes(1300 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    for lr in range(0, m):
+        for e in range(1, m - lr + 1):
+            lost, lost_r = rng.sample(range(k), e), rng.sample(range(m), lr)
+            damaged = blocks.copy()
+            damaged[:, lost] = 0x5A
+            op = [0 if i in lost else 1 for i in range(k)]
+            rp = [0 if j in lost_r else 1 for j in range(m)]
+            got = gpu_decode(ctx, dev, damaged, rec, op, rp, rs.DECODE_ANY_K)
+            assert np.array_equal(got, blocks), (lost, lost_r)
+
+
+@pytest.mark.parametrize("k,m,S,n", [(16, 4, 4096, 10), (64, 4, 4096, 5), (16, 2, 8192, 7)])
+def test_syndrome_decode_per_block_patterns(ctx, dev, k, m, S, n):
+    """Random pattern per block through the syndrome decoder (block-aligned tiles)."""
+    rng = random.Random(k + 5 * m + n)
+    blocks, rec, damaged, op, rp = _random_pattern_case(rng, k, m, S, n, 1400, lose_rec=m // 2)
+    got = gpu_decode(ctx, dev, damaged, rec, op, rp, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
+
+
+def test_syndrome_decode_pattern_cache(ctx, dev):
+    """Back-to-back syndrome decodes with different patterns of one shape."""
+    k, m, S, n = 16, 4, 4096, 3
+    blocks = np.stack([np.frombuffer(o.block_bytes(1500 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    for lost, lost_r in [([0, 1, 2, 3], []), ([15], [0, 1, 2]), ([0, 1, 2, 3], []), ([4, 9], [3]), ([15], [0, 1, 2])]:
+        damaged = blocks.copy()
+        damaged[:, lost] = 0
+        op = [0 if i in lost else 1 for i in range(k)]
+        rp = [0 if j in lost_r else 1 for j in range(m)]
+        assert np.array_equal(gpu_decode(ctx, dev, damaged, rec, op, rp, rs.DECODE_ANY_K), blocks)
+
+
 def test_general_decode_pattern_cache(ctx, dev):
     """Back-to-back calls with different patterns of the same shape must not reuse stale
     per-pattern matrices."""
