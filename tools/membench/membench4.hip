@@ -248,6 +248,49 @@ __global__ void tcpp(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, 
   if (acc == 0x12345) pad[0] = acc;
 }
 
+// NC64 tile copy (4 or 8 waves), XCD-contiguous tile ranges with an in-XCD order MODE:
+//   0: consecutive tiles;  1: block-strided (consecutive workgroups take the same tile of
+//   consecutive blocks);  2: consecutive, stores non-temporal;  3: consecutive, loads nt
+template <int NWV, int NWR, int MODE>
+__global__ void tcpm(const uint8_t* __restrict__ in, uint8_t* __restrict__ out, uint32_t S) {
+  extern __shared__ int pad[];
+  constexpr int NC = 64, K = 32, SH = K / NWV, Q = 4;
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  const uint32_t x = b & 7, q8 = G >> 3;
+  const uint32_t i = b >> 3;  // G % 8 == 0 here
+  const uint32_t tiles_per_shard = S / (64 * NC);
+  uint32_t L;
+  if (MODE == 1) {
+    const uint32_t nb = q8 / tiles_per_shard;  // blocks per XCD
+    L = x * q8 + (i % nb) * tiles_per_shard + i / nb;
+  } else {
+    L = x * q8 + i;
+  }
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const size_t bstride = (size_t)2 * K * S;
+  const uint32_t blk = L / tiles_per_shard, tt = L % tiles_per_shard;
+  const uint8_t* src = in + blk * bstride + (size_t)tt * NC * 64 + lane * 16;
+  uint8_t* dst = out + blk * bstride + (size_t)K * S + (size_t)tt * NC * 64 + lane * 16;
+  u32x4 v[SH][Q];
+#pragma unroll
+  for (int s = 0; s < SH; ++s)
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const u32x4* ptr = reinterpret_cast<const u32x4*>(src + (size_t)(wave * SH + s) * S + q * 1024);
+      v[s][q] = MODE == 3 ? __builtin_nontemporal_load(ptr) : *ptr;
+    }
+  if (v[0][0].x == 0xdeadbeef && threadIdx.x == 1000) pad[0] = 1;
+  if (wave * SH < NWR) {
+#pragma unroll
+    for (int s = 0; s < SH; ++s)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        u32x4* ptr = reinterpret_cast<u32x4*>(dst + (size_t)(wave * SH + s) * S + q * 1024);
+        if (MODE == 2) __builtin_nontemporal_store(v[s][q], ptr); else *ptr = v[s][q];
+      }
+  }
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP error %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
 
 static hipEvent_t e0, e1;
@@ -297,8 +340,11 @@ int main(int argc, char** argv) {
   snprintf(nm, sizeof nm, "tcpp waves%d wg/cu=%d D%d write%d", NWV, WPC, D, NWR);                     \
   timeit(nm, (double)nblk * (32 + NWR) * S, [&] { hipLaunchKernelGGL((tcpp<NWV, WPC, D, NWR>), dim3(256 * WPC), \
                                           dim3(64 * NWV), lds_for_wg[WPC], 0, (const uint8_t*)a, (uint8_t*)a, S, (uint32_t)(nblk * (S / 4096))); });
-  TW(64, 8, 32, 1) TW(64, 8, 16, 1) TW(64, 4, 32, 2) TW(64, 4, 16, 2)
-  TP(8, 1, 0, 32) TP(8, 1, 2000, 32) TP(8, 2, 0, 32) TP(8, 2, 1000, 32) TP(4, 2, 0, 32) TP(4, 2, 2000, 32) TP(4, 1, 0, 32)
-  TP(8, 1, 0, 16) TP(8, 1, 2000, 16) TP(8, 2, 0, 16) TP(4, 2, 0, 16) TP(4, 2, 2000, 16)
+#define TM(NWV, NWR, MODE, W)                                                                          \
+  snprintf(nm, sizeof nm, "tcpm waves%d write%d mode%d wg/cu<=%d", NWV, NWR, MODE, W);                 \
+  timeit(nm, (double)nblk * (32 + NWR) * S, [&] { hipLaunchKernelGGL((tcpm<NWV, NWR, MODE>), dim3(nblk * (S / 4096)), \
+                                          dim3(64 * NWV), lds_for_wg[W], 0, (const uint8_t*)a, (uint8_t*)a, S); });
+  TM(4, 32, 0, 2) TM(4, 32, 1, 2) TM(4, 32, 2, 2) TM(4, 32, 3, 2) TM(8, 32, 0, 2) TM(8, 32, 1, 2) TM(8, 32, 2, 2)
+  TM(4, 16, 0, 2) TM(4, 16, 1, 2) TM(8, 16, 0, 2) TM(8, 16, 1, 2) TM(8, 16, 3, 2)
   return 0;
 }
