@@ -579,16 +579,6 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
       static_for<16>([&](auto P) { r[t][decltype(P)::value] = 0; });
     }
   });
-  uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-  if (p.out_mask) {
-    if (!p.pattern_per_block) {
-      const uint64_t m = p.out_mask[0];
-      mask[0] = mask[1] = mask[2] = mask[3] = m;
-    } else {
-      const TileIO oi = tile_io(p, tile, lane, p.out_block_stride);
-      static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[oi.blk[decltype(Q)::value]]; });
-    }
-  }
   static_for<4>([&](auto T) {
     swap_halves(r[decltype(T)::value]);
     dev::planes_from_raw(r[decltype(T)::value]);
@@ -632,7 +622,17 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
 #if !(AG_XF_DIAG & 4)
   x8_swap<0, 0, 6>(wave, lane, lds, &flags, r);
 #endif
+  // store masks fetched only now: live across the transform they cost registers (spills)
   const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
+  uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+  if (p.out_mask) {
+    if (!p.pattern_per_block) {
+      const uint64_t m = p.out_mask[0];
+      mask[0] = mask[1] = mask[2] = mask[3] = m;
+    } else {
+      static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[out_io.blk[decltype(Q)::value]]; });
+    }
+  }
   uint32_t need = 0;
   static_for<4>([&](auto T) {
     const uint32_t sh = 4 * wave + decltype(T)::value;
