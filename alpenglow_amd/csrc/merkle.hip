@@ -1,0 +1,347 @@
+// Slice Merkle trees on the GPU.
+//
+// What it replaces: the reference builds one SHA-256 Merkle tree per slice over its 64
+// shreds (data shreds, then coding shreds; shredder.rs:628-632 build_merkle_tree) with
+// MerkleTree::new (crypto/merkle.rs:281-333), takes the root (:337) and one proof per shred
+// (create_proof, :351-370); receivers check proofs (check_proof / derive_root, :374-425)
+// and rebuild the tree after decoding (check_merkle_tree, shredder.rs:616-626).
+//   leaf  = SHA-256(LEAF_LABEL || shred bytes)                      (merkle.rs:457-460)
+//   inner = SHA-256(LEFT_LABEL || left || RIGHT_LABEL || right)     (merkle.rs:466-468)
+//   an odd node at height h pairs with EMPTY_ROOTS[h]               (merkle.rs:312-315)
+// SHA-256 is the sha2 crate's (crypto/hash.rs:64-79); here it is a plain FIPS 180-4
+// implementation shared by host and device.
+//
+// Kernels
+//   merkle_slices_kernel  one wave per slice: lane i hashes leaf i, the tree levels are
+//                         built in the wave's LDS, lane i writes its own proof.  Integer
+//                         VALU-bound (~2.6k VALU per 64-byte SHA block per lane).
+//   merkle_verify_kernel  one thread per (leaf, index, root, proof): derive_root == root.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstring>
+
+#include "merkle.hpp"
+
+namespace ag {
+namespace sha {
+
+__host__ __device__ constexpr uint32_t kK[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+__host__ __device__ constexpr uint32_t kIv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+                                                 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+
+// The 32-byte labels of merkle.rs:42-44 as big-endian message words.
+struct Label {
+  uint32_t w[8];
+};
+__host__ __device__ constexpr Label make_label(const char (&s)[33]) {
+  Label l{};
+  for (int i = 0; i < 8; ++i)
+    l.w[i] = (uint32_t(uint8_t(s[4 * i])) << 24) | (uint32_t(uint8_t(s[4 * i + 1])) << 16) |
+             (uint32_t(uint8_t(s[4 * i + 2])) << 8) | uint32_t(uint8_t(s[4 * i + 3]));
+  return l;
+}
+__host__ __device__ constexpr Label kLeafLabel = make_label("ALPENGLOW-MERKLE-TREE  LEAF-NODE");
+__host__ __device__ constexpr Label kLeftLabel = make_label("ALPENGLOW-MERKLE-TREE  LEFT-NODE");
+__host__ __device__ constexpr Label kRightLabel = make_label("ALPENGLOW-MERKLE-TREE RIGHT-NODE");
+
+__host__ __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+__host__ __device__ __forceinline__ uint32_t bswap(uint32_t x) {
+  return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
+}
+
+// One SHA-256 compression of the 16 big-endian words w (consumed as the schedule).
+__host__ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]) {
+  uint32_t a = st[0], b = st[1], c = st[2], d = st[3], e = st[4], f = st[5], g = st[6], h = st[7];
+#pragma unroll
+  for (int r = 0; r < 64; ++r) {
+    uint32_t wr;
+    if (r < 16) {
+      wr = w[r];
+    } else {
+      const uint32_t w15 = w[(r + 1) & 15], w2 = w[(r + 14) & 15];
+      const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
+      const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+      wr = w[r & 15] = w[r & 15] + s0 + w[(r + 9) & 15] + s1;
+    }
+    const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+    const uint32_t ch = (e & f) ^ (~e & g);
+    const uint32_t t1 = h + S1 + ch + kK[r] + wr;
+    const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+    const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+    const uint32_t t2 = S0 + mj;
+    h = g;
+    g = f;
+    f = e;
+    e = d + t1;
+    d = c;
+    c = b;
+    b = a;
+    a = t1 + t2;
+  }
+  st[0] += a;
+  st[1] += b;
+  st[2] += c;
+  st[3] += d;
+  st[4] += e;
+  st[5] += f;
+  st[6] += g;
+  st[7] += h;
+}
+
+// hash_pair: SHA-256(LEFT_LABEL || l || RIGHT_LABEL || r), 128 bytes = 2 blocks + padding.
+__host__ __device__ __forceinline__ void hash_pair(const uint32_t l[8], const uint32_t r[8], uint32_t out[8]) {
+  uint32_t st[8], w[16];
+  for (int i = 0; i < 8; ++i) st[i] = kIv[i];
+  for (int i = 0; i < 8; ++i) {
+    w[i] = kLeftLabel.w[i];
+    w[8 + i] = l[i];
+  }
+  compress(st, w);
+  for (int i = 0; i < 8; ++i) {
+    w[i] = kRightLabel.w[i];
+    w[8 + i] = r[i];
+  }
+  compress(st, w);
+  w[0] = 0x80000000u;
+  for (int i = 1; i < 15; ++i) w[i] = 0;
+  w[15] = 128 * 8;
+  compress(st, w);
+  for (int i = 0; i < 8; ++i) out[i] = st[i];
+}
+
+// Message word g (big-endian) of LEAF_LABEL || data[0..len) || SHA padding, total bytes
+// T = 32 + len; `word(j)` returns data word j (bytes 4j..4j+3, little-endian load order).
+template <typename DataWord, typename DataByte>
+__host__ __device__ __forceinline__ uint32_t leaf_msg_word(uint32_t g, uint32_t len, uint32_t nblk,
+                                                           DataWord&& word, DataByte&& byte) {
+  const uint32_t o = 4 * g, T = 32 + len;
+  if (o < 32) return kLeafLabel.w[g];
+  if (o + 4 <= T) return bswap(word((o - 32) >> 2));
+  if (g == 16 * nblk - 1) return T * 8;  // bit length (T < 2^29): low word
+  if (g == 16 * nblk - 2) return 0;      // bit length: high word
+  uint32_t v = 0;
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t ob = o + k;
+    uint32_t bv = 0;
+    if (ob < T) bv = byte(ob - 32);
+    else if (ob == T) bv = 0x80;
+    v |= bv << (24 - 8 * k);
+  }
+  return v;
+}
+
+}  // namespace sha
+
+namespace {
+
+using sha::hash_pair;
+
+// SHA-256(LEAF_LABEL || data[0..len)).  A4: data is 4-byte aligned (word loads).
+template <bool A4>
+__device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ data, uint32_t len, uint32_t out[8]) {
+  uint32_t st[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) st[i] = sha::kIv[i];
+  const uint32_t T = 32 + len, nblk = (T + 9 + 63) / 64;
+  auto word = [&](uint32_t j) -> uint32_t {
+    if constexpr (A4) {
+      return reinterpret_cast<const uint32_t*>(data)[j];
+    } else {
+      return uint32_t(data[4 * j]) | (uint32_t(data[4 * j + 1]) << 8) | (uint32_t(data[4 * j + 2]) << 16) |
+             (uint32_t(data[4 * j + 3]) << 24);
+    }
+  };
+  auto byte = [&](uint32_t i) -> uint32_t { return data[i]; };
+  for (uint32_t b = 0; b < nblk; ++b) {
+    uint32_t w[16];
+    const uint32_t o0 = 64 * b;
+    if (b > 0 && o0 + 64 <= T) {  // a block of data only: words j0 .. j0 + 15
+      const uint32_t j0 = (o0 - 32) >> 2;
+      if constexpr (A4) {
+#pragma unroll
+        for (int i = 0; i < 16; i += 4) {
+          const uint4 x = *reinterpret_cast<const uint4*>(data + 4 * (j0 + i));  // 16-B aligned when A4 & 16|stride
+          w[i] = sha::bswap(x.x);
+          w[i + 1] = sha::bswap(x.y);
+          w[i + 2] = sha::bswap(x.z);
+          w[i + 3] = sha::bswap(x.w);
+        }
+      } else {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) w[i] = sha::bswap(word(j0 + i));
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) w[i] = sha::leaf_msg_word(16 * b + i, len, nblk, word, byte);
+    }
+    sha::compress(st, w);
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) out[i] = st[i];
+}
+
+constexpr int kSlicesPerGroup = 4;  // one wave per slice
+
+// Digests are stored as 8 big-endian words -> 32 bytes in the crate's byte order.
+__device__ __forceinline__ void store_digest(uint8_t* dst, const uint32_t h[8]) {
+  uint4* d = reinterpret_cast<uint4*>(dst);
+  d[0] = make_uint4(sha::bswap(h[0]), sha::bswap(h[1]), sha::bswap(h[2]), sha::bswap(h[3]));
+  d[1] = make_uint4(sha::bswap(h[4]), sha::bswap(h[5]), sha::bswap(h[6]), sha::bswap(h[7]));
+}
+__device__ __forceinline__ void load_digest(const uint8_t* src, uint32_t h[8]) {
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  const uint4 a = s[0], b = s[1];
+  h[0] = sha::bswap(a.x);
+  h[1] = sha::bswap(a.y);
+  h[2] = sha::bswap(a.z);
+  h[3] = sha::bswap(a.w);
+  h[4] = sha::bswap(b.x);
+  h[5] = sha::bswap(b.y);
+  h[6] = sha::bswap(b.z);
+  h[7] = sha::bswap(b.w);
+}
+
+template <bool A4>
+__global__ __launch_bounds__(64 * kSlicesPerGroup) void merkle_slices_kernel(const MerkleBuildParams p) {
+  __shared__ uint32_t nodes[kSlicesPerGroup][2 * kMerkleMaxLeaves][8];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const uint64_t slice = static_cast<uint64_t>(blockIdx.x) * kSlicesPerGroup + wave;
+  if (slice >= p.nslices) return;  // whole wave
+  const uint32_t n = p.n_leaves;
+  uint32_t(*nd)[8] = nodes[wave];
+  // level 0: leaf hashes
+  if (static_cast<uint32_t>(lane) < n) {
+    uint32_t h[8];
+    leaf_hash<A4>(p.leaves + slice * p.slice_stride + static_cast<uint64_t>(lane) * p.leaf_stride, p.leaf_bytes, h);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) nd[lane][i] = h[i];
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  // inner levels (merkle.rs:303-328): level h has len_h nodes starting at off_h
+  uint32_t off = 0, len = n, height = 0;
+  while (len > 1) {
+    const uint32_t nlen = (len + 1) / 2;
+    if (static_cast<uint32_t>(lane) < nlen) {
+      uint32_t l[8], r[8], h[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) l[i] = nd[off + 2 * lane][i];
+      if (2 * static_cast<uint32_t>(lane) + 1 < len) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = nd[off + 2 * lane + 1][i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = p.empty_roots[8 * height + i];
+      }
+      hash_pair(l, r, h);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) nd[off + len + lane][i] = h[i];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    off += len;
+    len = nlen;
+    ++height;
+  }
+  const uint32_t total = off + 1;  // nodes in the tree; the root is the last one
+  if (lane == 0) store_digest(p.roots + slice * 32, nd[total - 1]);
+  if (p.nodes) {
+    for (uint32_t i = lane; i < total; i += 64) store_digest(p.nodes + slice * p.nodes_stride + 32ull * i, nd[i]);
+  }
+  if (p.proofs && static_cast<uint32_t>(lane) < n) {  // create_proof (merkle.rs:351-370)
+    uint8_t* dst = p.proofs + slice * p.proofs_stride + static_cast<uint64_t>(lane) * height * 32;
+    uint32_t i = lane, o = 0, l = n;
+    for (uint32_t h = 0; h < height; ++h) {
+      const uint32_t sib = i ^ 1;
+      uint32_t s[8];
+      if (sib >= l) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] = p.empty_roots[8 * h + q];
+      } else {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s[q] = nd[o + sib][q];
+      }
+      store_digest(dst + 32 * h, s);
+      o += l;
+      l = (l + 1) / 2;
+      i >>= 1;
+    }
+  }
+}
+
+// check_proof (merkle.rs:374-387, 417-428) for one leaf per thread.
+template <bool A4>
+__global__ __launch_bounds__(256) void merkle_verify_kernel(const MerkleVerifyParams p) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= p.n) return;
+  uint32_t node[8];
+  leaf_hash<A4>(p.leaves + t * p.leaf_stride, p.leaf_bytes, node);
+  uint32_t idx = p.index[t];
+  const uint8_t* pr = p.proofs + t * p.proofs_stride;
+  for (uint32_t h = 0; h < p.height; ++h) {
+    uint32_t s[8], nn[8];
+    load_digest(pr + 32 * h, s);
+    if (idx & 1) hash_pair(s, node, nn); else hash_pair(node, s, nn);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) node[i] = nn[i];
+    idx >>= 1;
+  }
+  uint32_t root[8];
+  load_digest(p.roots + t * p.roots_stride, root);
+  bool ok = true;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) ok = ok && node[i] == root[i];
+  p.ok[t] = ok ? 1 : 0;
+}
+
+}  // namespace
+
+hipError_t launch_merkle_build(const MerkleBuildParams& p, hipStream_t stream) {
+  if (p.nslices == 0) return hipSuccess;
+  if (p.n_leaves == 0 || p.n_leaves > kMerkleMaxLeaves) return hipErrorInvalidValue;
+  const uint64_t groups = (p.nslices + kSlicesPerGroup - 1) / kSlicesPerGroup;
+  if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const bool a16 = (reinterpret_cast<uintptr_t>(p.leaves) | p.leaf_stride | p.slice_stride) % 16 == 0;
+  const dim3 grid(static_cast<unsigned>(groups));
+  if (a16) hipLaunchKernelGGL((merkle_slices_kernel<true>), grid, dim3(64 * kSlicesPerGroup), 0, stream, p);
+  else hipLaunchKernelGGL((merkle_slices_kernel<false>), grid, dim3(64 * kSlicesPerGroup), 0, stream, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_merkle_verify(const MerkleVerifyParams& p, hipStream_t stream) {
+  if (p.n == 0) return hipSuccess;
+  const uint64_t groups = (p.n + 255) / 256;
+  if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const bool a16 = (reinterpret_cast<uintptr_t>(p.leaves) | p.leaf_stride) % 16 == 0;
+  const dim3 grid(static_cast<unsigned>(groups));
+  if (a16) hipLaunchKernelGGL((merkle_verify_kernel<true>), grid, dim3(256), 0, stream, p);
+  else hipLaunchKernelGGL((merkle_verify_kernel<false>), grid, dim3(256), 0, stream, p);
+  return hipGetLastError();
+}
+
+// EMPTY_ROOTS (merkle.rs:62-157): hash_leaf([]) then hash_pair(node, node) per height.
+void merkle_empty_roots(uint32_t out[kMerkleMaxHeight][8]) {
+  uint32_t st[8], w[16];
+  for (int i = 0; i < 8; ++i) st[i] = sha::kIv[i];
+  for (int i = 0; i < 8; ++i) w[i] = sha::kLeafLabel.w[i];
+  w[8] = 0x80000000u;
+  for (int i = 9; i < 15; ++i) w[i] = 0;
+  w[15] = 32 * 8;
+  sha::compress(st, w);
+  for (int i = 0; i < 8; ++i) out[0][i] = st[i];
+  for (int h = 1; h < kMerkleMaxHeight; ++h) sha::hash_pair(out[h - 1], out[h - 1], out[h]);
+}
+
+}  // namespace ag

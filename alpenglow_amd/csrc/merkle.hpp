@@ -1,0 +1,54 @@
+// Slice Merkle trees (merkle.hip): parameter blocks and launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace ag {
+
+// TOTAL_SHREDS (shredder.rs:47): every shredder's slice tree has 64 leaves.
+constexpr uint32_t kMerkleMaxLeaves = 64;
+// MAX_MERKLE_TREE_HEIGHT (merkle.rs:33)
+constexpr int kMerkleMaxHeight = 32;
+
+// nslices trees of n_leaves leaves; leaf j of slice s: leaves + s*slice_stride + j*leaf_stride,
+// leaf_bytes long.  Outputs (device): roots[s] (32 B); nodes (optional) = the reference's
+// `nodes` vector (leaf hashes, then each level); proofs (optional) = create_proof(j) for
+// every leaf, height digests each.
+struct MerkleBuildParams {
+  const uint8_t* leaves;
+  uint64_t leaf_stride;
+  uint64_t slice_stride;
+  uint32_t leaf_bytes;
+  uint32_t n_leaves;
+  uint64_t nslices;
+  const uint32_t* empty_roots;  // device [32][8] big-endian words (EMPTY_ROOTS)
+  uint8_t* roots;
+  uint8_t* nodes;  // may be null
+  uint64_t nodes_stride;
+  uint8_t* proofs;  // may be null
+  uint64_t proofs_stride;
+};
+hipError_t launch_merkle_build(const MerkleBuildParams& p, hipStream_t stream);
+
+// check_proof for n leaves: leaf t at leaves + t*leaf_stride, its index index[t], the root
+// roots + t*roots_stride, height proof digests at proofs + t*proofs_stride; ok[t] = 0/1.
+struct MerkleVerifyParams {
+  const uint8_t* leaves;
+  uint64_t leaf_stride;
+  uint32_t leaf_bytes;
+  uint32_t height;
+  const uint32_t* index;
+  const uint8_t* roots;
+  uint64_t roots_stride;
+  const uint8_t* proofs;
+  uint64_t proofs_stride;
+  uint64_t n;
+  uint8_t* ok;
+};
+hipError_t launch_merkle_verify(const MerkleVerifyParams& p, hipStream_t stream);
+
+// EMPTY_ROOTS[h] as big-endian words (host; the same SHA-256 code as the kernels).
+void merkle_empty_roots(uint32_t out[kMerkleMaxHeight][8]);
+
+}  // namespace ag

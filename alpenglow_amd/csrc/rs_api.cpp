@@ -19,6 +19,7 @@
 
 #include "../../include/alpenglow_rs.h"
 #include "gf16.hpp"
+#include "merkle.hpp"
 #include "rs_launch.hpp"
 
 using ag::next_pow2;
@@ -106,6 +107,7 @@ struct ag_rs_ctx {
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
+  DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
   // host-memory calls: two staging slots, H2D / D2H streams next to the compute stream
@@ -184,7 +186,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
                       &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -791,6 +793,104 @@ int ag_rs_fill_splitmix(ag_rs_ctx* c, uint8_t* dst, size_t nblocks, size_t block
   return ag::launch_fill_splitmix(dst, nblocks, block_bytes, dst_stride, seed_base, c->stream) == hipSuccess
              ? AG_RS_OK
              : AG_RS_ERR_DEVICE;
+}
+
+// ---- slice Merkle trees --------------------------------------------------------------
+
+size_t ag_merkle_height(size_t n) {
+  size_t h = 0;
+  for (size_t len = n; len > 1; len = (len + 1) / 2) ++h;
+  return h;
+}
+
+size_t ag_merkle_node_count(size_t n) {
+  size_t total = n;
+  for (size_t len = n; len > 1;) {
+    len = (len + 1) / 2;
+    total += len;
+  }
+  return total;
+}
+
+int ag_merkle_empty_root(size_t height, uint8_t out[32]) {
+  if (!out || height >= static_cast<size_t>(ag::kMerkleMaxHeight)) return AG_RS_ERR_INVALID_ARGUMENT;
+  uint32_t er[ag::kMerkleMaxHeight][8];
+  ag::merkle_empty_roots(er);
+  for (int i = 0; i < 8; ++i)
+    for (int b = 0; b < 4; ++b) out[4 * i + b] = static_cast<uint8_t>(er[height][i] >> (24 - 8 * b));
+  return AG_RS_OK;
+}
+
+namespace {
+int ensure_empty_roots(ag_rs_ctx* c) {
+  if (c->d_empty_roots.ptr) return AG_RS_OK;
+  uint32_t er[ag::kMerkleMaxHeight][8];
+  ag::merkle_empty_roots(er);
+  int st = c->d_empty_roots.ensure(sizeof er, c->stream);
+  if (st) return st;
+  AG_HIP(hipMemcpy(c->d_empty_roots.ptr, er, sizeof er, hipMemcpyHostToDevice));
+  return AG_RS_OK;
+}
+}  // namespace
+
+int ag_merkle_build_batch(ag_rs_ctx* c, size_t n_leaves, size_t leaf_bytes, size_t nslices, const uint8_t* leaves,
+                          size_t leaf_stride, size_t slice_stride, uint8_t* roots, uint8_t* nodes,
+                          size_t nodes_stride, uint8_t* proofs, size_t proofs_stride) {
+  if (!c || n_leaves == 0 || n_leaves > AG_MERKLE_MAX_LEAVES || leaf_bytes >= (size_t{1} << 28))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (nslices == 0) return AG_RS_OK;
+  if ((leaf_bytes && !leaves) || !roots || (n_leaves > 1 && leaf_stride < leaf_bytes) ||
+      (nslices > 1 && slice_stride < (n_leaves - 1) * leaf_stride + leaf_bytes))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  const size_t h = ag_merkle_height(n_leaves);
+  if ((nodes && (nodes_stride % 16 || (nslices > 1 && nodes_stride < 32 * ag_merkle_node_count(n_leaves)))) ||
+      (proofs && (proofs_stride % 16 || (nslices > 1 && proofs_stride < 32 * h * n_leaves))) ||
+      reinterpret_cast<uintptr_t>(roots) % 16 || reinterpret_cast<uintptr_t>(nodes) % 16 ||
+      reinterpret_cast<uintptr_t>(proofs) % 16)
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  int st = ensure_empty_roots(c);
+  if (st) return st;
+  ag::MerkleBuildParams p{};
+  p.leaves = leaves;
+  p.leaf_stride = leaf_stride;
+  p.slice_stride = slice_stride;
+  p.leaf_bytes = static_cast<uint32_t>(leaf_bytes);
+  p.n_leaves = static_cast<uint32_t>(n_leaves);
+  p.nslices = nslices;
+  p.empty_roots = c->d_empty_roots.as<uint32_t>();
+  p.roots = roots;
+  p.nodes = nodes;
+  p.nodes_stride = nodes_stride;
+  p.proofs = proofs;
+  p.proofs_stride = proofs_stride;
+  return ag::launch_merkle_build(p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+int ag_merkle_verify_batch(ag_rs_ctx* c, size_t n, size_t leaf_bytes, const uint8_t* leaves, size_t leaf_stride,
+                           const uint32_t* index, const uint8_t* roots, size_t roots_stride, const uint8_t* proofs,
+                           size_t proofs_stride, size_t height, uint8_t* ok) {
+  if (!c || leaf_bytes >= (size_t{1} << 28) || height > static_cast<size_t>(ag::kMerkleMaxHeight))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if ((leaf_bytes && !leaves) || !index || !roots || !ok || (height && !proofs) || roots_stride % 16 ||
+      proofs_stride % 16 || reinterpret_cast<uintptr_t>(roots) % 16 || reinterpret_cast<uintptr_t>(proofs) % 16 ||
+      (n > 1 && leaf_stride < leaf_bytes))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  ag::MerkleVerifyParams p{};
+  p.leaves = leaves;
+  p.leaf_stride = leaf_stride;
+  p.leaf_bytes = static_cast<uint32_t>(leaf_bytes);
+  p.height = static_cast<uint32_t>(height);
+  p.index = index;
+  p.roots = roots;
+  p.roots_stride = roots_stride;
+  p.proofs = proofs;
+  p.proofs_stride = proofs_stride;
+  p.n = n;
+  p.ok = ok;
+  return ag::launch_merkle_verify(p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
 }
 
 }  // extern "C"

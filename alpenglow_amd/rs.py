@@ -131,6 +131,11 @@ def load():
         "ag_rs_coder_deshred": ([p, sz, p, p, p, p, psz, p, p, psz], i),
         "ag_rs_coder_shred_batch": ([p, sz, sz, sz, p, sz, p, p, sz], i),
         "ag_rs_coder_deshred_batch": ([p, sz, sz, sz, p, sz, p, p, i, p], i),
+        "ag_merkle_empty_root": ([sz, p], i),
+        "ag_merkle_height": ([sz], sz),
+        "ag_merkle_node_count": ([sz], sz),
+        "ag_merkle_build_batch": ([p, sz, sz, sz, p, sz, sz, p, p, sz, p, sz], i),
+        "ag_merkle_verify_batch": ([p, sz, sz, p, sz, p, p, sz, p, sz, sz, p], i),
     }
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
@@ -418,3 +423,38 @@ class ReedSolomonCoder:
         if getattr(self, "handle", None):
             self._lib.ag_rs_coder_free(self.handle)
             self.handle = None
+
+
+# ---- slice Merkle trees (crypto/merkle.rs; shredder.rs:628-632) -----------------------
+
+def merkle_empty_root(height: int) -> bytes:
+    """EMPTY_ROOTS[height] (merkle.rs:62-157), computed by the library (no GPU needed)."""
+    out = ctypes.create_string_buffer(32)
+    _check(load().ag_merkle_empty_root(height, out), "ag_merkle_empty_root")
+    return out.raw
+
+
+def merkle_height(n_leaves: int) -> int:
+    return load().ag_merkle_height(n_leaves)
+
+
+def merkle_node_count(n_leaves: int) -> int:
+    return load().ag_merkle_node_count(n_leaves)
+
+
+def merkle_build_batch(ctx: Context, n_leaves: int, leaf_bytes: int, nslices: int, leaves, leaf_stride: int,
+                       slice_stride: int, roots, nodes=None, nodes_stride: int = 0, proofs=None,
+                       proofs_stride: int = 0):
+    """MerkleTree::new + get_root + create_proof for a batch of slices (device buffers)."""
+    _check(load().ag_merkle_build_batch(ctx.handle, n_leaves, leaf_bytes, nslices, _ptr(leaves), leaf_stride,
+                                        slice_stride, _ptr(roots), _ptr(nodes) if nodes is not None else None,
+                                        nodes_stride, _ptr(proofs) if proofs is not None else None,
+                                        proofs_stride), "ag_merkle_build_batch")
+
+
+def merkle_verify_batch(ctx: Context, n: int, leaf_bytes: int, leaves, leaf_stride: int, index, roots,
+                        roots_stride: int, proofs, proofs_stride: int, height: int, ok):
+    """check_proof for n leaves (device buffers); ok[t] = 1 / 0."""
+    _check(load().ag_merkle_verify_batch(ctx.handle, n, leaf_bytes, _ptr(leaves), leaf_stride, _ptr(index),
+                                         _ptr(roots), roots_stride, _ptr(proofs), proofs_stride, height,
+                                         _ptr(ok)), "ag_merkle_verify_batch")

@@ -16,6 +16,8 @@
  *   3. ag_rs_encode_batch / ag_rs_decode_batch -- batched, device-resident forms of 1.
  *      (the GPU-shaped entry points: many blocks per launch)
  *   4. context / stream / utility
+ *   5. ag_merkle_*     -- the slice Merkle tree over the shreds (crypto/merkle.rs,
+ *      shredder.rs:628-632), batched on the device
  *
  * Conventions: the caller owns every buffer; the library borrows them for the call
  * (reed_solomon.rs copies out of the crate's borrowed results, :118,125,187,226).  A
@@ -212,6 +214,36 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* ctx, size_t num_coding, size_t nslices,
                               size_t shred_bytes, uint8_t* codewords, size_t codeword_stride,
                               const uint8_t* data_present, const uint8_t* coding_present,
                               int mode, int64_t* payload_len_out);
+
+/* ---- 5. slice Merkle trees -----------------------------------------------------------
+ * The SHA-256 Merkle tree the shredder builds over each slice's 64 shreds (data shreds,
+ * then coding shreds; shredder.rs:628-632) -- crypto/merkle.rs MerkleTree:
+ *   leaf  = SHA-256("ALPENGLOW-MERKLE-TREE  LEAF-NODE" || shred)      (merkle.rs:457-460)
+ *   inner = SHA-256(LEFT_LABEL || left || RIGHT_LABEL || right)       (merkle.rs:466-468)
+ *   odd node at height h pairs with EMPTY_ROOTS[h]                    (merkle.rs:303-328)
+ * Device-resident batches (all pointers device memory, on the context's stream). */
+#define AG_MERKLE_MAX_LEAVES 64
+
+/* EMPTY_ROOTS[height] (merkle.rs:62-157) computed by the library's SHA-256; no GPU needed. */
+int ag_merkle_empty_root(size_t height, uint8_t out[32]);
+/* Height and node count (reference `nodes.len()`) of a tree of n_leaves leaves. */
+size_t ag_merkle_height(size_t n_leaves);
+size_t ag_merkle_node_count(size_t n_leaves);
+/* MerkleTree::new + get_root + create_proof for every leaf (merkle.rs:281-370), nslices
+ * slices.  Leaf j of slice s: leaves + s*slice_stride + j*leaf_stride, leaf_bytes long
+ * (1 <= n_leaves <= 64).  roots: 32 B per slice.  nodes (nullable): node_count digests per
+ * slice at nodes_stride.  proofs (nullable): height digests per leaf, n_leaves*height*32 B
+ * per slice at proofs_stride. */
+int ag_merkle_build_batch(ag_rs_ctx* ctx, size_t n_leaves, size_t leaf_bytes, size_t nslices,
+                          const uint8_t* leaves, size_t leaf_stride, size_t slice_stride, uint8_t* roots,
+                          uint8_t* nodes, size_t nodes_stride, uint8_t* proofs, size_t proofs_stride);
+/* check_proof (merkle.rs:374-387) for n leaves: leaf t at leaves + t*leaf_stride, index[t],
+ * root at roots + t*roots_stride, height digests at proofs + t*proofs_stride;
+ * ok[t] = 1 if the proof derives the root, else 0. */
+int ag_merkle_verify_batch(ag_rs_ctx* ctx, size_t n, size_t leaf_bytes, const uint8_t* leaves,
+                           size_t leaf_stride, const uint32_t* index, const uint8_t* roots,
+                           size_t roots_stride, const uint8_t* proofs, size_t proofs_stride, size_t height,
+                           uint8_t* ok);
 
 #ifdef __cplusplus
 }
