@@ -12,9 +12,11 @@
 // implementation shared by host and device.
 //
 // Kernels
-//   merkle_slices_kernel  one wave per slice: lane i hashes leaf i, the tree levels are
-//                         built in the wave's LDS, lane i writes its own proof.  Integer
-//                         VALU-bound (~2.6k VALU per 64-byte SHA block per lane).
+//   merkle_leaf_kernel    one thread per leaf (all slices): SHA-256 of label || shred.
+//                         Integer VALU-bound (~1.2k VALU per 64-byte SHA-256 block and
+//                         lane: v_alignbit rotations, v_bitop3 sigma XORs / ch / maj, v_add3)
+//   merkle_level_kernel   one launch per tree level, one thread per (slice, pair)
+//   merkle_proof_kernel   one thread per leaf: its create_proof siblings
 //   merkle_verify_kernel  one thread per (leaf, index, root, proof): derive_root == root.
 #include <hip/hip_runtime.h>
 
@@ -26,7 +28,7 @@
 namespace ag {
 namespace sha {
 
-__host__ __device__ constexpr uint32_t kK[64] = {
+constexpr uint32_t kK[64] = {
     0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
     0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
     0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
@@ -35,7 +37,7 @@ __host__ __device__ constexpr uint32_t kK[64] = {
     0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
     0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
     0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
-__host__ __device__ constexpr uint32_t kIv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
+constexpr uint32_t kIv[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a,
                                                  0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
 
 // The 32-byte labels of merkle.rs:42-44 as big-endian message words.
@@ -49,11 +51,19 @@ __host__ __device__ constexpr Label make_label(const char (&s)[33]) {
              (uint32_t(uint8_t(s[4 * i + 2])) << 8) | uint32_t(uint8_t(s[4 * i + 3]));
   return l;
 }
-__host__ __device__ constexpr Label kLeafLabel = make_label("ALPENGLOW-MERKLE-TREE  LEAF-NODE");
-__host__ __device__ constexpr Label kLeftLabel = make_label("ALPENGLOW-MERKLE-TREE  LEFT-NODE");
-__host__ __device__ constexpr Label kRightLabel = make_label("ALPENGLOW-MERKLE-TREE RIGHT-NODE");
+constexpr Label kLeafLabel = make_label("ALPENGLOW-MERKLE-TREE  LEAF-NODE");
+constexpr Label kLeftLabel = make_label("ALPENGLOW-MERKLE-TREE  LEFT-NODE");
+constexpr Label kRightLabel = make_label("ALPENGLOW-MERKLE-TREE RIGHT-NODE");
 
 __host__ __device__ __forceinline__ uint32_t rotr(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+// 3-input XOR: one v_bitop3_b32 on the device (LLVM leaves the sigma XORs as two ops)
+__host__ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+#ifdef __HIP_DEVICE_COMPILE__
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+#else
+  return a ^ b ^ c;
+#endif
+}
 __host__ __device__ __forceinline__ uint32_t bswap(uint32_t x) {
   return (x >> 24) | ((x >> 8) & 0xFF00u) | ((x << 8) & 0xFF0000u) | (x << 24);
 }
@@ -68,14 +78,14 @@ __host__ __device__ __forceinline__ void compress(uint32_t st[8], uint32_t w[16]
       wr = w[r];
     } else {
       const uint32_t w15 = w[(r + 1) & 15], w2 = w[(r + 14) & 15];
-      const uint32_t s0 = rotr(w15, 7) ^ rotr(w15, 18) ^ (w15 >> 3);
-      const uint32_t s1 = rotr(w2, 17) ^ rotr(w2, 19) ^ (w2 >> 10);
+      const uint32_t s0 = xor3(rotr(w15, 7), rotr(w15, 18), w15 >> 3);
+      const uint32_t s1 = xor3(rotr(w2, 17), rotr(w2, 19), w2 >> 10);
       wr = w[r & 15] = w[r & 15] + s0 + w[(r + 9) & 15] + s1;
     }
-    const uint32_t S1 = rotr(e, 6) ^ rotr(e, 11) ^ rotr(e, 25);
+    const uint32_t S1 = xor3(rotr(e, 6), rotr(e, 11), rotr(e, 25));
     const uint32_t ch = (e & f) ^ (~e & g);
     const uint32_t t1 = h + S1 + ch + kK[r] + wr;
-    const uint32_t S0 = rotr(a, 2) ^ rotr(a, 13) ^ rotr(a, 22);
+    const uint32_t S0 = xor3(rotr(a, 2), rotr(a, 13), rotr(a, 22));
     const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
     const uint32_t t2 = S0 + mj;
     h = g;
@@ -189,8 +199,6 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ data, uint
   for (int i = 0; i < 8; ++i) out[i] = st[i];
 }
 
-constexpr int kSlicesPerGroup = 4;  // one wave per slice
-
 // Digests are stored as 8 big-endian words -> 32 bytes in the crate's byte order.
 __device__ __forceinline__ void store_digest(uint8_t* dst, const uint32_t h[8]) {
   uint4* d = reinterpret_cast<uint4*>(dst);
@@ -210,74 +218,69 @@ __device__ __forceinline__ void load_digest(const uint8_t* src, uint32_t h[8]) {
   h[7] = sha::bswap(b.w);
 }
 
+// Build = one kernel per tree level, every launch fully parallel over all slices (a fused
+// one-wave-per-slice build left 50..98% of the lanes idle in its 6 dependent levels of 3
+// compressions each: as long as the 17-block leaf phase).
+//   level 0: thread (slice, leaf) hashes the leaf into nodes[slice][leaf]
+//   level h: thread (slice, j) hashes nodes[off + 2j], nodes[off + 2j + 1] (or EMPTY_ROOTS[h]
+//            past the end) into nodes[off + len + j]; the last level also writes the root
+//   proofs:  thread (slice, leaf) copies its siblings (create_proof)
 template <bool A4>
-__global__ __launch_bounds__(64 * kSlicesPerGroup) void merkle_slices_kernel(const MerkleBuildParams p) {
-  __shared__ uint32_t nodes[kSlicesPerGroup][2 * kMerkleMaxLeaves][8];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const uint64_t slice = static_cast<uint64_t>(blockIdx.x) * kSlicesPerGroup + wave;
-  if (slice >= p.nslices) return;  // whole wave
-  const uint32_t n = p.n_leaves;
-  uint32_t(*nd)[8] = nodes[wave];
-  // level 0: leaf hashes
-  if (static_cast<uint32_t>(lane) < n) {
-    uint32_t h[8];
-    leaf_hash<A4>(p.leaves + slice * p.slice_stride + static_cast<uint64_t>(lane) * p.leaf_stride, p.leaf_bytes, h);
+__global__ __launch_bounds__(256) void merkle_leaf_kernel(const MerkleBuildParams p, uint8_t* nodes,
+                                                          uint64_t nodes_stride) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= p.nslices * p.n_leaves) return;
+  const uint64_t s = t / p.n_leaves, j = t - s * p.n_leaves;
+  uint32_t h[8];
+  leaf_hash<A4>(p.leaves + s * p.slice_stride + j * p.leaf_stride, p.leaf_bytes, h);
+  store_digest(nodes + s * nodes_stride + 32 * j, h);
+  if (p.n_leaves == 1) store_digest(p.roots + 32 * s, h);  // a one-leaf tree's root is the leaf
+}
+
+__global__ __launch_bounds__(256) void merkle_level_kernel(const MerkleBuildParams p, uint8_t* nodes,
+                                                           uint64_t nodes_stride, uint32_t off, uint32_t len,
+                                                           uint32_t height) {
+  const uint32_t nlen = (len + 1) / 2;
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= p.nslices * nlen) return;
+  const uint64_t s = t / nlen, j = t - s * nlen;
+  uint8_t* nd = nodes + s * nodes_stride;
+  uint32_t l[8], r[8], h[8];
+  load_digest(nd + 32 * (off + 2 * j), l);
+  if (2 * j + 1 < len) {
+    load_digest(nd + 32 * (off + 2 * j + 1), r);
+  } else {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) nd[lane][i] = h[i];
+    for (int i = 0; i < 8; ++i) r[i] = p.empty_roots[8 * height + i];
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  // inner levels (merkle.rs:303-328): level h has len_h nodes starting at off_h
-  uint32_t off = 0, len = n, height = 0;
-  while (len > 1) {
-    const uint32_t nlen = (len + 1) / 2;
-    if (static_cast<uint32_t>(lane) < nlen) {
-      uint32_t l[8], r[8], h[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) l[i] = nd[off + 2 * lane][i];
-      if (2 * static_cast<uint32_t>(lane) + 1 < len) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = nd[off + 2 * lane + 1][i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = p.empty_roots[8 * height + i];
-      }
-      hash_pair(l, r, h);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) nd[off + len + lane][i] = h[i];
+  hash_pair(l, r, h);
+  store_digest(nd + 32 * (off + len + j), h);
+  if (nlen == 1) store_digest(p.roots + 32 * s, h);
+}
+
+__global__ __launch_bounds__(256) void merkle_proof_kernel(const MerkleBuildParams p, const uint8_t* nodes,
+                                                           uint64_t nodes_stride, uint32_t height) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= p.nslices * p.n_leaves) return;
+  const uint64_t s = t / p.n_leaves, j = t - s * p.n_leaves;
+  const uint8_t* nd = nodes + s * nodes_stride;
+  uint8_t* dst = p.proofs + s * p.proofs_stride + j * height * 32;
+  uint32_t i = static_cast<uint32_t>(j), o = 0, l = p.n_leaves;
+  for (uint32_t h = 0; h < height; ++h) {
+    const uint32_t sib = i ^ 1;
+    uint4* d = reinterpret_cast<uint4*>(dst + 32 * h);
+    if (sib >= l) {
+      const uint32_t* e = p.empty_roots + 8 * h;
+      d[0] = make_uint4(sha::bswap(e[0]), sha::bswap(e[1]), sha::bswap(e[2]), sha::bswap(e[3]));
+      d[1] = make_uint4(sha::bswap(e[4]), sha::bswap(e[5]), sha::bswap(e[6]), sha::bswap(e[7]));
+    } else {
+      const uint4* src = reinterpret_cast<const uint4*>(nd + 32 * (o + sib));
+      d[0] = src[0];
+      d[1] = src[1];
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    off += len;
-    len = nlen;
-    ++height;
-  }
-  const uint32_t total = off + 1;  // nodes in the tree; the root is the last one
-  if (lane == 0) store_digest(p.roots + slice * 32, nd[total - 1]);
-  if (p.nodes) {
-    for (uint32_t i = lane; i < total; i += 64) store_digest(p.nodes + slice * p.nodes_stride + 32ull * i, nd[i]);
-  }
-  if (p.proofs && static_cast<uint32_t>(lane) < n) {  // create_proof (merkle.rs:351-370)
-    uint8_t* dst = p.proofs + slice * p.proofs_stride + static_cast<uint64_t>(lane) * height * 32;
-    uint32_t i = lane, o = 0, l = n;
-    for (uint32_t h = 0; h < height; ++h) {
-      const uint32_t sib = i ^ 1;
-      uint32_t s[8];
-      if (sib >= l) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) s[q] = p.empty_roots[8 * h + q];
-      } else {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) s[q] = nd[o + sib][q];
-      }
-      store_digest(dst + 32 * h, s);
-      o += l;
-      l = (l + 1) / 2;
-      i >>= 1;
-    }
+    o += l;
+    l = (l + 1) / 2;
+    i >>= 1;
   }
 }
 
@@ -308,15 +311,27 @@ __global__ __launch_bounds__(256) void merkle_verify_kernel(const MerkleVerifyPa
 
 }  // namespace
 
-hipError_t launch_merkle_build(const MerkleBuildParams& p, hipStream_t stream) {
+hipError_t launch_merkle_build(const MerkleBuildParams& p, uint8_t* nodes, uint64_t nodes_stride,
+                               hipStream_t stream) {
   if (p.nslices == 0) return hipSuccess;
-  if (p.n_leaves == 0 || p.n_leaves > kMerkleMaxLeaves) return hipErrorInvalidValue;
-  const uint64_t groups = (p.nslices + kSlicesPerGroup - 1) / kSlicesPerGroup;
-  if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  if (p.n_leaves == 0 || p.n_leaves > kMerkleMaxLeaves || !nodes || nodes_stride % 16) return hipErrorInvalidValue;
+  auto grid_of = [](uint64_t threads) { return dim3(static_cast<unsigned>((threads + 255) / 256)); };
+  if ((p.nslices * p.n_leaves + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const bool a16 = (reinterpret_cast<uintptr_t>(p.leaves) | p.leaf_stride | p.slice_stride) % 16 == 0;
-  const dim3 grid(static_cast<unsigned>(groups));
-  if (a16) hipLaunchKernelGGL((merkle_slices_kernel<true>), grid, dim3(64 * kSlicesPerGroup), 0, stream, p);
-  else hipLaunchKernelGGL((merkle_slices_kernel<false>), grid, dim3(64 * kSlicesPerGroup), 0, stream, p);
+  const dim3 g0 = grid_of(p.nslices * p.n_leaves);
+  if (a16) hipLaunchKernelGGL((merkle_leaf_kernel<true>), g0, dim3(256), 0, stream, p, nodes, nodes_stride);
+  else hipLaunchKernelGGL((merkle_leaf_kernel<false>), g0, dim3(256), 0, stream, p, nodes, nodes_stride);
+  uint32_t off = 0, len = p.n_leaves, height = 0;
+  while (len > 1) {
+    const uint32_t nlen = (len + 1) / 2;
+    hipLaunchKernelGGL(merkle_level_kernel, grid_of(p.nslices * nlen), dim3(256), 0, stream, p, nodes, nodes_stride,
+                       off, len, height);
+    off += len;
+    len = nlen;
+    ++height;
+  }
+  if (p.proofs && height)
+    hipLaunchKernelGGL(merkle_proof_kernel, g0, dim3(256), 0, stream, p, nodes, nodes_stride, height);
   return hipGetLastError();
 }
 

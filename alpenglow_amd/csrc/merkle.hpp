@@ -24,12 +24,13 @@ struct MerkleBuildParams {
   uint64_t nslices;
   const uint32_t* empty_roots;  // device [32][8] big-endian words (EMPTY_ROOTS)
   uint8_t* roots;
-  uint8_t* nodes;  // may be null
-  uint64_t nodes_stride;
   uint8_t* proofs;  // may be null
   uint64_t proofs_stride;
 };
-hipError_t launch_merkle_build(const MerkleBuildParams& p, hipStream_t stream);
+// nodes: the node digests (reference order, nodes_stride per slice; the caller's buffer or
+// scratch) -- the levels are built there.
+hipError_t launch_merkle_build(const MerkleBuildParams& p, uint8_t* nodes, uint64_t nodes_stride,
+                               hipStream_t stream);
 
 // check_proof for n leaves: leaf t at leaves + t*leaf_stride, its index index[t], the root
 // roots + t*roots_stride, height proof digests at proofs + t*proofs_stride; ok[t] = 0/1.

@@ -108,6 +108,7 @@ struct ag_rs_ctx {
   DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
+  DevBuf d_merkle_nodes;                    // Merkle node scratch (callers without a nodes buffer)
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
   // host-memory calls: two staging slots, H2D / D2H streams next to the compute stream
@@ -186,7 +187,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_merkle_nodes, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
                       &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -860,11 +861,14 @@ int ag_merkle_build_batch(ag_rs_ctx* c, size_t n_leaves, size_t leaf_bytes, size
   p.nslices = nslices;
   p.empty_roots = c->d_empty_roots.as<uint32_t>();
   p.roots = roots;
-  p.nodes = nodes;
-  p.nodes_stride = nodes_stride;
   p.proofs = proofs;
   p.proofs_stride = proofs_stride;
-  return ag::launch_merkle_build(p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+  if (!nodes) {  // the levels are built in memory: scratch when the caller wants no nodes
+    nodes_stride = (32 * ag_merkle_node_count(n_leaves) + 255) / 256 * 256;
+    if ((st = c->d_merkle_nodes.ensure(nslices * nodes_stride, c->stream))) return st;
+    nodes = c->d_merkle_nodes.as<uint8_t>();
+  }
+  return ag::launch_merkle_build(p, nodes, nodes_stride, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
 }
 
 int ag_merkle_verify_batch(ag_rs_ctx* c, size_t n, size_t leaf_bytes, const uint8_t* leaves, size_t leaf_stride,
