@@ -320,6 +320,14 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
                   int mode) {
   if (nblocks == 0) return AG_RS_OK;
   const int hr = ag::use_high_rate(k, m);
+  // one erasure pattern repeated for every block (a repair batch, a uniform loss) is one
+  // pattern: uniform store masks, and the bitsliced kernels regardless of block alignment
+  if (npat > 1) {
+    bool same = true;
+    for (size_t p = 1; p < npat && same; ++p)
+      same = std::memcmp(opres, opres + p * k, k) == 0 && std::memcmp(rpres, rpres + p * m, m) == 0;
+    if (same) npat = 1;
+  }
   // classify patterns: 0 = nothing to restore, 1 = transform kernel (full recovery set),
   // 3 = bitsliced general decoder, 2 = table-driven generic kernel.
   // The transform inverts the encoder only when all N recovery points exist (m == N):

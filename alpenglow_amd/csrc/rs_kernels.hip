@@ -1522,23 +1522,39 @@ __global__ __launch_bounds__(256) void coder_pad_kernel(const uint8_t* __restric
 
 // Per slice: payload length after stripping the bit padding (trailing zeros, then a 0x80
 // marker), or -1 when the padding is invalid.  One workgroup per slice.
+// Padding strip (reed_solomon.rs:191-203): the last non-zero byte of the data region must
+// be 0x80.  The padding sits at the end, so the workgroup scans 4 KiB windows backwards
+// with 16-byte loads and stops at the first window holding a non-zero byte.
 __global__ __launch_bounds__(256) void coder_strip_kernel(const uint8_t* __restrict__ cw, uint64_t cw_stride,
                                                           uint32_t data_bytes, int64_t* out) {
-  __shared__ int32_t best[256];
+  __shared__ int32_t best;
   const uint8_t* d = cw + static_cast<uint64_t>(blockIdx.x) * cw_stride;
-  int32_t last = -1;
-  for (uint32_t i = threadIdx.x; i < data_bytes; i += blockDim.x)
-    if (d[i]) last = static_cast<int32_t>(i);
-  best[threadIdx.x] = last;
-  __syncthreads();
-  for (int w = 128; w > 0; w >>= 1) {
-    if (static_cast<int>(threadIdx.x) < w) best[threadIdx.x] = max(best[threadIdx.x], best[threadIdx.x + w]);
+  const bool a16 = ((reinterpret_cast<uintptr_t>(cw) | cw_stride) & 15) == 0;
+  int32_t found = -1;
+  for (int64_t hi = data_bytes; hi > 0 && found < 0; hi -= 4096) {
+    const int64_t lo = hi > 4096 ? hi - 4096 : 0;
+    if (threadIdx.x == 0) best = -1;
+    __syncthreads();
+    const int64_t i0 = lo + 16 * static_cast<int64_t>(threadIdx.x);
+    int32_t last = -1;
+    if (i0 < hi) {  // data_bytes % 16 == 0: whole 16-byte pieces
+      uint8_t v[16];
+      if (a16) {
+        const uint4 x = *reinterpret_cast<const uint4*>(d + i0);
+        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+        for (int i = 0; i < 16; ++i) v[i] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+      } else {
+        for (int i = 0; i < 16; ++i) v[i] = d[i0 + i];
+      }
+      for (int i = 0; i < 16; ++i)
+        if (v[i]) last = static_cast<int32_t>(i0 + i);
+    }
+    if (last >= 0) atomicMax(&best, last);
+    __syncthreads();
+    found = best;
     __syncthreads();
   }
-  if (threadIdx.x == 0) {
-    const int32_t m = best[0];
-    out[blockIdx.x] = (m < 0 || d[m] != 0x80) ? -1 : m;
-  }
+  if (threadIdx.x == 0) out[blockIdx.x] = (found < 0 || d[found] != 0x80) ? -1 : found;
 }
 
 // =====================================================================================

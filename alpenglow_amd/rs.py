@@ -247,27 +247,39 @@ def coder_shred_batch(ctx: Context, num_coding: int, nslices: int, shred_bytes: 
                       payload_stride: int, payload_lens, codewords, codeword_stride: int):
     """Batched ReedSolomonCoder::shred (device-resident): payload b (device) -> padded data
     shards + num_coding coding shards in codeword b.  payloads None: already in place."""
-    lens = (ctypes.c_uint32 * nslices)(*payload_lens)
+    import numpy as np
+
+    lens = np.ascontiguousarray(np.asarray(payload_lens, dtype=np.uint32))
+    if lens.size != nslices:
+        raise ValueError("payload_lens does not match the batch")
     _check(load().ag_rs_coder_shred_batch(ctx.handle, num_coding, nslices, shred_bytes,
                                           _ptr(payloads) if payloads is not None else None,
-                                          payload_stride, lens, _ptr(codewords), codeword_stride),
+                                          payload_stride, lens.ctypes.data, _ptr(codewords), codeword_stride),
            "ag_rs_coder_shred_batch")
 
 
 def coder_deshred_batch(ctx: Context, num_coding: int, nslices: int, shred_bytes: int, codewords,
                         codeword_stride: int, data_present, coding_present,
-                        mode: int = DECODE_EXACT) -> list:
+                        mode: int = DECODE_EXACT, as_array: bool = False):
     """Batched ReedSolomonCoder::deshred (device-resident, in place).  Returns per slice the
-    payload length or an RSError kind string ('NotEnoughShards' / 'InvalidPadding')."""
-    dp = bytes(bytearray(data_present))
-    cp = bytes(bytearray(coding_present))
-    if len(dp) != nslices * 32 or len(cp) != nslices * num_coding:
+    payload length or an RSError kind string ('NotEnoughShards' / 'InvalidPadding'); with
+    as_array, an int64 numpy array of lengths / -status codes (no per-slice Python work)."""
+    import numpy as np
+
+    dp = np.ascontiguousarray(np.frombuffer(bytes(data_present), np.uint8) if isinstance(data_present, (bytes, bytearray))
+                              else np.asarray(data_present, dtype=np.uint8))
+    cp = np.ascontiguousarray(np.frombuffer(bytes(coding_present), np.uint8) if isinstance(coding_present, (bytes, bytearray))
+                              else np.asarray(coding_present, dtype=np.uint8))
+    if dp.size != nslices * 32 or cp.size != nslices * num_coding:
         raise ValueError("present-flag arrays do not match the batch")
-    out = (ctypes.c_int64 * nslices)()
+    out = np.empty(nslices, np.int64)
     _check(load().ag_rs_coder_deshred_batch(ctx.handle, num_coding, nslices, shred_bytes,
-                                            _ptr(codewords), codeword_stride, dp, cp, mode, out),
+                                            _ptr(codewords), codeword_stride, dp.ctypes.data, cp.ctypes.data, mode,
+                                            out.ctypes.data),
            "ag_rs_coder_deshred_batch")
-    return [v if v >= 0 else STATUS_KIND.get(-v, f"Status{-v}") for v in out]
+    if as_array:
+        return out
+    return [int(v) if v >= 0 else STATUS_KIND.get(int(-v), f"Status{int(-v)}") for v in out]
 
 
 def fill_splitmix(ctx: Context, device_dst, nblocks: int, block_bytes: int, dst_block_stride: int,
