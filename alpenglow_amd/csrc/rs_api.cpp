@@ -19,6 +19,7 @@
 
 #include "../../include/alpenglow_rs.h"
 #include "gf16.hpp"
+#include "cipher.hpp"
 #include "merkle.hpp"
 #include "rs_launch.hpp"
 
@@ -109,6 +110,7 @@ struct ag_rs_ctx {
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
   DevBuf d_merkle_nodes;                    // Merkle node scratch (callers without a nodes buffer)
+  DevBuf d_aon_lens, d_aon_digests, d_aon_keys;  // all-or-nothing transforms
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
   // host-memory calls: two staging slots, H2D / D2H streams next to the compute stream
@@ -187,7 +189,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_merkle_nodes, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
                       &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -618,6 +620,7 @@ const char* ag_rs_status_string(int s) {
     case AG_RS_ERR_TOO_MUCH_DATA: return "too much data";
     case AG_RS_ERR_INVALID_PADDING: return "invalid padding";
     case AG_RS_ERR_INVALID_LAYOUT: return "invalid layout";
+    case AG_RS_ERR_BAD_ENCODING: return "bad encoding";
     case AG_RS_ERR_INVALID_ARGUMENT: return "invalid argument";
     case AG_RS_ERR_NO_DEVICE: return "no HIP device";
     case AG_RS_ERR_DEVICE: return "HIP runtime error";
@@ -903,6 +906,110 @@ int ag_merkle_verify_batch(ag_rs_ctx* c, size_t n, size_t leaf_bytes, const uint
   p.n = n;
   p.ok = ok;
   return ag::launch_merkle_verify(p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+// ---- all-or-nothing payload transforms ------------------------------------------------
+
+int ag_aes128_encrypt_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]) {
+  if (!key || !in || !out) return AG_RS_ERR_INVALID_ARGUMENT;
+  ag::aes128_encrypt_block(key, in, out);
+  return AG_RS_OK;
+}
+
+namespace {
+// lengths (host) -> device; the batch descriptor
+int aon_batch(ag_rs_ctx* c, size_t n, uint8_t* buffers, size_t stride, const uint32_t* lens, uint32_t extra,
+              ag::BufferBatch* bb) {
+  uint32_t mx = 0;
+  for (size_t b = 0; b < n; ++b) {
+    if (lens[b] > (1u << 28)) return AG_RS_ERR_INVALID_ARGUMENT;
+    mx = std::max(mx, lens[b]);
+  }
+  if (n > 1 && stride < static_cast<size_t>(mx) + extra) return AG_RS_ERR_INVALID_ARGUMENT;
+  int st = c->d_aon_lens.ensure(n * 4, c->stream);
+  if (st) return st;
+  AG_HIP(hipStreamSynchronize(c->stream));  // a previous call's upload may still be pending
+  AG_HIP(hipMemcpy(c->d_aon_lens.ptr, lens, n * 4, hipMemcpyHostToDevice));
+  bb->base = buffers;
+  bb->stride = stride;
+  bb->lens = c->d_aon_lens.as<uint32_t>();
+  bb->n = n;
+  bb->max_len = mx;
+  return AG_RS_OK;
+}
+}  // namespace
+
+int ag_cipher_apply_keystream_batch(ag_rs_ctx* c, size_t n, const uint8_t* keys, uint8_t* buffers, size_t stride,
+                                    const uint32_t* lens) {
+  if (!c || (n && (!keys || !buffers || !lens))) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  ag::BufferBatch bb;
+  int st = aon_batch(c, n, buffers, stride, lens, 0, &bb);
+  if (st) return st;
+  return ag::launch_apply_keystream(bb, keys, 0, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+int ag_sha256_batch(ag_rs_ctx* c, size_t n, const uint8_t* buffers, size_t stride, const uint32_t* lens,
+                    uint8_t* digests) {
+  if (!c || (n && (!buffers || !lens || !digests))) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  ag::BufferBatch bb;
+  int st = aon_batch(c, n, const_cast<uint8_t*>(buffers), stride, lens, 0, &bb);
+  if (st) return st;
+  return ag::launch_sha256(bb, 0, digests, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+int ag_aon_encrypt_batch(ag_rs_ctx* c, int scheme, size_t n, const uint8_t* keys, uint8_t* buffers, size_t stride,
+                         const uint32_t* lens) {
+  if (!c || (scheme != AG_AON_AONT && scheme != AG_AON_PETS) || (n && (!keys || !buffers || !lens)))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  ag::BufferBatch bb;
+  int st = aon_batch(c, n, buffers, stride, lens, ag::kCipherKeyBytes, &bb);
+  if (st) return st;
+  const bool aont = scheme == AG_AON_AONT;
+  if (aont && (st = c->d_aon_digests.ensure(n * 32, c->stream))) return st;
+  if (ag::launch_apply_keystream(bb, keys, 0, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  if (aont && ag::launch_sha256(bb, 0, c->d_aon_digests.as<uint8_t>(), c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  return ag::launch_write_key_tail(bb, aont, keys, aont ? c->d_aon_digests.as<uint8_t>() : nullptr, c->stream) ==
+                 hipSuccess
+             ? AG_RS_OK
+             : AG_RS_ERR_DEVICE;
+}
+
+int ag_aon_decrypt_batch(ag_rs_ctx* c, int scheme, size_t n, uint8_t* buffers, size_t stride, const uint32_t* lens,
+                         int64_t* plain_len_out) {
+  if (!c || (scheme != AG_AON_AONT && scheme != AG_AON_PETS) || (n && (!buffers || !lens || !plain_len_out)))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  // buffers too short for a key: BadEncoding, left untouched (length 16 => empty payload)
+  std::vector<uint32_t> lv(lens, lens + n);
+  for (size_t b = 0; b < n; ++b) {
+    plain_len_out[b] = lens[b] < ag::kCipherKeyBytes ? -AG_RS_ERR_BAD_ENCODING
+                                                      : static_cast<int64_t>(lens[b]) - ag::kCipherKeyBytes;
+    if (lens[b] < ag::kCipherKeyBytes) lv[b] = ag::kCipherKeyBytes;  // no-op (empty ciphertext, key unused)
+  }
+  ag::BufferBatch bb;
+  int st = aon_batch(c, n, buffers, stride, lv.data(), 0, &bb);
+  if (st) return st;
+  const bool aont = scheme == AG_AON_AONT;
+  if ((st = c->d_aon_keys.ensure(n * 16, c->stream))) return st;
+  if (aont) {
+    if ((st = c->d_aon_digests.ensure(n * 32, c->stream))) return st;
+    if (ag::launch_sha256(bb, ag::kCipherKeyBytes, c->d_aon_digests.as<uint8_t>(), c->stream) != hipSuccess)
+      return AG_RS_ERR_DEVICE;
+  }
+  if (ag::launch_derive_keys(bb, aont, aont ? c->d_aon_digests.as<uint8_t>() : nullptr, c->d_aon_keys.as<uint8_t>(),
+                             c->stream) != hipSuccess ||
+      ag::launch_apply_keystream(bb, c->d_aon_keys.as<uint8_t>(), ag::kCipherKeyBytes, c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  AG_HIP(hipStreamSynchronize(c->stream));
+  return AG_RS_OK;
 }
 
 }  // extern "C"

@@ -136,6 +136,11 @@ def load():
         "ag_merkle_node_count": ([sz], sz),
         "ag_merkle_build_batch": ([p, sz, sz, sz, p, sz, sz, p, p, sz, p, sz], i),
         "ag_merkle_verify_batch": ([p, sz, sz, p, sz, p, p, sz, p, sz, sz, p], i),
+        "ag_aes128_encrypt_block": ([p, p, p], i),
+        "ag_cipher_apply_keystream_batch": ([p, sz, p, p, sz, p], i),
+        "ag_sha256_batch": ([p, sz, p, sz, p, p], i),
+        "ag_aon_encrypt_batch": ([p, i, sz, p, p, sz, p], i),
+        "ag_aon_decrypt_batch": ([p, i, sz, p, sz, p, p], i),
     }
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
@@ -470,3 +475,57 @@ def merkle_verify_batch(ctx: Context, n: int, leaf_bytes: int, leaves, leaf_stri
     _check(load().ag_merkle_verify_batch(ctx.handle, n, leaf_bytes, _ptr(leaves), leaf_stride, _ptr(index),
                                          _ptr(roots), roots_stride, _ptr(proofs), proofs_stride, height,
                                          _ptr(ok)), "ag_merkle_verify_batch")
+
+
+# ---- all-or-nothing payload transforms (AONT / PETS; shredder.rs:403-528) -------------
+
+AON_AONT, AON_PETS = 0, 1
+
+
+def aes128_encrypt_block(key: bytes, block: bytes) -> bytes:
+    """One AES-128 block with the library's tables (host)."""
+    out = ctypes.create_string_buffer(16)
+    _check(load().ag_aes128_encrypt_block(bytes(key), bytes(block), out), "ag_aes128_encrypt_block")
+    return out.raw
+
+
+def _u32(lens, n):
+    import numpy as np
+
+    a = np.ascontiguousarray(np.asarray(lens, dtype=np.uint32))
+    if a.size != n:
+        raise ValueError("lens does not match the batch")
+    return a
+
+
+def cipher_apply_keystream_batch(ctx: Context, n: int, keys, buffers, stride: int, lens):
+    """cipher::apply_keystream on n device buffers (keys: device, 16 B each)."""
+    a = _u32(lens, n)
+    _check(load().ag_cipher_apply_keystream_batch(ctx.handle, n, _ptr(keys), _ptr(buffers), stride, a.ctypes.data),
+           "ag_cipher_apply_keystream_batch")
+
+
+def sha256_batch(ctx: Context, n: int, buffers, stride: int, lens, digests):
+    """hash::hash of n device buffers into device digests (32 B each)."""
+    a = _u32(lens, n)
+    _check(load().ag_sha256_batch(ctx.handle, n, _ptr(buffers), stride, a.ctypes.data, _ptr(digests)),
+           "ag_sha256_batch")
+
+
+def aon_encrypt_batch(ctx: Context, scheme: int, n: int, keys, buffers, stride: int, lens):
+    """AONT / PETS shred-side payload transform, in place (payload || 16-byte key tail)."""
+    a = _u32(lens, n)
+    _check(load().ag_aon_encrypt_batch(ctx.handle, scheme, n, _ptr(keys), _ptr(buffers), stride, a.ctypes.data),
+           "ag_aon_encrypt_batch")
+
+
+def aon_decrypt_batch(ctx: Context, scheme: int, n: int, buffers, stride: int, lens):
+    """AONT / PETS deshred-side transform, in place.  Returns an int64 array: plaintext
+    lengths, or -AG_RS_ERR_BAD_ENCODING (23) for a buffer shorter than the key."""
+    import numpy as np
+
+    a = _u32(lens, n)
+    out = np.empty(n, np.int64)
+    _check(load().ag_aon_decrypt_batch(ctx.handle, scheme, n, _ptr(buffers), stride, a.ctypes.data, out.ctypes.data),
+           "ag_aon_decrypt_batch")
+    return out

@@ -18,6 +18,8 @@
  *   4. context / stream / utility
  *   5. ag_merkle_*     -- the slice Merkle tree over the shreds (crypto/merkle.rs,
  *      shredder.rs:628-632), batched on the device
+ *   6. ag_aon_* / ag_cipher_* / ag_sha256_* -- the AONT / PETS shredders' payload
+ *      transforms (shredder.rs:403-528, crypto/cipher.rs, crypto/hash.rs)
  *
  * Conventions: the caller owns every buffer; the library borrows them for the call
  * (reed_solomon.rs copies out of the crate's borrowed results, :118,125,187,226).  A
@@ -58,6 +60,7 @@ enum {
   AG_RS_ERR_TOO_MUCH_DATA = 20,               /* TooMuchData (reed_solomon.rs:20,29) */
   AG_RS_ERR_INVALID_PADDING = 21,             /* InvalidPadding (reed_solomon.rs:31) */
   AG_RS_ERR_INVALID_LAYOUT = 22,              /* DeshredError::InvalidLayout (shredder.rs:75) */
+  AG_RS_ERR_BAD_ENCODING = 23,                /* DeshredError::BadEncoding (decrypt_payload, shredder.rs:518) */
   AG_RS_ERR_INVALID_ARGUMENT = 100,
   AG_RS_ERR_NO_DEVICE = 101,                  /* no usable GPU: never a CPU fallback */
   AG_RS_ERR_DEVICE = 102,                     /* HIP runtime / kernel launch failure */
@@ -244,6 +247,33 @@ int ag_merkle_verify_batch(ag_rs_ctx* ctx, size_t n, size_t leaf_bytes, const ui
                            size_t leaf_stride, const uint32_t* index, const uint8_t* roots,
                            size_t roots_stride, const uint8_t* proofs, size_t proofs_stride, size_t height,
                            uint8_t* ok);
+
+/* ---- 6. all-or-nothing payload transforms (AONT / PETS shredders) ---------------------
+ * AontShredder::shred (shredder.rs:463-470): payload := AES-128-CTR_key(payload) ||
+ * (key ^ SHA-256(ciphertext)[0..16)); PetsShredder::shred (:414-418): ... || key.  The
+ * deshred side (decrypt_payload, :509-528) splits the 16-byte tail, derives the key (AONT:
+ * tail ^ SHA-256(ciphertext); PETS: the tail) and decrypts in place.  AES-128-CTR is
+ * cipher::apply_keystream (crypto/cipher.rs:25-30: ctr::Ctr64LE, all-zero IV); SHA-256 is
+ * hash::hash (crypto/hash.rs:64-67).  Buffers/keys/digests: device memory; lengths: HOST
+ * arrays.  Asynchronous on the context stream unless stated. */
+enum { AG_AON_AONT = 0, AG_AON_PETS = 1 };
+/* One AES-128 block with the library's tables (host; known-answer checks). */
+int ag_aes128_encrypt_block(const uint8_t key[16], const uint8_t in[16], uint8_t out[16]);
+/* apply_keystream to n buffers (buffer b: buffers + b*stride, lens[b] bytes, key keys + 16*b). */
+int ag_cipher_apply_keystream_batch(ag_rs_ctx* ctx, size_t n, const uint8_t* keys, uint8_t* buffers, size_t stride,
+                                    const uint32_t* lens);
+/* hash::hash of n buffers -> digests + 32*b. */
+int ag_sha256_batch(ag_rs_ctx* ctx, size_t n, const uint8_t* buffers, size_t stride, const uint32_t* lens,
+                    uint8_t* digests);
+/* The shred side: encrypt buffer b's lens[b] payload bytes in place under keys + 16*b and
+ * write the 16-byte tail after them (the buffer then holds lens[b] + 16 bytes). */
+int ag_aon_encrypt_batch(ag_rs_ctx* ctx, int scheme, size_t n, const uint8_t* keys, uint8_t* buffers, size_t stride,
+                         const uint32_t* lens);
+/* The deshred side: buffer b holds lens[b] bytes (ciphertext || tail); decrypts in place.
+ * plain_len_out (HOST): lens[b] - 16, or -AG_RS_ERR_BAD_ENCODING when lens[b] < 16.
+ * Synchronous. */
+int ag_aon_decrypt_batch(ag_rs_ctx* ctx, int scheme, size_t n, uint8_t* buffers, size_t stride, const uint32_t* lens,
+                         int64_t* plain_len_out);
 
 #ifdef __cplusplus
 }
