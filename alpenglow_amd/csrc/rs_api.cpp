@@ -354,6 +354,12 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   }
   std::vector<ag::SynPattern> syn;
   if (syn_chunk) syn.resize(npat);
+  // LowRate (next_pow2(k) = 32): recovery chunk j = FFT_{32(j+1)}(IFFT_0(originals)), so a
+  // fully present chunk inverts through the transform kernel: originals =
+  // FFT_0(IFFT_{32(j+1)}(chunk j)).  ANY_K only (MDS uniqueness), chunks j < 4.
+  const bool lr_geo = mode == AG_RS_DECODE_ANY_K && hr == 0 && next_pow2(k) == 32 && S % 64 == 0 && aligned;
+  std::vector<uint8_t> lr_chunk(npat, 0xFF);
+  bool any_lr = false;
   bool any_fast = false, any_generic = false, any_x = false, any_syn = false;
   for (size_t p = 0; p < npat; ++p) {
     size_t no = 0, nr = 0;
@@ -365,6 +371,19 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     } else if (fast_geo && nr == m) {
       cls[p] = 1;
       any_fast = true;
+    } else if (lr_geo && [&] {
+                 for (size_t j = 0; j < 4 && 32 * (j + 1) <= m; ++j) {
+                   bool full = true;
+                   for (size_t i = 32 * j; i < 32 * (j + 1) && full; ++i) full = rpres[p * m + i] != 0;
+                   if (full) {
+                     lr_chunk[p] = static_cast<uint8_t>(j);
+                     return true;
+                   }
+                 }
+                 return false;
+               }()) {
+      cls[p] = 5;
+      any_lr = true;
     } else if (syn_chunk && build_syn_pattern(k, m, opres + p * k, rpres + p * m, G.data(), &syn[p])) {
       cls[p] = 4;
       any_syn = true;
@@ -406,6 +425,38 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
     const auto kind = npts == 32 ? ag::XformKind::kDecode32 : ag::XformKind::kDecode64;
     if (ag::launch_xform(kind, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
+  if (any_lr) {
+    // one launch per recovery chunk in use; store masks select that chunk's patterns
+    for (unsigned j = 0; j < 4; ++j) {
+      std::vector<uint64_t> mask(npat, 0);
+      bool used = false;
+      for (size_t p = 0; p < npat; ++p)
+        if (cls[p] == 5 && lr_chunk[p] == j) {
+          used = true;
+          for (size_t i = 0; i < k; ++i)
+            if (!opres[p * k + i]) mask[p] |= uint64_t{1} << i;
+        }
+      if (!used) continue;
+      AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read mask_host
+      if ((st = c->d_mask.ensure(mask.size() * 8, c->stream))) return st;
+      c->mask_host = mask;
+      AG_HIP(hipMemcpyAsync(c->d_mask.ptr, c->mask_host.data(), mask.size() * 8, hipMemcpyHostToDevice, c->stream));
+      ag::XformParams p{};
+      p.in = rec + static_cast<size_t>(32) * j * S;
+      p.in_block_stride = rstride;
+      p.in_shard_stride = S;
+      p.out = orig;
+      p.out_block_stride = ostride;
+      p.out_shard_stride = S;
+      p.out_mask = c->d_mask.as<uint64_t>();
+      p.pattern_per_block = npat > 1 ? 1u : 0u;
+      p.n_in = 32;
+      p.n_out = static_cast<uint32_t>(k);
+      p.chunks_per_shard = static_cast<uint32_t>(S / 64);
+      p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
+      if (ag::launch_xform_lowrate_decode(j, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    }
   }
   if (any_syn) {
     // pattern upload only when (k, m, flags) changed; non-syndrome patterns stay zeroed

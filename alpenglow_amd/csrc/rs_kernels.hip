@@ -1613,6 +1613,21 @@ hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hi
   return hipGetLastError();
 }
 
+hipError_t launch_xform_lowrate_decode(unsigned j, const XformParams& p, hipStream_t stream) {
+  if (p.total_columns == 0) return hipSuccess;
+  const uint64_t tiles = (p.total_columns + 63) / 64;
+  if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<unsigned>(tiles));
+  switch (j) {
+    case 0: hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p); break;
+    case 1: hipLaunchKernelGGL((xform_kernel<4, 64, 0>), grid, dim3(256), 0, stream, p); break;
+    case 2: hipLaunchKernelGGL((xform_kernel<4, 96, 0>), grid, dim3(256), 0, stream, p); break;
+    case 3: hipLaunchKernelGGL((xform_kernel<4, 128, 0>), grid, dim3(256), 0, stream, p); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
   if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;

@@ -33,6 +33,9 @@ bool xform_supported(unsigned n);
 // LowRate encode, recovery chunk j: out = FFT_n(IFFT_n(in, 0), n * (j + 1)) for
 // n = next_pow2(k) in {32 (j < 4), 64 (j < 3)} -- the crate's LowRate encoder per chunk.
 hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hipStream_t stream);
+// LowRate decode from a fully present recovery chunk j < 4 (next_pow2(k) = 32):
+// originals = FFT_0(IFFT_{32(j+1)}(chunk j)); in = chunk j, out = originals (masked).
+hipError_t launch_xform_lowrate_decode(unsigned j, const XformParams& p, hipStream_t stream);
 // Multi-chunk HighRate encode with chunk = next_pow2(m) in {1, 2, 4} and k <= 64:
 // in = originals (n_in = k), out = recovery (n_out = m).  out_mask unused.
 hipError_t launch_encode_mc(unsigned chunk, const XformParams& p, hipStream_t stream);

@@ -30,6 +30,9 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--exact", action="store_true", help="crate decoder (EXACT) instead of ANY_K")
+    ap.add_argument("--coding-only", action="store_true",
+                    help="CodingOnlyShredder shape: 32:64, deshred from coding shreds 32..63 (the "
+                         "reference bench drops the first 32 output shreds)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     import numpy as np
@@ -42,13 +45,15 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    n, S, m = args.slices, 1024, 32
+    n, S, m = args.slices, 1024, (64 if args.coding_only else 32)
     L = 32 * S - 1  # MAX_DATA_PER_SLICE payload: pads to S = 1024 (reed_solomon.rs:94-95)
     stride = (32 + m) * S
     cw = torch.empty((n, stride), dtype=torch.uint8, device=dev)
     rs.fill_splitmix(ctx, cw, n, 32 * S, stride, 0xC0DE0000)  # payload bytes in the data regions
     lens = np.full(n, L, np.uint32)
     dpres, cpres = np.zeros(32 * n, np.uint8), np.ones(m * n, np.uint8)
+    if args.coding_only:  # output shreds are the 64 coding shreds; the first 32 are dropped
+        cpres = np.tile(np.array([0] * 32 + [1] * 32, np.uint8), n)
     mode = rs.DECODE_EXACT if args.exact else rs.DECODE_ANY_K
 
     def shred():
@@ -85,7 +90,7 @@ def main():
         spot &= host[i, :32 * S].tobytes() == b"".join(raw.data)
         spot &= host[i, 32 * S:].tobytes() == b"".join(raw.coding)
     line = {
-        "metric": "slices/s ReedSolomonCoder shred + deshred (32 data shreds lost), max slices",
+        "metric": "slices/s ReedSolomonCoder shred + deshred (first 32 output shreds lost), max slices",
         "value": n * args.steps / wall,
         "unit": "slices/s",
         "n_gpus": 1,
@@ -97,13 +102,15 @@ def main():
         "vs_baseline": None,
         "dtype": "u8 (GF(2^16) symbols)",
         "data": "synthetic (splitmix64 payloads, device-generated)",
-        "config": {"workload": f"{n} slices x {L} B payload, 32:32 shreds of {S} B, deshred from the 32 coding shreds",
+        "config": {"workload": f"{n} slices x {L} B payload, 32:{m} shreds of {S} B, deshred from "
+                               + ("coding shreds 32..63 (CodingOnlyShredder)" if args.coding_only else
+                                  "the 32 coding shreds (RegularShredder)"),
                    "mode": "EXACT" if args.exact else "ANY_K"},
         "payload_GiBps": n * L * args.steps / wall / GIB,
         "calls_ms": {"shred_batch": t_sh * 1e3 / args.steps, "deshred_batch": t_de * 1e3 / args.steps},
         "verify": {"all_slices_restored": ok, "shreds_match_oracle": bool(spot)},
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and not args.coding_only:
         import ro_c
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
         ns = min(n, 2048)

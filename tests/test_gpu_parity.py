@@ -292,6 +292,40 @@ def test_syndrome_decode_per_block_patterns(ctx, dev, k, m, S, n):
     assert np.array_equal(got, blocks)
 
 
+@pytest.mark.parametrize("k,m,S,n", [(32, 64, 1024, 5), (20, 100, 128, 6), (32, 33, 4096, 3), (17, 128, 64, 9),
+                                     (32, 128, 256, 4)])
+def test_lowrate_decode_from_full_chunk(ctx, dev, k, m, S, n):
+    """LowRate decode through the transform (ANY_K): a fully present recovery chunk j gives
+    every original; CodingOnlyShredder's reference-bench pattern is 32:64 with chunk 1."""
+    rng = random.Random(k * 3 + m + S)
+    blocks = np.stack([np.frombuffer(o.block_bytes(1600 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    for j in range(min(4, m // 32)):
+        lost = rng.sample(range(k), rng.randint(1, k))
+        damaged = blocks.copy()
+        damaged[:, lost] = 0x3C
+        op = [0 if i in lost else 1 for i in range(k)]
+        rp = [1 if 32 * j <= i < 32 * (j + 1) else rng.randint(0, 1) for i in range(m)]
+        got = gpu_decode(ctx, dev, damaged, rec, op, rp, rs.DECODE_ANY_K)
+        assert np.array_equal(got, blocks), (j, lost)
+
+
+def test_lowrate_decode_per_block_chunks(ctx, dev):
+    """Per-block patterns over different recovery chunks (one launch per chunk in use)."""
+    k, m, S, n = 32, 64, 4096, 6
+    rng = random.Random(99)
+    blocks = np.stack([np.frombuffer(o.block_bytes(1700 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    op, rp, damaged = [], [], blocks.copy()
+    for b in range(n):
+        j = b % 2
+        lost = rng.sample(range(k), rng.randint(1, k))
+        damaged[b, lost] = 0
+        op += [0 if i in lost else 1 for i in range(k)]
+        rp += [1 if 32 * j <= i < 32 * (j + 1) else 0 for i in range(m)]
+    assert np.array_equal(gpu_decode(ctx, dev, damaged, rec, op, rp, rs.DECODE_ANY_K), blocks)
+
+
 def test_syndrome_decode_pattern_cache(ctx, dev):
     """Back-to-back syndrome decodes with different patterns of one shape."""
     k, m, S, n = 16, 4, 4096, 3
