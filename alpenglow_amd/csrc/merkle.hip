@@ -161,7 +161,8 @@ __global__ __launch_bounds__(256) void merkle_proof_kernel(const MerkleBuildPara
   }
 }
 
-// check_proof (merkle.rs:374-387, 417-428) for one leaf per thread.
+// check_proof (merkle.rs:374-387, 417-428) for one leaf per thread; derive_root (:411-428)
+// when roots_out is set.
 template <bool A4>
 __global__ __launch_bounds__(256) void merkle_verify_kernel(const MerkleVerifyParams p) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
@@ -177,6 +178,12 @@ __global__ __launch_bounds__(256) void merkle_verify_kernel(const MerkleVerifyPa
 #pragma unroll
     for (int i = 0; i < 8; ++i) node[i] = nn[i];
     idx >>= 1;
+  }
+  if (p.roots_out) {  // derive_root: the root digest bytes (big-endian words)
+    uint32_t* o = reinterpret_cast<uint32_t*>(p.roots_out + 32 * t);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = sha::bswap(node[i]);
+    return;
   }
   uint32_t root[8];
   load_digest(p.roots + t * p.roots_stride, root);

@@ -32,7 +32,7 @@ struct MerkleBuildParams {
 hipError_t launch_merkle_build(const MerkleBuildParams& p, uint8_t* nodes, uint64_t nodes_stride,
                                hipStream_t stream);
 
-// check_proof for n leaves: leaf t at leaves + t*leaf_stride, its index index[t], the root
+// check_proof for n leaves (or, with roots_out set, derive_root: the root each proof yields): leaf t at leaves + t*leaf_stride, its index index[t], the root
 // roots + t*roots_stride, height proof digests at proofs + t*proofs_stride; ok[t] = 0/1.
 struct MerkleVerifyParams {
   const uint8_t* leaves;
@@ -46,6 +46,7 @@ struct MerkleVerifyParams {
   uint64_t proofs_stride;
   uint64_t n;
   uint8_t* ok;
+  uint8_t* roots_out;  // derive_root mode (merkle.rs:411-428): root digests out, 32 B each; ok unused
 };
 hipError_t launch_merkle_verify(const MerkleVerifyParams& p, hipStream_t stream);
 

@@ -20,6 +20,7 @@
 #include "../../include/alpenglow_rs.h"
 #include "gf16.hpp"
 #include "cipher.hpp"
+#include "ed25519.hpp"
 #include "merkle.hpp"
 #include "rs_launch.hpp"
 
@@ -112,6 +113,8 @@ struct ag_rs_ctx {
   DevBuf d_merkle_nodes;                    // Merkle node scratch (callers without a nodes buffer)
   DevBuf d_aon_lens, d_aon_digests, d_aon_keys;  // all-or-nothing transforms
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
+  DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
+  DevBuf d_sh_roots, d_sh_commit, d_sh_onvalid, d_sh_list;  // shred validation scratch
   DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
   // host-memory calls: two staging slots, H2D / D2H streams next to the compute stream
   struct Slot {
@@ -189,7 +192,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &stage_in, &stage_out, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &one_in,
                       &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -1464,6 +1467,200 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   }
   AG_HIP(hipStreamSynchronize(c->stream));
   return AG_RS_OK;
+}
+
+// ---- Ed25519 shred signatures ------------------------------------------------------------
+
+namespace {
+int ensure_ed_base(ag_rs_ctx* c) {
+  if (c->d_ed_base.ptr) return AG_RS_OK;
+  int st = c->d_ed_base.ensure(ag::kEdBaseTableBytes, c->stream);
+  if (st) return st;
+  return ag::launch_ed25519_init(c->d_ed_base.as<int32_t>(), c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+constexpr size_t kMaxSigBatch = size_t{1} << 31;
+}  // namespace
+
+int ag_ed25519_public_key_batch(ag_rs_ctx* c, size_t n, const uint8_t* seeds, uint8_t* pks) {
+  if (!c || n >= kMaxSigBatch || (n && (!seeds || !pks))) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  int st = ensure_ed_base(c);
+  if (st) return st;
+  return ag::launch_ed25519_public_key(seeds, pks, n, c->d_ed_base.as<int32_t>(), c->stream) == hipSuccess
+             ? AG_RS_OK
+             : AG_RS_ERR_DEVICE;
+}
+
+int ag_ed25519_sign_batch(ag_rs_ctx* c, size_t n, const uint8_t* seeds, size_t seed_stride, const uint8_t* pks,
+                          size_t pk_stride, const uint8_t* msgs, size_t msg_stride, size_t msg_len, uint8_t* sigs) {
+  if (!c || n >= kMaxSigBatch || msg_len >= (size_t{1} << 28) ||
+      (n && (!seeds || !pks || !sigs || (msg_len && !msgs))))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  int st = ensure_ed_base(c);
+  if (st) return st;
+  ag::EdSignParams p{};
+  p.seeds = seeds;
+  p.seed_stride = seed_stride;
+  p.pks = pks;
+  p.pk_stride = pk_stride;
+  p.msgs = msgs;
+  p.msg_stride = msg_stride;
+  p.msg_len = static_cast<uint32_t>(msg_len);
+  p.sigs = sigs;
+  p.n = n;
+  p.base_table = c->d_ed_base.as<int32_t>();
+  return ag::launch_ed25519_sign(p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+int ag_ed25519_verify_batch(ag_rs_ctx* c, size_t n, const uint8_t* pks, size_t pk_stride, const uint8_t* msgs,
+                            size_t msg_stride, const uint32_t* msg_lens, size_t msg_len, const uint8_t* sigs,
+                            size_t sig_stride, uint8_t* ok) {
+  if (!c || n >= kMaxSigBatch || msg_len >= (size_t{1} << 28) || (n && (!pks || !sigs || !ok)) ||
+      (n && !msgs && (msg_lens || msg_len)))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  int st = ensure_ed_base(c);
+  if (st) return st;
+  ag::EdVerifyParams p{};
+  p.pks = pks;
+  p.pk_stride = pk_stride;
+  p.msgs = msgs;
+  p.msg_stride = msg_stride;
+  p.msg_lens = msg_lens;
+  p.msg_len = static_cast<uint32_t>(msg_len);
+  p.sigs = sigs;
+  p.sig_stride = sig_stride;
+  p.n = n;
+  p.ok = ok;
+  p.base_table = c->d_ed_base.as<int32_t>();
+  return ag::launch_ed25519_verify(p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+int ag_shred_validate_batch(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data_stride, size_t data_bytes,
+                            const uint32_t* shred_index, const uint8_t* proofs, size_t proofs_stride, size_t height,
+                            const uint64_t* slots, const uint64_t* slice_indices, const uint8_t* is_last,
+                            const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
+                            const uint8_t* has_cached, uint8_t* status, uint8_t* roots_out, uint8_t* commitments_out) {
+  if (!c || n >= kMaxSigBatch || data_bytes >= (size_t{1} << 28) ||
+      height > static_cast<size_t>(ag::kMerkleMaxHeight) ||
+      (n && (!shred_index || !slots || !slice_indices || !is_last || !sigs || !pk || !status ||
+             (data_bytes && !data) || (height && !proofs))) ||
+      (cached == nullptr) != (has_cached == nullptr) || proofs_stride % 16 ||
+      reinterpret_cast<uintptr_t>(proofs) % 16 || (n > 1 && data_stride < data_bytes))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  int st = ensure_ed_base(c);
+  if (st) return st;
+  uint8_t* roots = roots_out;
+  if (!roots) {
+    if ((st = c->d_sh_roots.ensure(32 * n, c->stream))) return st;
+    roots = c->d_sh_roots.as<uint8_t>();
+  }
+  uint8_t* commits = commitments_out;
+  if (!commits) {
+    if ((st = c->d_sh_commit.ensure(ag::kSliceCommitmentLen * n, c->stream))) return st;
+    commits = c->d_sh_commit.as<uint8_t>();
+  }
+  if ((st = c->d_sh_onvalid.ensure(n, c->stream)) || (st = c->d_sh_list.ensure(4 * (n + 1), c->stream))) return st;
+  uint32_t* list = c->d_sh_list.as<uint32_t>();
+  uint32_t* count = list + n;
+  // 1. Shred::slice_root (shredder.rs:168-175): derive_root from the Merkle path
+  ag::MerkleVerifyParams mp{};
+  mp.leaves = data;
+  mp.leaf_stride = data_stride;
+  mp.leaf_bytes = static_cast<uint32_t>(data_bytes);
+  mp.height = static_cast<uint32_t>(height);
+  mp.index = shred_index;
+  mp.proofs = proofs;
+  mp.proofs_stride = proofs_stride;
+  mp.n = n;
+  mp.roots_out = roots;
+  if (ag::launch_merkle_verify(mp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  // 2. SliceCommitment + cached-commitment rule (validated_shred.rs:57-64)
+  AG_HIP(hipMemsetAsync(count, 0, 4, c->stream));
+  ag::ShredCommitParams cp{};
+  cp.slots = slots;
+  cp.slice_indices = slice_indices;
+  cp.is_last = is_last;
+  cp.roots = roots;
+  cp.cached = cached;
+  cp.has_cached = has_cached;
+  cp.n = n;
+  cp.commitments = commits;
+  cp.status = status;
+  cp.on_valid = c->d_sh_onvalid.as<uint8_t>();
+  cp.list = list;
+  cp.list_count = count;
+  if (ag::launch_shred_commit(cp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  // 3. signature checks for the listed shreds (validated_shred.rs:65-77)
+  ag::EdVerifyParams vp{};
+  vp.pks = pk;
+  vp.pk_stride = 0;
+  vp.msgs = commits;
+  vp.msg_stride = ag::kSliceCommitmentLen;
+  vp.msg_len = ag::kSliceCommitmentLen;
+  vp.sigs = sigs;
+  vp.sig_stride = sig_stride;
+  vp.n = n;
+  vp.list = list;
+  vp.list_count = count;
+  vp.status = status;
+  vp.on_valid = c->d_sh_onvalid.as<uint8_t>();
+  vp.base_table = c->d_ed_base.as<int32_t>();
+  return ag::launch_ed25519_verify(vp, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+int ag_slice_sign_batch(ag_rs_ctx* c, size_t nslices, const uint8_t* seed, const uint8_t* pk, const uint64_t* slots,
+                        const uint64_t* slice_indices, const uint8_t* is_last, const uint8_t* roots, uint8_t* sigs,
+                        uint8_t* commitments_out) {
+  if (!c || nslices >= kMaxSigBatch ||
+      (nslices && (!seed || !pk || !slots || !slice_indices || !is_last || !roots || !sigs)))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (nslices == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  int st = ensure_ed_base(c);
+  if (st) return st;
+  uint8_t* commits = commitments_out;
+  if (!commits) {
+    if ((st = c->d_sh_commit.ensure(ag::kSliceCommitmentLen * nslices, c->stream))) return st;
+    commits = c->d_sh_commit.as<uint8_t>();
+  }
+  const size_t n = nslices;
+  if ((st = c->d_sh_onvalid.ensure(2 * n, c->stream)) || (st = c->d_sh_list.ensure(4 * (n + 1), c->stream)))
+    return st;
+  uint32_t* list = c->d_sh_list.as<uint32_t>();
+  AG_HIP(hipMemsetAsync(list + n, 0, 4, c->stream));
+  // SliceCommitment::new (shredder.rs:206-215); no cache, so every slice is listed
+  ag::ShredCommitParams cp{};
+  cp.slots = slots;
+  cp.slice_indices = slice_indices;
+  cp.is_last = is_last;
+  cp.roots = roots;
+  cp.n = n;
+  cp.commitments = commits;
+  cp.status = c->d_sh_onvalid.as<uint8_t>() + n;
+  cp.on_valid = c->d_sh_onvalid.as<uint8_t>();
+  cp.list = list;
+  cp.list_count = list + n;
+  if (ag::launch_shred_commit(cp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  // sk.sign_bytes(commitment) (shredder.rs:540)
+  ag::EdSignParams p{};
+  p.seeds = seed;
+  p.seed_stride = 0;
+  p.pks = pk;
+  p.pk_stride = 0;
+  p.msgs = commits;
+  p.msg_stride = ag::kSliceCommitmentLen;
+  p.msg_len = ag::kSliceCommitmentLen;
+  p.sigs = sigs;
+  p.n = n;
+  p.base_table = c->d_ed_base.as<int32_t>();
+  return ag::launch_ed25519_sign(p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
 }
 
 }  // extern "C"

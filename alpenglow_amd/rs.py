@@ -72,6 +72,12 @@ EXPORTS = (
     "ag_rs_decoder_restored_original", "ag_rs_decoder_free",
     "ag_rs_coder_new", "ag_rs_coder_free", "ag_rs_coder_shred", "ag_rs_coder_deshred",
     "ag_rs_coder_shred_batch", "ag_rs_coder_deshred_batch",
+    "ag_merkle_empty_root", "ag_merkle_height", "ag_merkle_node_count", "ag_merkle_build_batch",
+    "ag_merkle_verify_batch",
+    "ag_aes128_encrypt_block", "ag_cipher_apply_keystream_batch", "ag_sha256_batch", "ag_aon_encrypt_batch",
+    "ag_aon_decrypt_batch",
+    "ag_ed25519_public_key_batch", "ag_ed25519_sign_batch", "ag_ed25519_verify_batch", "ag_shred_validate_batch",
+    "ag_slice_sign_batch",
 )
 
 
@@ -141,6 +147,11 @@ def load():
         "ag_sha256_batch": ([p, sz, p, sz, p, p], i),
         "ag_aon_encrypt_batch": ([p, i, sz, p, p, sz, p], i),
         "ag_aon_decrypt_batch": ([p, i, sz, p, sz, p, p], i),
+        "ag_ed25519_public_key_batch": ([p, sz, p, p], i),
+        "ag_ed25519_sign_batch": ([p, sz, p, sz, p, sz, p, sz, sz, p], i),
+        "ag_ed25519_verify_batch": ([p, sz, p, sz, p, sz, p, sz, p, sz, p], i),
+        "ag_shred_validate_batch": ([p, sz, p, sz, sz, p, p, sz, sz, p, p, p, p, sz, p, p, p, p, p, p], i),
+        "ag_slice_sign_batch": ([p, sz, p, p, p, p, p, p, p, p], i),
     }
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
@@ -529,3 +540,53 @@ def aon_decrypt_batch(ctx: Context, scheme: int, n: int, buffers, stride: int, l
     _check(load().ag_aon_decrypt_batch(ctx.handle, scheme, n, _ptr(buffers), stride, a.ctypes.data, out.ctypes.data),
            "ag_aon_decrypt_batch")
     return out
+
+
+# ---- shred signatures (crypto/signature.rs; shredder/validated_shred.rs) --------------
+
+SLICE_COMMITMENT_LEN = 49
+SHRED_OK, SHRED_INVALID_SIGNATURE, SHRED_EQUIVOCATION = 0, 1, 2
+
+
+def _optr(x):
+    return _ptr(x) if x is not None else None
+
+
+def ed25519_public_key_batch(ctx: Context, n: int, seeds, pks):
+    """SecretKey::to_pk for n device seeds (32 B each) into device pks."""
+    _check(load().ag_ed25519_public_key_batch(ctx.handle, n, _ptr(seeds), _ptr(pks)), "ag_ed25519_public_key_batch")
+
+
+def ed25519_sign_batch(ctx: Context, n: int, seeds, seed_stride: int, pks, pk_stride: int, msgs, msg_stride: int,
+                       msg_len: int, sigs):
+    """SecretKey::sign_bytes for n device messages (64-byte signatures into sigs)."""
+    _check(load().ag_ed25519_sign_batch(ctx.handle, n, _ptr(seeds), seed_stride, _ptr(pks), pk_stride,
+                                        _optr(msgs), msg_stride, msg_len, _ptr(sigs)), "ag_ed25519_sign_batch")
+
+
+def ed25519_verify_batch(ctx: Context, n: int, pks, pk_stride: int, msgs, msg_stride: int, sigs, sig_stride: int,
+                         ok, msg_len: int = 0, msg_lens=None):
+    """Signature::verify_bytes for n device triples; ok[t] = 1 / 0 (device)."""
+    _check(load().ag_ed25519_verify_batch(ctx.handle, n, _ptr(pks), pk_stride, _optr(msgs), msg_stride,
+                                          _optr(msg_lens), msg_len, _ptr(sigs), sig_stride, _ptr(ok)),
+           "ag_ed25519_verify_batch")
+
+
+def shred_validate_batch(ctx: Context, n: int, data, data_stride: int, data_bytes: int, shred_index, proofs,
+                         proofs_stride: int, height: int, slots, slice_indices, is_last, sigs, sig_stride: int, pk,
+                         status, cached=None, has_cached=None, roots_out=None, commitments_out=None):
+    """ValidatedShred::try_new for n shreds of one leader (device buffers); status[t] gets
+    SHRED_OK / SHRED_INVALID_SIGNATURE / SHRED_EQUIVOCATION."""
+    _check(load().ag_shred_validate_batch(ctx.handle, n, _optr(data), data_stride, data_bytes, _ptr(shred_index),
+                                          _optr(proofs), proofs_stride, height, _ptr(slots), _ptr(slice_indices),
+                                          _ptr(is_last), _ptr(sigs), sig_stride, _ptr(pk), _optr(cached),
+                                          _optr(has_cached), _ptr(status), _optr(roots_out),
+                                          _optr(commitments_out)), "ag_shred_validate_batch")
+
+
+def slice_sign_batch(ctx: Context, nslices: int, seed, pk, slots, slice_indices, is_last, roots, sigs,
+                     commitments_out=None):
+    """The shred side's slice signatures (shredder.rs:540) for nslices slices (device)."""
+    _check(load().ag_slice_sign_batch(ctx.handle, nslices, _ptr(seed), _ptr(pk), _ptr(slots), _ptr(slice_indices),
+                                      _ptr(is_last), _ptr(roots), _ptr(sigs), _optr(commitments_out)),
+           "ag_slice_sign_batch")

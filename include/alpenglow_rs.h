@@ -20,6 +20,9 @@
  *      shredder.rs:628-632), batched on the device
  *   6. ag_aon_* / ag_cipher_* / ag_sha256_* -- the AONT / PETS shredders' payload
  *      transforms (shredder.rs:403-528, crypto/cipher.rs, crypto/hash.rs)
+ *   7. ag_ed25519_* / ag_shred_validate_batch / ag_slice_sign_batch -- the leader's slice
+ *      signatures (crypto/signature.rs over ed25519-zebra 4.2.0) and the per-shred check
+ *      ValidatedShred::try_new (shredder/validated_shred.rs:52-81)
  *
  * Conventions: the caller owns every buffer; the library borrows them for the call
  * (reed_solomon.rs copies out of the crate's borrowed results, :118,125,187,226).  A
@@ -274,6 +277,48 @@ int ag_aon_encrypt_batch(ag_rs_ctx* ctx, int scheme, size_t n, const uint8_t* ke
  * Synchronous. */
 int ag_aon_decrypt_batch(ag_rs_ctx* ctx, int scheme, size_t n, uint8_t* buffers, size_t stride, const uint32_t* lens,
                          int64_t* plain_len_out);
+
+/* ---- 7. shred signatures (Ed25519) ----------------------------------------------------
+ * crypto/signature.rs wraps ed25519-zebra 4.2.0: RFC 8032 keys and signatures, ZIP-215
+ * verification (s < l required; A and R need only decode to curve points, non-canonical y
+ * accepted; accept iff [8]([s]B - [k]A - R) = 0 with k = SHA-512(R || A || M) mod l).
+ * Device-resident batches on the context stream; every pointer is device memory. */
+#define AG_SLICE_COMMITMENT_LEN 49
+enum { AG_SHRED_OK = 0, AG_SHRED_INVALID_SIGNATURE = 1, AG_SHRED_EQUIVOCATION = 2 };
+/* SecretKey::to_pk (signature.rs:54-58): 32-byte seeds -> 32-byte public keys. */
+int ag_ed25519_public_key_batch(ag_rs_ctx* ctx, size_t n, const uint8_t* seeds, uint8_t* pks);
+/* SecretKey::sign_bytes (signature.rs:69-72): sig t (64 B at sigs + 64*t) over msg_len bytes
+ * at msgs + t*msg_stride with seed seeds + t*seed_stride and its public key pks +
+ * t*pk_stride (strides 0: one key for the batch). */
+int ag_ed25519_sign_batch(ag_rs_ctx* ctx, size_t n, const uint8_t* seeds, size_t seed_stride, const uint8_t* pks,
+                          size_t pk_stride, const uint8_t* msgs, size_t msg_stride, size_t msg_len, uint8_t* sigs);
+/* Signature::verify_bytes (signature.rs:100-103): ok[t] = 1 / 0 for key pks + t*pk_stride,
+ * message msgs + t*msg_stride of msg_lens[t] bytes (msg_lens null: msg_len each), signature
+ * sigs + t*sig_stride. */
+int ag_ed25519_verify_batch(ag_rs_ctx* ctx, size_t n, const uint8_t* pks, size_t pk_stride, const uint8_t* msgs,
+                            size_t msg_stride, const uint32_t* msg_lens, size_t msg_len, const uint8_t* sigs,
+                            size_t sig_stride, uint8_t* ok);
+/* ValidatedShred::try_new (validated_shred.rs:52-81) for n shreds of one leader (pk):
+ * shred t has payload data + t*data_stride (data_bytes), index shred_index[t], Merkle path
+ * proofs + t*proofs_stride (height digests), header slots[t] / slice_indices[t] / is_last[t]
+ * and slice_sig sigs + t*sig_stride.  Its root is derived from the path (Shred::slice_root,
+ * shredder.rs:168-175), the SliceCommitment built (shredder.rs:206-215), and, when
+ * has_cached[t] (cached + 49*t is the commitment of an earlier shred of that slice), a match
+ * is OK without a signature check, a valid signature over a different commitment is
+ * AG_SHRED_EQUIVOCATION; otherwise the signature decides OK / AG_SHRED_INVALID_SIGNATURE.
+ * status[t] gets the verdict; roots_out (32 B each) and commitments_out (49 B each) are
+ * optional.  cached and has_cached are both null or both set. */
+int ag_shred_validate_batch(ag_rs_ctx* ctx, size_t n, const uint8_t* data, size_t data_stride, size_t data_bytes,
+                            const uint32_t* shred_index, const uint8_t* proofs, size_t proofs_stride, size_t height,
+                            const uint64_t* slots, const uint64_t* slice_indices, const uint8_t* is_last,
+                            const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
+                            const uint8_t* has_cached, uint8_t* status, uint8_t* roots_out, uint8_t* commitments_out);
+/* The shred side (shredder.rs:540): slice_sig = sign(SliceCommitment(header, root)) for
+ * nslices slices with one leader key (seed, pk: 32 B each); roots 32 B per slice; sigs 64 B
+ * per slice; commitments_out (49 B per slice) optional. */
+int ag_slice_sign_batch(ag_rs_ctx* ctx, size_t nslices, const uint8_t* seed, const uint8_t* pk, const uint64_t* slots,
+                        const uint64_t* slice_indices, const uint8_t* is_last, const uint8_t* roots, uint8_t* sigs,
+                        uint8_t* commitments_out);
 
 #ifdef __cplusplus
 }

@@ -25,7 +25,7 @@ def lib():
 def header_symbols():
     text = open(HEADER).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
-    return sorted(set(re.findall(r"\b(ag_rs_\w+)\s*\(", text)))
+    return sorted(set(re.findall(r"\b(ag_\w+)\s*\(", text)))
 
 
 def test_header_declares_what_python_binds():
@@ -35,7 +35,7 @@ def test_header_declares_what_python_binds():
 def test_library_exports_every_header_symbol(lib):
     out = subprocess.run(["nm", "-D", "--defined-only", rs.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout
-    exported = set(re.findall(r"\bT (ag_rs_\w+)", out))
+    exported = set(re.findall(r"\bT (ag_\w+)", out))
     missing = [s for s in header_symbols() if s not in exported]
     assert not missing, missing
     for s in header_symbols():
