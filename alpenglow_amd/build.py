@@ -27,13 +27,28 @@ ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else "hipcc")
 CXX = os.environ.get("CXX_HOST", "g++")
 
-SOURCES = ["rs_kernels.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "rs_api.cpp", "gf16.cpp"]
-HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_launch.hpp", "rs_consts.inc", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp"]
+SOURCES = ["rs_kernels.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hip", "rs_api.cpp", "gf16.cpp"]
+HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_launch.hpp", "rs_consts.inc", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp"]
 # -fno-slp-vectorize: the SLP vectoriser packs the bitsliced XOR networks into <2 x i32>
 # ops, which lengthens live ranges (measured +40 VGPRs on the transform kernel).
 HIP_FLAGS = [*os.environ.get("AG_RS_EXTRA_HIPFLAGS", "").split(),
              "-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
              "-Wall", "-Wno-unused-command-line-argument", f"-I{INCLUDE}", f"-I{CSRC}"]
+
+
+def _deps(source: str, seen=None) -> list[str]:
+    """The csrc headers `source` includes, transitively (rebuild only what a header touches)."""
+    import re
+
+    seen = set() if seen is None else seen
+    path = os.path.join(CSRC, source)
+    if not os.path.exists(path):
+        return []
+    for h in re.findall(r'#include "([^"/]+)"', open(path).read()):
+        if h not in seen:
+            seen.add(h)
+            _deps(h, seen)
+    return sorted(seen)
 
 
 def _run(cmd):
@@ -68,14 +83,13 @@ def build(force: bool = False) -> str:
         raise RuntimeError("hipcc not found: cannot build the HIP extension")
     gen_consts()
     os.makedirs(OBJDIR, exist_ok=True)
-    hdr_time = max(_mtime(os.path.join(CSRC, h)) for h in HEADERS)
-    hdr_time = max(hdr_time, _mtime(os.path.join(INCLUDE, "alpenglow_rs.h")))
     objs, jobs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(OBJDIR, s + ".o")
         objs.append(obj)
-        if force or _mtime(obj) < max(_mtime(src), hdr_time):
+        deps = [os.path.join(CSRC, h) for h in _deps(s)] + [os.path.join(INCLUDE, "alpenglow_rs.h")]
+        if force or _mtime(obj) < max(_mtime(src), *(_mtime(d) for d in deps)):
             jobs.append([HIPCC, *HIP_FLAGS, "-c", src, "-o", obj])
     with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         list(ex.map(_run, jobs))

@@ -21,6 +21,7 @@
 #include "gf16.hpp"
 #include "cipher.hpp"
 #include "ed25519.hpp"
+#include "wire.hpp"
 #include "merkle.hpp"
 #include "rs_launch.hpp"
 
@@ -1661,6 +1662,55 @@ int ag_slice_sign_batch(ag_rs_ctx* c, size_t nslices, const uint8_t* seed, const
   p.n = n;
   p.base_table = c->d_ed_base.as<int32_t>();
   return ag::launch_ed25519_sign(p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+// ---- shred wire format ----------------------------------------------------------------
+
+namespace {
+bool columns_ok(const ag_shred_columns* c) {
+  return c && c->kind && c->slot && c->slice_index && c->is_last && c->shred_index && c->data_len && c->sig &&
+         c->height && (c->data || c->data_stride == 0) && (c->proof || c->proof_stride == 0);
+}
+ag::ShredColumns to_columns(const ag_shred_columns* c) {
+  ag::ShredColumns r{};
+  r.kind = c->kind;
+  r.slot = c->slot;
+  r.slice_index = c->slice_index;
+  r.is_last = c->is_last;
+  r.shred_index = c->shred_index;
+  r.data = c->data;
+  r.data_stride = c->data_stride;
+  r.data_len = c->data_len;
+  r.sig = c->sig;
+  r.proof = c->proof;
+  r.proof_stride = c->proof_stride;
+  r.height = c->height;
+  return r;
+}
+}  // namespace
+
+int ag_shred_deserialize_batch(ag_rs_ctx* c, size_t n, const uint8_t* packets, size_t packet_stride,
+                               const uint32_t* packet_lens, const ag_shred_columns* cols, uint8_t* status) {
+  if (!c || n >= kMaxSigBatch || (n && (!packets || !packet_lens || !status || !columns_ok(cols))))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  return ag::launch_shred_deserialize(packets, packet_stride, packet_lens, n, to_columns(cols), status, c->stream) ==
+                 hipSuccess
+             ? AG_RS_OK
+             : AG_RS_ERR_DEVICE;
+}
+
+int ag_shred_serialize_batch(ag_rs_ctx* c, size_t n, const ag_shred_columns* cols, uint8_t* packets,
+                             size_t packet_stride, uint32_t* packet_lens) {
+  if (!c || n >= kMaxSigBatch || (n && (!packets || !packet_lens || !columns_ok(cols))))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (n == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  return ag::launch_shred_serialize(to_columns(cols), n, packets, packet_stride, packet_lens, c->stream) ==
+                 hipSuccess
+             ? AG_RS_OK
+             : AG_RS_ERR_DEVICE;
 }
 
 }  // extern "C"

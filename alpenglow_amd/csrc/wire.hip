@@ -1,0 +1,144 @@
+// Shred wire format on the device.
+//
+// A received datagram is one wincode-encoded `Shred` (shredder.rs:113-186; decoded by
+// network::deserialize, network.rs:52-64: DefaultConfig with preallocation capped at
+// MTU_BYTES, exact consumption).  Layout (bincode-compatible wincode 0.6):
+//   u32 variant | u64 slot | u64 slice_index | u8 is_last | u64 shred_index |
+//   u64 data_len | data | 64 B slice_sig | u64 proof_len | proof_len x 32 B
+// (oracle/shred_wire_oracle.py restates it; parity unpinned -- the reference holds no
+// serialized bytes).
+//
+// Kernels: one wave per packet.  Lane 0 reads the fixed fields and the two lengths (the
+// offsets depend on data_len), the wave then copies the data, signature and proof bytes
+// lane-parallel (byte-granular: the data starts at offset 37, unaligned).  The packet bytes
+// are read once and the columns written once: HBM-bound, ~1.3 KB per shred each way.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "wire.hpp"
+
+namespace ag {
+
+namespace {
+
+__device__ __forceinline__ uint64_t ld_u64(const uint8_t* p) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int i = 7; i >= 0; --i) v = (v << 8) | p[i];
+  return v;
+}
+__device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
+  return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
+}
+__device__ __forceinline__ void st_u64(uint8_t* p, uint64_t v) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) p[i] = static_cast<uint8_t>(v >> (8 * i));
+}
+
+__global__ __launch_bounds__(256) void shred_deserialize_kernel(const uint8_t* __restrict__ packets,
+                                                                uint64_t packet_stride,
+                                                                const uint32_t* __restrict__ packet_lens, uint64_t n,
+                                                                const ShredColumns c, uint8_t* __restrict__ status) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= n) return;
+  const uint8_t* pk = packets + t * packet_stride;
+  const uint32_t len = packet_lens[t];
+  // header parse (wave-uniform values; every lane reads the same bytes)
+  uint32_t st = kWireOk;
+  uint64_t dlen = 0, plen = 0;
+  if (len > packet_stride) st = kWireTooLarge;  // the caller's row cannot hold it: never read past it
+  else if (len < kShredHeadBytes) st = kWireMalformed;
+  uint32_t kind = 0, is_last = 0;
+  uint64_t slot = 0, si = 0, idx = 0;
+  if (st == kWireOk) {
+    kind = ld_u32(pk);
+    slot = ld_u64(pk + 4);
+    si = ld_u64(pk + 12);
+    is_last = pk[20];
+    idx = ld_u64(pk + 21);
+    dlen = ld_u64(pk + 29);
+    if (kind > 1 || is_last > 1 || si >= kMaxSlicesPerBlock || idx >= kTotalShreds || dlen > kMtuBytes ||
+        kShredHeadBytes + dlen + 64 + 8 > len)
+      st = kWireMalformed;
+  }
+  const uint32_t o_sig = kShredHeadBytes + static_cast<uint32_t>(dlen);
+  if (st == kWireOk) {
+    plen = ld_u64(pk + o_sig + 64);
+    if (plen * 32 > kMtuBytes || o_sig + 72 + 32 * plen != len) st = kWireMalformed;  // exact consumption
+  }
+  if (st == kWireOk && (dlen > c.data_stride || 32 * plen > c.proof_stride)) st = kWireTooLarge;
+  if (lane == 0) {
+    status[t] = static_cast<uint8_t>(st);
+    if (st == kWireOk) {
+      c.kind[t] = static_cast<uint8_t>(kind);
+      c.slot[t] = slot;
+      c.slice_index[t] = si;
+      c.is_last[t] = static_cast<uint8_t>(is_last);
+      c.shred_index[t] = static_cast<uint32_t>(idx);
+      c.data_len[t] = static_cast<uint32_t>(dlen);
+      c.height[t] = static_cast<uint32_t>(plen);
+    }
+  }
+  if (st != kWireOk) return;
+  uint8_t* dd = c.data + t * c.data_stride;
+  for (uint32_t i = lane; i < dlen; i += 64) dd[i] = pk[kShredHeadBytes + i];
+  c.sig[64 * t + lane] = pk[o_sig + lane];
+  uint8_t* pp = c.proof + t * c.proof_stride;
+  for (uint32_t i = lane; i < 32 * plen; i += 64) pp[i] = pk[o_sig + 72 + i];
+}
+
+__global__ __launch_bounds__(256) void shred_serialize_kernel(const ShredColumns c, uint64_t n,
+                                                              uint8_t* __restrict__ packets, uint64_t packet_stride,
+                                                              uint32_t* __restrict__ packet_lens) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (t >= n) return;
+  uint8_t* pk = packets + t * packet_stride;
+  const uint32_t dlen = c.data_len[t], plen = c.height[t];
+  const uint32_t o_sig = kShredHeadBytes + dlen;
+  if (dlen > c.data_stride || 32ull * plen > c.proof_stride || uint64_t{o_sig} + 72 + 32ull * plen > packet_stride) {
+    if (lane == 0) packet_lens[t] = 0;  // does not fit the caller's rows: nothing written
+    return;
+  }
+  if (lane == 0) {
+    const uint32_t kind = c.kind[t];
+    pk[0] = static_cast<uint8_t>(kind);
+    pk[1] = pk[2] = pk[3] = 0;
+    st_u64(pk + 4, c.slot[t]);
+    st_u64(pk + 12, c.slice_index[t]);
+    pk[20] = c.is_last[t] ? 1 : 0;
+    st_u64(pk + 21, c.shred_index[t]);
+    st_u64(pk + 29, dlen);
+    st_u64(pk + o_sig + 64, plen);
+    packet_lens[t] = o_sig + 72 + 32 * plen;
+  }
+  const uint8_t* dd = c.data + t * c.data_stride;
+  for (uint32_t i = lane; i < dlen; i += 64) pk[kShredHeadBytes + i] = dd[i];
+  pk[o_sig + lane] = c.sig[64 * t + lane];
+  const uint8_t* pp = c.proof + t * c.proof_stride;
+  for (uint32_t i = lane; i < 32 * plen; i += 64) pk[o_sig + 72 + i] = pp[i];
+}
+
+}  // namespace
+
+hipError_t launch_shred_deserialize(const uint8_t* packets, uint64_t packet_stride, const uint32_t* packet_lens,
+                                    uint64_t n, const ShredColumns& c, uint8_t* status, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if ((n + 3) / 4 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(shred_deserialize_kernel, dim3(static_cast<unsigned>((n + 3) / 4)), dim3(256), 0, stream,
+                     packets, packet_stride, packet_lens, n, c, status);
+  return hipGetLastError();
+}
+
+hipError_t launch_shred_serialize(const ShredColumns& c, uint64_t n, uint8_t* packets, uint64_t packet_stride,
+                                  uint32_t* packet_lens, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if ((n + 3) / 4 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(shred_serialize_kernel, dim3(static_cast<unsigned>((n + 3) / 4)), dim3(256), 0, stream, c, n,
+                     packets, packet_stride, packet_lens);
+  return hipGetLastError();
+}
+
+}  // namespace ag

@@ -77,7 +77,7 @@ EXPORTS = (
     "ag_aes128_encrypt_block", "ag_cipher_apply_keystream_batch", "ag_sha256_batch", "ag_aon_encrypt_batch",
     "ag_aon_decrypt_batch",
     "ag_ed25519_public_key_batch", "ag_ed25519_sign_batch", "ag_ed25519_verify_batch", "ag_shred_validate_batch",
-    "ag_slice_sign_batch",
+    "ag_slice_sign_batch", "ag_shred_deserialize_batch", "ag_shred_serialize_batch",
 )
 
 
@@ -152,6 +152,8 @@ def load():
         "ag_ed25519_verify_batch": ([p, sz, p, sz, p, sz, p, sz, p, sz, p], i),
         "ag_shred_validate_batch": ([p, sz, p, sz, sz, p, p, sz, sz, p, p, p, p, sz, p, p, p, p, p, p], i),
         "ag_slice_sign_batch": ([p, sz, p, p, p, p, p, p, p, p], i),
+        "ag_shred_deserialize_batch": ([p, sz, p, sz, p, p, p], i),
+        "ag_shred_serialize_batch": ([p, sz, p, p, sz, p], i),
     }
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
@@ -590,3 +592,35 @@ def slice_sign_batch(ctx: Context, nslices: int, seed, pk, slots, slice_indices,
     _check(load().ag_slice_sign_batch(ctx.handle, nslices, _ptr(seed), _ptr(pk), _ptr(slots), _ptr(slice_indices),
                                       _ptr(is_last), _ptr(roots), _ptr(sigs), _optr(commitments_out)),
            "ag_slice_sign_batch")
+
+
+# ---- shred wire format (shredder.rs:113-186, wincode 0.6; network.rs:52-64) -----------
+
+WIRE_OK, WIRE_MALFORMED, WIRE_TOO_LARGE = 0, 1, 2
+
+
+class ShredColumns(ctypes.Structure):
+    """ag_shred_columns: one device array per Shred field."""
+    _fields_ = [("kind", ctypes.c_void_p), ("slot", ctypes.c_void_p), ("slice_index", ctypes.c_void_p),
+                ("is_last", ctypes.c_void_p), ("shred_index", ctypes.c_void_p), ("data", ctypes.c_void_p),
+                ("data_stride", ctypes.c_size_t), ("data_len", ctypes.c_void_p), ("sig", ctypes.c_void_p),
+                ("proof", ctypes.c_void_p), ("proof_stride", ctypes.c_size_t), ("height", ctypes.c_void_p)]
+
+    @classmethod
+    def of(cls, kind, slot, slice_index, is_last, shred_index, data, data_stride, data_len, sig, proof,
+           proof_stride, height):
+        return cls(_ptr(kind), _ptr(slot), _ptr(slice_index), _ptr(is_last), _ptr(shred_index), _ptr(data),
+                   data_stride, _ptr(data_len), _ptr(sig), _ptr(proof), proof_stride, _ptr(height))
+
+
+def shred_deserialize_batch(ctx: Context, n: int, packets, packet_stride: int, packet_lens, cols: ShredColumns,
+                            status):
+    """network::deserialize::<Shred> for n device packets into device columns."""
+    _check(load().ag_shred_deserialize_batch(ctx.handle, n, _ptr(packets), packet_stride, _ptr(packet_lens),
+                                             ctypes.byref(cols), _ptr(status)), "ag_shred_deserialize_batch")
+
+
+def shred_serialize_batch(ctx: Context, n: int, cols: ShredColumns, packets, packet_stride: int, packet_lens):
+    """wincode::serialize(&Shred) for n shreds (device columns -> device packets)."""
+    _check(load().ag_shred_serialize_batch(ctx.handle, n, ctypes.byref(cols), _ptr(packets), packet_stride,
+                                           _ptr(packet_lens)), "ag_shred_serialize_batch")

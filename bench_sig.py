@@ -10,6 +10,9 @@ Timed kernels (device-resident inputs, HIP events on the launch stream):
             receive path's worst case, validated_shred.rs:52-81)
   cached    the same with every shred's cached commitment matching (no signature work)
   sign      the shred side: SliceCommitment + sign per slice (shredder.rs:540)
+  serialize / deserialize
+            the Shred datagram (wincode layout, shredder.rs:113-186; network.rs:52-64)
+            for every shred: columns -> packets and back (HBM-bound byte movement)
 The headline is verifications per second.  The kernels are VALU-bound (field multiplies,
 v_mad_i64_i32); the report gives the instruction-level estimate next to the rate.  CPU
 baselines (one host thread): the oracle (oracle/ed25519_oracle.py, pure Python, kind
@@ -67,10 +70,10 @@ def main():
     roots = torch.empty((n, 32), dtype=torch.uint8, device=dev)
     proofs = torch.empty((n, 32 * h * L), dtype=torch.uint8, device=dev)
     rs.merkle_build_batch(ctx, L, S, n, shreds, S, L * S, roots, None, 0, proofs, 32 * h * L)
-    slots = torch.full((n,), 4242, dtype=torch.int64, device=dev)
-    slice_idx = torch.arange(n, dtype=torch.int64, device=dev)
-    last = torch.zeros(n, dtype=torch.uint8, device=dev)
-    last[-1] = 1
+    # consecutive slices of consecutive slots (MAX_SLICES_PER_BLOCK = 1024 slices per slot)
+    slots = 4242 + torch.arange(n, dtype=torch.int64, device=dev) // 1024
+    slice_idx = torch.arange(n, dtype=torch.int64, device=dev) % 1024
+    last = ((slice_idx == 1023) | (torch.arange(n, device=dev) == n - 1)).to(torch.uint8)
     ssig = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
     commits = torch.zeros((n, 49), dtype=torch.uint8, device=dev)
     rs.slice_sign_batch(ctx, n, seed, pk, slots, slice_idx, last, roots, ssig, commits)
@@ -95,8 +98,34 @@ def main():
     def k_sign():
         rs.slice_sign_batch(ctx, n, seed, pk, slots, slice_idx, last, roots, ssig)
 
+    # wire format: the shreds as columns (data rows = the shreds themselves), packets back
+    NS = n * L
+    sh_kind = (sh_idx >= 32).to(torch.uint8)
+    sh_dlen = torch.full((NS,), S, dtype=torch.int32, device=dev)
+    sh_h = torch.full((NS,), h, dtype=torch.int32, device=dev)
+    sh_proofs = proofs.view(NS, 32 * h)
+    cols_in = rs.ShredColumns.of(sh_kind, sh_slot, sh_slice, sh_last, sh_idx, shreds, S, sh_dlen, sh_sig, sh_proofs,
+                                 32 * h, sh_h)
+    pstride = 1536
+    packets = torch.zeros((NS, pstride), dtype=torch.uint8, device=dev)
+    plens = torch.zeros(NS, dtype=torch.int32, device=dev)
+    out = {k: torch.zeros_like(v) for k, v in dict(kind=sh_kind, slot=sh_slot, slice=sh_slice, last=sh_last,
+                                                    idx=sh_idx, dlen=sh_dlen, h=sh_h).items()}
+    o_data = torch.zeros((NS, S), dtype=torch.uint8, device=dev)
+    o_sig = torch.zeros((NS, 64), dtype=torch.uint8, device=dev)
+    o_proof = torch.zeros((NS, 32 * h), dtype=torch.uint8, device=dev)
+    cols_out = rs.ShredColumns.of(out["kind"], out["slot"], out["slice"], out["last"], out["idx"], o_data, S,
+                                  out["dlen"], o_sig, o_proof, 32 * h, out["h"])
+    wstatus = torch.zeros(NS, dtype=torch.uint8, device=dev)
+
+    def k_ser():
+        rs.shred_serialize_batch(ctx, NS, cols_in, packets, pstride, plens)
+
+    def k_deser():
+        rs.shred_deserialize_batch(ctx, NS, packets, pstride, plens, cols_out, wstatus)
+
     phases = [("verify", k_verify), ("validate", lambda: k_validate(False)), ("cached", lambda: k_validate(True)),
-              ("sign", k_sign)]
+              ("sign", k_sign), ("serialize", k_ser), ("deserialize", k_deser)]
     for _ in range(args.warmup):
         for _, f in phases:
             f()
@@ -111,11 +140,14 @@ def main():
         torch.cuda.synchronize()
         res[name] = e0.elapsed_time(e1) / args.steps
     # correctness of what was timed
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
     verify_ok = bool(ok.all().item())
     k_validate(False)
     torch.cuda.synchronize()
     validate_ok = bool((status == 0).all().item())
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    wire_ok = bool((wstatus == 0).all().item()) and torch.equal(o_data, shreds.view(NS, S)) and \
+        torch.equal(o_proof, sh_proofs) and torch.equal(out["idx"], sh_idx) and torch.equal(o_sig, sh_sig)
+    import shred_wire_oracle as wo  # the checker (oracle/ is on sys.path)
     import ed25519_oracle as eo
     pkb = pk.cpu().numpy().tobytes()
     mh, sh = msgs[:4].cpu().numpy(), sigs[:4].cpu().numpy()
@@ -124,7 +156,13 @@ def main():
         sh[i].tobytes() == eo.sign(seed.cpu().numpy().tobytes(), mh[i].tobytes()) for i in range(4))
 
     rate = {"verify": N / (res["verify"] * 1e-3), "validate": n * L / (res["validate"] * 1e-3),
-            "cached": n * L / (res["cached"] * 1e-3), "sign": n / (res["sign"] * 1e-3)}
+            "cached": n * L / (res["cached"] * 1e-3), "sign": n / (res["sign"] * 1e-3),
+            "serialize": NS / (res["serialize"] * 1e-3), "deserialize": NS / (res["deserialize"] * 1e-3)}
+    pkt0 = packets[0, :int(plens[0].item())].cpu().numpy().tobytes()
+    wire_ok = wire_ok and wo.deserialize(pkt0) is not None and wo.serialize(*wo.deserialize(pkt0)) == pkt0
+    wire_bytes = 2 * int(plens.to(torch.int64).sum().item())  # packet bytes once + column bytes once
+    wire = {k: {"ms": res[k], "algorithmic_bytes": wire_bytes,
+                "achieved_GBps": wire_bytes / (res[k] * 1e-3) / 1e9} for k in ("serialize", "deserialize")}
     line = {
         "metric": "Ed25519 shred signature verifications/s (ZIP-215, 49-byte slice commitments, one leader key)",
         "value": rate["verify"],
@@ -145,9 +183,12 @@ def main():
                      "note": "compute-bound integer kernel: no HBM roofline applies (64 B of key/message/"
                              "signature per verification); see DESIGN.md §3.9 for the instruction estimate"},
         "kernels": {k: {"ms": res[k], "per_s": rate[k]} for k in res},
+        "wire_roofline": {k: {**v, "peak_GBps": 8000.0, "frac": v["achieved_GBps"] / 8000.0} for k, v in wire.items()},
         "rates": {"verify_per_s": rate["verify"], "validate_shreds_per_s": rate["validate"],
-                  "validate_cached_shreds_per_s": rate["cached"], "sign_slices_per_s": rate["sign"]},
+                  "validate_cached_shreds_per_s": rate["cached"], "sign_slices_per_s": rate["sign"],
+                  "serialize_shreds_per_s": rate["serialize"], "deserialize_shreds_per_s": rate["deserialize"]},
         "verify": {"all_signatures_accepted": verify_ok, "all_shreds_valid": validate_ok,
+                   "wire_round_trip": wire_ok,
                    "oracle_spot_check": oracle_ok},
     }
     if not args.no_cpu_baseline:

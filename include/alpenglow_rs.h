@@ -23,6 +23,8 @@
  *   7. ag_ed25519_* / ag_shred_validate_batch / ag_slice_sign_batch -- the leader's slice
  *      signatures (crypto/signature.rs over ed25519-zebra 4.2.0) and the per-shred check
  *      ValidatedShred::try_new (shredder/validated_shred.rs:52-81)
+ *   8. ag_shred_serialize_batch / ag_shred_deserialize_batch -- the Shred datagram
+ *      (shredder.rs:113-186 encoded by wincode 0.6; network.rs:52-64)
  *
  * Conventions: the caller owns every buffer; the library borrows them for the call
  * (reed_solomon.rs copies out of the crate's borrowed results, :118,125,187,226).  A
@@ -319,6 +321,39 @@ int ag_shred_validate_batch(ag_rs_ctx* ctx, size_t n, const uint8_t* data, size_
 int ag_slice_sign_batch(ag_rs_ctx* ctx, size_t nslices, const uint8_t* seed, const uint8_t* pk, const uint64_t* slots,
                         const uint64_t* slice_indices, const uint8_t* is_last, const uint8_t* roots, uint8_t* sigs,
                         uint8_t* commitments_out);
+
+/* ---- 8. shred wire format --------------------------------------------------------------
+ * One UDP datagram per Shred (shredder.rs:113-186), wincode 0.6 (bincode-compatible):
+ *   u32 variant (0 Data, 1 Coding) | u64 slot | u64 slice_index | u8 is_last |
+ *   u64 shred_index | u64 data_len | data | 64 B slice_sig | u64 proof_len | proof_len x 32 B
+ * decoded like network::deserialize (network.rs:52-64): preallocation capped at MTU (1500
+ * bytes), trailing bytes rejected; slice_index < 1024 and shred_index < 64
+ * (types/slice_index.rs:115-132, shred_index.rs:91-108).  Columns are device arrays. */
+typedef struct ag_shred_columns {
+  uint8_t* kind;          /* ShredPayloadType: 0 Data, 1 Coding */
+  uint64_t* slot;
+  uint64_t* slice_index;
+  uint8_t* is_last;
+  uint32_t* shred_index;
+  uint8_t* data;          /* row t at data + t*data_stride (capacity data_stride bytes) */
+  size_t data_stride;
+  uint32_t* data_len;
+  uint8_t* sig;           /* 64 B per shred */
+  uint8_t* proof;         /* row t at proof + t*proof_stride: height digests of 32 B */
+  size_t proof_stride;
+  uint32_t* height;
+} ag_shred_columns;
+enum { AG_WIRE_OK = 0, AG_WIRE_MALFORMED = 1, AG_WIRE_TOO_LARGE = 2 };
+/* Packets (device; packet t at packets + t*packet_stride, packet_lens[t] bytes) -> columns.
+ * status[t]: AG_WIRE_OK, AG_WIRE_MALFORMED (the reference's deserialize rejects it) or
+ * AG_WIRE_TOO_LARGE (valid, but wider than the caller's rows); columns are written only
+ * for AG_WIRE_OK. */
+int ag_shred_deserialize_batch(ag_rs_ctx* ctx, size_t n, const uint8_t* packets, size_t packet_stride,
+                               const uint32_t* packet_lens, const ag_shred_columns* cols, uint8_t* status);
+/* Columns -> packets; packet_lens[t] = encoded length, or 0 (packet untouched) when the
+ * shred does not fit packet_stride or its own rows. */
+int ag_shred_serialize_batch(ag_rs_ctx* ctx, size_t n, const ag_shred_columns* cols, uint8_t* packets,
+                             size_t packet_stride, uint32_t* packet_lens);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,12 @@ def golden():
 
 @pytest.fixture(scope="session")
 def ctx():
+    import torch
+
     from alpenglow_amd import rs
+    # torch's HIP runtime first: when the library's context initialises the device before
+    # torch does, torch then reports "No HIP GPUs are available" in that process
+    torch.zeros(1, device="cuda:0")
     c = rs.Context(0)
     yield c
     c.close()
