@@ -31,8 +31,12 @@ SOURCES = ["rs_kernels.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hi
 HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_launch.hpp", "rs_consts.inc", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp"]
 # -fno-slp-vectorize: the SLP vectoriser packs the bitsliced XOR networks into <2 x i32>
 # ops, which lengthens live ranges (measured +40 VGPRs on the transform kernel).
+# -amdgpu-promote-alloca-to-vector-limit=512: keeps decode_x's four-Russians tables
+# (4 x 16 words, wave-uniform picks) in VGPRs (v_movrels) instead of scratch; no other
+# kernel's code changes (checked on the ISA).
 HIP_FLAGS = [*os.environ.get("AG_RS_EXTRA_HIPFLAGS", "").split(),
              "-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
+             "-mllvm", "-amdgpu-promote-alloca-to-vector-limit=512",
              "-Wall", "-Wno-unused-command-line-argument", f"-I{INCLUDE}", f"-I{CSRC}"]
 
 
