@@ -36,8 +36,8 @@ GIB = float(1 << 30)
 def parse():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=30)
     ap.add_argument("--nblocks", type=int, default=4096, help="blocks per GPU (weak scaling)")
     ap.add_argument("--stream-blocks", type=int, default=0,
                     help="strong scaling: split one stream of this many blocks over the GPUs "
@@ -96,6 +96,8 @@ def main():
     cw_stride = (k + m) * S
 
     ctx = rs.Context(local)
+    if os.environ.get("AG_XFORM_VARIANT"):  # A/B aid (tools/ab_xform.py variants); 0 = default
+        rs.load().ag_rs_internal_set_xform_variant(int(os.environ["AG_XFORM_VARIANT"]))
     stream = torch.cuda.Stream(dev)  # explicit stream: torch work, kernels and events share it
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
@@ -175,8 +177,8 @@ def main():
 
     line = None
     if rank == 0:
-        # each byte went through encode and reconstruct
-        processed = (args.stream_blocks if args.stream_blocks else world * n) * B
+        # each byte went through encode and reconstruct, once per timed step
+        processed = (args.stream_blocks if args.stream_blocks else world * n) * B * args.steps
         enc_bytes = n * B * (1 + m / k)
         dec_bytes = n * B * (1 + e / k)
         kern = {

@@ -11,7 +11,7 @@ export TMPDIR=/tmp
 fatal() { case "$1" in 0|1) return 0 ;; *) echo "FATAL step exit $1"; exit "$1" ;; esac; }
 SKIP_PROF=1 bash tools/gpu_check.sh; rc=$?; fatal $rc; [ $rc = 0 ] || exit $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/prof -o kt --output-format csv -- \
-  python3 bench.py --steps 20 --warmup 2 --no-cpu-baseline --no-verify > $OUT/prof_bench.json 2> $OUT/prof.err
+  python3 bench.py --steps 20 --warmup 30 --no-cpu-baseline --no-verify > $OUT/prof_bench.json 2> $OUT/prof.err
 rc=$?; echo "rocprof kernel-trace exit $rc"; fatal $rc
 rm -rf $OUT/pmc
 PMC_PASSES="FETCH_SIZE;WRITE_SIZE;SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU;SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE" \

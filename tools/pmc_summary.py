@@ -22,7 +22,7 @@ vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(args.dir, "p*", "pmc_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        short = "encode" if "xform_kernel<4, 32, 0" in name else \
+        short = "encode" if ("xform8_kernel<32, 0" in name or "xform_kernel<4, 32, 0" in name) else \
                 "reconstruct" if ("xform8_kernel<0, 32" in name or "xform_kernel<4, 0, 32" in name) else \
                 name.split("(")[0].split("::")[-1][:60]
         vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
