@@ -31,12 +31,14 @@ SOURCES = ["rs_kernels.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hi
 HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_launch.hpp", "rs_consts.inc", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp"]
 # -fno-slp-vectorize: the SLP vectoriser packs the bitsliced XOR networks into <2 x i32>
 # ops, which lengthens live ranges (measured +40 VGPRs on the transform kernel).
-# -amdgpu-promote-alloca-to-vector-limit=512: keeps decode_x's four-Russians tables
-# (4 x 16 words, wave-uniform picks) in VGPRs (v_movrels) instead of scratch; no other
-# kernel's code changes (checked on the ISA).
+# -amdgpu-promote-alloca-to-vector-limit: keeps the four-Russians tables of decode_x and
+# decode_syn (4 x 16 words, wave-uniform picks) in VGPRs (v_movrels) instead of scratch.
+# rs_kernels.hip needs 2048 (at 512 two of decode_syn's four tables land in scratch; no
+# other RS kernel's VGPR or scratch use changes, checked with
+# -Rpass-analysis=kernel-resource-usage); the other sources keep 512, the setting their
+# kernels were measured with (2048 would change the Ed25519 kernels' scratch use).
 HIP_FLAGS = [*os.environ.get("AG_RS_EXTRA_HIPFLAGS", "").split(),
              "-O3", "-std=c++20", "-fPIC", f"--offload-arch={ARCH}", "-fno-slp-vectorize",
-             "-mllvm", "-amdgpu-promote-alloca-to-vector-limit=512",
              "-Wall", "-Wno-unused-command-line-argument", f"-I{INCLUDE}", f"-I{CSRC}"]
 
 
@@ -94,7 +96,9 @@ def build(force: bool = False) -> str:
         objs.append(obj)
         deps = [os.path.join(CSRC, h) for h in _deps(s)] + [os.path.join(INCLUDE, "alpenglow_rs.h")]
         if force or _mtime(obj) < max(_mtime(src), *(_mtime(d) for d in deps)):
-            jobs.append([HIPCC, *HIP_FLAGS, "-c", src, "-o", obj])
+            limit = 2048 if s == "rs_kernels.hip" else 512
+            jobs.append([HIPCC, *HIP_FLAGS, "-mllvm", f"-amdgpu-promote-alloca-to-vector-limit={limit}", "-c", src,
+                         "-o", obj])
     with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         list(ex.map(_run, jobs))
     if force or jobs or _mtime(LIB) < max(_mtime(o) for o in objs):

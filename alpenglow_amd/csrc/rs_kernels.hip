@@ -1225,10 +1225,15 @@ __device__ __forceinline__ void syn_load(const DecodeSynParams& p, const TileIO&
   });
 }
 
+#ifndef AG_SYN_RT4
+#define AG_SYN_RT4 1
+#endif
 template <int C>
 __global__ __launch_bounds__(256, 2) void decode_syn_kernel(const DecodeSynParams p) {
   constexpr int NCMAX = kMcMaxK / C;
+#if !AG_SYN_RT4
   __shared__ uint32_t stab[4][64 * 64];  // per wave: 4 groups x 16 entries x 64 lanes
+#endif
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint64_t tile = static_cast<uint64_t>(dev::xcd_tile(blockIdx.x, gridDim.x)) * 4 + wave;
@@ -1304,6 +1309,47 @@ __global__ __launch_bounds__(256, 2) void decode_syn_kernel(const DecodeSynParam
       });
       store_shard(p.orig + sp->out[a] * p.orig_shard_stride, io, io.valid, out);
     }
+  });
+#elif AG_SYN_RT4
+  // Four Russians in registers (mul_rt4's scheme): per syndrome b, the 16 XOR combinations
+  // of each 4-plane group (44 VALU) serve all e outputs; output plane o of Minv[a][b] S_b is
+  // the XOR of 4 entries picked by row o's wave-uniform nibbles (one v_movrels each).
+  // Syndromes, tables and outputs stay in VGPRs (2 waves per SIMD: 256 available).
+  uint32_t out[C][16];
+  static_for<C>([&](auto A) { static_for<16>([&](auto P) { out[decltype(A)::value][decltype(P)::value] = 0; }); });
+  // one set of 4 tables reused for every syndrome: LLVM promotes these allocas to VGPRs
+  // (dynamic picks = v_movrels) within its promote-alloca budget; a set per syndrome
+  // overflows the budget and lands in scratch
+  uint32_t t0[16], t1[16], t2[16], t3[16];
+  static_for<C>([&](auto B) {
+    constexpr int b = decltype(B)::value;
+    if (b < e) {
+      const uint32_t* x = raw[0][b];
+      auto fill = [&](uint32_t* t, const uint32_t* v) {
+        const u32x16 c = syn_table(v);
+        static_for<16>([&](auto V) { t[decltype(V)::value] = c[decltype(V)::value]; });
+      };
+      fill(t0, x);
+      fill(t1, x + 4);
+      fill(t2, x + 8);
+      fill(t3, x + 12);
+      static_for<C>([&](auto A) {
+        constexpr int a = decltype(A)::value;
+        if (a < e) {
+          const uint32_t* rows = sp->rows[a][b];
+          static_for<16>([&](auto O) {
+            constexpr int o = decltype(O)::value;
+            const uint32_t r = __builtin_amdgcn_readfirstlane(rows[o]);
+            out[a][o] = dev::xor3(out[a][o], t0[r & 15], t1[(r >> 4) & 15]) ^
+                        dev::xor3(t2[(r >> 8) & 15], t3[(r >> 12) & 15], 0u);
+          });
+        }
+      });
+    }
+  });
+  static_for<C>([&](auto A) {
+    constexpr int a = decltype(A)::value;
+    if (a < e) store_shard(p.orig + sp->out[a] * p.orig_shard_stride, io, io.valid, out[a]);
   });
 #else
   // Four Russians: per syndrome, the 16 XOR combinations of each 4-plane group go to this
