@@ -95,12 +95,23 @@ def build(force: bool = False) -> str:
         obj = os.path.join(OBJDIR, s + ".o")
         objs.append(obj)
         deps = [os.path.join(CSRC, h) for h in _deps(s)] + [os.path.join(INCLUDE, "alpenglow_rs.h")]
-        if force or _mtime(obj) < max(_mtime(src), *(_mtime(d) for d in deps)):
-            limit = 2048 if s == "rs_kernels.hip" else 512
-            jobs.append([HIPCC, *HIP_FLAGS, "-mllvm", f"-amdgpu-promote-alloca-to-vector-limit={limit}", "-c", src,
-                         "-o", obj])
+        limit = 2048 if s == "rs_kernels.hip" else 512
+        cmd = [HIPCC, *HIP_FLAGS, "-mllvm", f"-amdgpu-promote-alloca-to-vector-limit={limit}", "-c", src, "-o", obj]
+        # the stamp holds the full compile command: a flag change (AG_RS_EXTRA_HIPFLAGS
+        # diagnostics, the promote-alloca limit) rebuilds the object even when no file changed
+        stamp = obj + ".cmd"
+        old = open(stamp).read() if os.path.exists(stamp) else None
+        if force or old != " ".join(cmd) or _mtime(obj) < max(_mtime(src), *(_mtime(d) for d in deps)):
+            jobs.append((cmd, stamp))
+    def _compile(job):
+        cmd, stamp = job
+        if os.path.exists(stamp):
+            os.remove(stamp)
+        _run(cmd)
+        with open(stamp, "w") as f:
+            f.write(" ".join(cmd))
     with cf.ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
-        list(ex.map(_run, jobs))
+        list(ex.map(_compile, jobs))
     if force or jobs or _mtime(LIB) < max(_mtime(o) for o in objs):
         tmp = LIB + ".tmp"
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", tmp])

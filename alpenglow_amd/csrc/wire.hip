@@ -66,7 +66,8 @@ __global__ __launch_bounds__(256) void shred_deserialize_kernel(const uint8_t* _
   const uint32_t o_sig = kShredHeadBytes + static_cast<uint32_t>(dlen);
   if (st == kWireOk) {
     plen = ld_u64(pk + o_sig + 64);
-    if (plen * 32 > kMtuBytes || o_sig + 72 + 32 * plen != len) st = kWireMalformed;  // exact consumption
+    // bound plen before any multiply: 32 * plen wraps in u64 for plen >= 2^59
+    if (plen > kMtuBytes / 32 || o_sig + 72 + 32 * plen != len) st = kWireMalformed;  // exact consumption
   }
   if (st == kWireOk && (dlen > c.data_stride || 32 * plen > c.proof_stride)) st = kWireTooLarge;
   if (lane == 0) {

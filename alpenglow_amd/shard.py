@@ -26,3 +26,59 @@ def max_over_ranks(value: float, dist=None, device=None) -> float:
     t = torch.tensor([float(value)], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+# ---- the bench's per-rank plan (bench.py; tested under gloo in tests/test_dist.py) ----
+
+SEED_BASE = 0x5EED_A19E_0000_0000  # block b is seeded SEED_BASE + b
+
+
+class RankPlan:
+    """Which blocks of the global stream one rank owns and what it reports.
+
+    weak scaling   (``stream_blocks == 0``): every rank owns ``nblocks`` blocks, rank r the
+                   global blocks [r * nblocks, (r + 1) * nblocks);
+    strong scaling (``stream_blocks > 0``):  one stream of ``stream_blocks`` blocks split
+                   into contiguous ranges (``block_range``).
+    Block g of the stream is generated from seed ``SEED_BASE + g`` on whichever rank owns
+    it, so the ranks' blocks are disjoint parts of one stream."""
+
+    def __init__(self, rank: int, world: int, nblocks: int, stream_blocks: int = 0):
+        if world <= 0 or not 0 <= rank < world:
+            raise ValueError("bad rank/world")
+        self.rank, self.world = rank, world
+        if stream_blocks:
+            self.first, last = block_range(rank, world, stream_blocks)
+            self.nblocks = last - self.first
+            self.total = stream_blocks
+            self.scaling = "strong"
+        else:
+            self.first, self.nblocks = rank * nblocks, nblocks
+            self.total = world * nblocks
+            self.scaling = "weak"
+
+    @property
+    def seed_base(self) -> int:
+        return SEED_BASE + self.first
+
+    def processed_bytes(self, block_bytes: int, steps: int) -> int:
+        """Block payload bytes that went through the timed steps on all ranks together."""
+        return self.total * block_bytes * steps
+
+
+def erasure_patterns(plan: RankPlan, k: int, m: int, erased: int, lost_coding: int, random_patterns: bool):
+    """Per-block presence flags (opres: k per block, rpres: m per block) for the blocks of
+    ``plan``; one shared pattern (the first ``erased`` data and ``lost_coding`` coding
+    shreds lost) unless ``random_patterns``.  Random patterns are a function of the global
+    block index only, so they do not depend on the world size."""
+    if not random_patterns:
+        return [0] * erased + [1] * (k - erased), [0] * lost_coding + [1] * (m - lost_coding)
+    import random
+
+    opres, rpres = [], []
+    for g in range(plan.first, plan.first + plan.nblocks):
+        rng = random.Random(0xA1_0000_0000 + g)
+        lost, lost_r = set(rng.sample(range(k), erased)), set(rng.sample(range(m), lost_coding))
+        opres += [0 if i in lost else 1 for i in range(k)]
+        rpres += [0 if j in lost_r else 1 for j in range(m)]
+    return opres, rpres

@@ -77,15 +77,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from alpenglow_amd.shard import block_range, max_over_ranks
+    from alpenglow_amd.shard import RankPlan, erasure_patterns, max_over_ranks
 
     k, m, B = args.k, args.m, args.block_bytes
-    if args.stream_blocks:
-        first, last = block_range(rank, world, args.stream_blocks)
-        n = last - first
-    else:
-        n = args.nblocks
-        first = rank * n  # rank-disjoint blocks of one stream
+    plan = RankPlan(rank, world, args.nblocks, args.stream_blocks)
+    n = plan.nblocks
     if B % k or (B // k) % 2:
         raise SystemExit("block bytes must split into k even-sized shards")
     S = B // k
@@ -104,21 +100,10 @@ def main():
 
     # codeword buffer: block b = k data shards then m coding shards (HBM-resident)
     cw = torch.empty((n, cw_stride), dtype=torch.uint8, device=dev)
-    seed_base = 0x5EED_A19E_0000_0000 + first
+    seed_base = plan.seed_base
     rs.fill_splitmix(ctx, cw, n, k * S, cw_stride, seed_base)
     data_ptr, par_ptr = cw.data_ptr(), cw.data_ptr() + k * S
-    if args.random_patterns:  # per block: e random data shreds and lc random coding shreds lost
-        import random as _random
-
-        rng = _random.Random(0xA1 + first)
-        opres, rpres = [], []
-        for _ in range(n):
-            lost, lost_r = set(rng.sample(range(k), e)), set(rng.sample(range(m), lc))
-            opres += [0 if i in lost else 1 for i in range(k)]
-            rpres += [0 if j in lost_r else 1 for j in range(m)]
-    else:
-        opres = [0] * e + [1] * (k - e)
-        rpres = [0] * lc + [1] * (m - lc)
+    opres, rpres = erasure_patterns(plan, k, m, e, lc, args.random_patterns)
 
     def encode():
         rs.encode_batch(ctx, k, m, S, n, data_ptr, cw_stride, par_ptr, cw_stride)
@@ -165,20 +150,25 @@ def main():
     # regeneration of the data; and a 2-block bit-exact spot check of the parity vs oracle
     verify = None
     if not args.no_verify:
+        # zero every shred the decoder is told is absent (erased data AND lost coding), so a
+        # decoder that read an absent shred could not pass
         view = cw.view(n, k + m, S)
         lost = torch.tensor(opres, dtype=torch.uint8).view(-1, k)[: n if args.random_patterns else 1] == 0
+        lost_r = torch.tensor(rpres, dtype=torch.uint8).view(-1, m)[: n if args.random_patterns else 1] == 0
         view[:, :k][lost.to(dev).expand(n, k)] = 0
+        view[:, k:][lost_r.to(dev).expand(n, m)] = 0
         reconstruct()
         ref = torch.empty((n, k * S), dtype=torch.uint8, device=dev)
         rs.fill_splitmix(ctx, ref, n, k * S, k * S, seed_base)
         ok_rec = bool(torch.equal(cw[:, : k * S], ref))
         del ref
+        encode()  # restore the zeroed coding shreds for the CPU baseline's parity comparison
         verify = {"reconstruct_restores_all_blocks": ok_rec}
 
     line = None
     if rank == 0:
         # each byte went through encode and reconstruct, once per timed step
-        processed = (args.stream_blocks if args.stream_blocks else world * n) * B * args.steps
+        processed = plan.processed_bytes(B, args.steps)
         enc_bytes = n * B * (1 + m / k)
         dec_bytes = n * B * (1 + e / k)
         kern = {
@@ -199,7 +189,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
-            "scaling": "strong" if args.stream_blocks else "weak",
+            "scaling": plan.scaling,
             "vs_baseline": None,
             "dtype": "u8 (GF(2^16) symbols, bitsliced u32 planes)",
             "data": "synthetic (splitmix64 random blocks, device-generated)",

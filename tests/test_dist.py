@@ -62,3 +62,71 @@ def test_gloo_world2_max_and_coverage():
     for rank, t, cnt in res:
         assert t == 2.0          # slowest rank's time everywhere
         assert cnt == 65536      # blocks covered exactly once in total
+
+
+# ---- the bench's rank logic (bench.py uses exactly these) ----------------------------
+
+from alpenglow_amd.shard import SEED_BASE, RankPlan, erasure_patterns  # noqa: E402
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_rank_plan_weak_and_strong(world):
+    B, steps = 1 << 20, 20
+    weak = [RankPlan(r, world, 4096) for r in range(world)]
+    assert [p.first for p in weak] == [4096 * r for r in range(world)]
+    assert all(p.nblocks == 4096 and p.scaling == "weak" for p in weak)
+    assert {p.processed_bytes(B, steps) for p in weak} == {world * 4096 * B * steps}
+    strong = [RankPlan(r, world, 4096, stream_blocks=65536) for r in range(world)]
+    assert sum(p.nblocks for p in strong) == 65536 and all(p.scaling == "strong" for p in strong)
+    assert {p.processed_bytes(B, steps) for p in strong} == {65536 * B * steps}
+    # seeds: block g of the stream is SEED_BASE + g on whichever rank owns it
+    seeds = [p.seed_base + i for p in strong for i in range(p.nblocks)]
+    assert seeds == [SEED_BASE + g for g in range(65536)]
+
+
+def test_random_patterns_independent_of_world():
+    k, m, e, lc = 32, 32, 16, 8
+    whole = RankPlan(0, 1, 64)
+    o1, r1 = erasure_patterns(whole, k, m, e, lc, True)
+    parts = [erasure_patterns(RankPlan(r, 4, 16), k, m, e, lc, True) for r in range(4)]
+    assert sum((p[0] for p in parts), []) == o1 and sum((p[1] for p in parts), []) == r1
+    for b in range(64):
+        assert o1[b * k:(b + 1) * k].count(0) == e and r1[b * m:(b + 1) * m].count(0) == lc
+    o, r = erasure_patterns(whole, k, m, e, lc, False)
+    assert o == [0] * e + [1] * (k - e) and r == [0] * lc + [1] * (m - lc)
+
+
+def _bench_worker(rank, world, port, q):
+    import torch
+    import torch.distributed as dist
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    plan = RankPlan(rank, world, 0, stream_blocks=1001)
+    # every rank reports the bytes of the whole job; time is the slowest rank's
+    wall = max_over_ranks(0.5 * (rank + 1), dist)
+    own = torch.tensor([plan.first, plan.nblocks], dtype=torch.int64)
+    got = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+    dist.all_gather(got, own)
+    q.put((rank, wall, plan.processed_bytes(1 << 20, 5), [tuple(int(v) for v in g) for g in got]))
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_bench_rank_logic():
+    import torch.multiprocessing as mp
+
+    world, port = 2, _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, wall, processed, ranges in res:
+        assert wall == 1.0
+        assert processed == 1001 * (1 << 20) * 5
+        assert ranges == [(0, 501), (501, 500)]  # contiguous, disjoint, covering the stream

@@ -671,3 +671,42 @@ def test_host_memory_decode_pipeline(ctx, case):
     rs.decode_batch(ctx, k, m, S, n, orig.ctypes.data, k * S, recb.ctypes.data, m * S, op, rp, mode=mode,
                     memory=rs.MEM_HOST)
     assert np.array_equal(orig.reshape(n, k, S), blocks)
+
+
+# ------------------------------------------------- C4 sweep points at their full shard size
+
+@pytest.mark.parametrize("k,m,S,n", [(16, 4, 65536, 3), (16, 4, 262144, 2), (32, 32, 32768, 4),
+                                     (32, 32, 131072, 2), (64, 64, 16384, 3), (64, 64, 65536, 2)])
+def test_c4_large_shard_sizes(ctx, dev, k, m, S, n):
+    """BASELINE configs[3] block sizes above the other tests' shard sizes (S up to 256 KiB):
+    device-resident encode, then reconstruct with k/2 (at most m) data shards erased, and a
+    per-block random pattern that also loses coding shards (the general decoders), all
+    compared with the C oracle (catches 32-bit offset and tiling faults at these sizes)."""
+    assert rs.has_fast_path(k, m, S)
+    blocks = np.stack([np.frombuffer(o.block_bytes(5000 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = gpu_encode(ctx, dev, blocks, m)
+    assert np.array_equal(rec, ro_c.encode_blocks(blocks, m, threads=8))
+    e = min(k // 2, m)
+    damaged = blocks.copy()
+    damaged[:, :e] = 0
+    got = gpu_decode(ctx, dev, damaged, rec, [0] * e + [1] * (k - e), [1] * m, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
+    # per-block random patterns with lost coding shreds
+    rng = random.Random(k * 1000 + S)
+    lc = min(4, m - e) if m > e else 0
+    e2 = min(e, m - lc)
+    op, rp = [], []
+    damaged = blocks.copy()
+    rec2 = rec.copy()
+    for b in range(n):
+        lost = set(rng.sample(range(k), e2))
+        lost_r = set(rng.sample(range(m), lc))
+        op += [0 if i in lost else 1 for i in range(k)]
+        rp += [0 if j in lost_r else 1 for j in range(m)]
+        for i in lost:
+            damaged[b, i] = 0x5A
+        for j in lost_r:
+            rec2[b, j] = 0xA5
+    for mode in (rs.DECODE_ANY_K, rs.DECODE_EXACT):
+        got = gpu_decode(ctx, dev, damaged, rec2, op, rp, mode)
+        assert np.array_equal(got, blocks), mode

@@ -48,11 +48,28 @@ def malformed_variants(b: bytes):
     return out
 
 
+def huge_proof_len_variants(b: bytes):
+    """Proof lengths whose 32x product wraps in u64 (2^59 + h: 32 * that = 32 * h mod 2^64),
+    so an unguarded exact-length check would accept them; wincode's MTU cap rejects them."""
+    dlen = struct.unpack_from("<Q", b, 29)[0]
+    off = 37 + dlen + 64
+    h = struct.unpack_from("<Q", b, off)[0]
+    out = []
+    for v in (2**59 + h, 2**59, 2**63 + h, 2**64 - 1):
+        x = bytearray(b)
+        struct.pack_into("<Q", x, off, v)
+        out.append(bytes(x))
+    return out
+
+
 def test_oracle_rejects_malformed():
     rng = random.Random(2)
     b = wo.serialize(*_shred(rng))
     for bad in malformed_variants(b):
         assert wo.deserialize(bad) is None
+    for height in (0, 1, 6):
+        for bad in huge_proof_len_variants(wo.serialize(*_shred(rng, height=height))):
+            assert wo.deserialize(bad) is None
     # empty data, empty proof, kind/slice/shred at their maxima are fine
     edge = (wo.CODING, 2**64 - 1, 1023, True, 63, b"", bytes(64), [])
     assert wo.deserialize(wo.serialize(*edge)) == edge
@@ -131,6 +148,7 @@ def test_gpu_deserialize_matches_oracle(ctx):
         b = wo.serialize(*_shred(rng, S=rng.choice([0, 5, 1024]), height=rng.choice([0, 6])))
         pkts.append(b)
         pkts.extend(malformed_variants(b)[:: rng.choice([1, 2, 3])])
+        pkts.extend(huge_proof_len_variants(b))  # u64 wrap of 32 * proof_len (always included)
     big = wo.serialize(*_shred(rng, S=1024, height=10))   # valid, but wider than the proof rows
     pkts.append(big)
     n, stride = len(pkts), 1600
