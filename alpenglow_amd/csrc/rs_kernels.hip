@@ -14,6 +14,8 @@
 //   fill_splitmix     synthetic input blocks (bench / tests), generated on the device.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "rs_device.hpp"
 #include "rs_launch.hpp"
 
@@ -412,10 +414,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
 // =====================================================================================
 using Regs4 = uint32_t[4][16];
 
-template <int L>
-struct X8Layout {  // position bit held by slot bit k (sb) and by wave bit k (wb)
-  static constexpr int sb[2] = {L == 0 ? 0 : L == 3 ? 4 : 2, L >= 2 ? 3 : 1};
-  static constexpr int wb[3] = {L == 0 ? 2 : 0, L == 0 || L == 1 ? 3 : 1, L == 3 ? 2 : 4};
+// Position bits held by slot bits (S0, S1) and wave bits (W0, W1, W2).
+template <int S0, int S1, int W0, int W1, int W2>
+struct X8Lay {
+  static constexpr int sb[2] = {S0, S1};
+  static constexpr int wb[3] = {W0, W1, W2};
   static constexpr int pos(int w, int t) {
     return (((t >> 0) & 1) << sb[0]) | (((t >> 1) & 1) << sb[1]) | (((w >> 0) & 1) << wb[0]) |
            (((w >> 1) & 1) << wb[1]) | (((w >> 2) & 1) << wb[2]);
@@ -424,6 +427,18 @@ struct X8Layout {  // position bit held by slot bit k (sb) and by wave bit k (wb
   // wave bits whose position bit exceeds b (the ones a layer-b constant depends on)
   static constexpr int rel(int b) { return (wb[0] > b ? 1 : 0) | (wb[1] > b ? 2 : 0) | (wb[2] > b ? 4 : 0); }
 };
+template <int L>
+struct X8LayoutSel;
+template <>
+struct X8LayoutSel<0> { using T = X8Lay<0, 1, 2, 3, 4>; };
+template <>
+struct X8LayoutSel<1> { using T = X8Lay<2, 1, 0, 3, 4>; };
+template <>
+struct X8LayoutSel<2> { using T = X8Lay<2, 3, 0, 1, 4>; };
+template <>
+struct X8LayoutSel<3> { using T = X8Lay<4, 3, 0, 1, 2>; };
+template <int L>
+using X8Layout = typename X8LayoutSel<L>::T;
 
 constexpr int x8_popc(int m) { return (m & 1) + ((m >> 1) & 1) + ((m >> 2) & 1); }
 // wave bits selected by REL packed into the low bits, and back
@@ -442,50 +457,66 @@ constexpr int x8_expand(int v, int rel) {
   return w;
 }
 
-// The butterfly on slots (T, T | 2^i) of layer bit B in layout L for the wave bits V.
-template <int L, int B, bool INV, int DELTA, int T, int V>
-__device__ __forceinline__ void x8_bfly(uint32_t* x, uint32_t* y) {
-  using Lay = X8Layout<L>;
+// The butterfly on slots (T, T | 2^i) of layer bit B in layout Lay for the wave bits V.
+// FFT butterflies with upd_y false skip y ^= x (y's new value is never used).
+template <typename Lay, int B, bool INV, int DELTA, int T, int V>
+__device__ __forceinline__ void x8_bfly(uint32_t* x, uint32_t* y, bool upd_y) {
   constexpr int w = x8_expand(V, Lay::rel(B));
   constexpr int S = (Lay::pos(w, T) & ~((2 << B) - 1)) + (1 << B) + DELTA - 1;
-  if constexpr (INV) dev::ifft_bfly<S>(x, y); else dev::fft_bfly<S>(x, y);
+  if constexpr (INV) {
+    dev::ifft_bfly<S>(x, y);
+  } else {
+    if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(x, y);
+    if (upd_y) dev::xor_planes(y, x);
+  }
 }
-template <int L, int B, bool INV, int DELTA, int T>
-__device__ __forceinline__ void x8_bfly_w(int v, uint32_t* x, uint32_t* y) {
-  constexpr int n = 1 << x8_popc(X8Layout<L>::rel(B));
+template <typename Lay, int B, bool INV, int DELTA, int T>
+__device__ __forceinline__ void x8_bfly_w(int v, uint32_t* x, uint32_t* y, bool upd_y = true) {
+  constexpr int n = 1 << x8_popc(Lay::rel(B));
   if constexpr (n == 1) {
-    x8_bfly<L, B, INV, DELTA, T, 0>(x, y);
+    x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y);
   } else if constexpr (n == 2) {
-    if (v == 0) x8_bfly<L, B, INV, DELTA, T, 0>(x, y); else x8_bfly<L, B, INV, DELTA, T, 1>(x, y);
+    if (v == 0) x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); else x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y);
   } else if constexpr (n == 4) {
     switch (v) {
-      case 0: x8_bfly<L, B, INV, DELTA, T, 0>(x, y); break;
-      case 1: x8_bfly<L, B, INV, DELTA, T, 1>(x, y); break;
-      case 2: x8_bfly<L, B, INV, DELTA, T, 2>(x, y); break;
-      default: x8_bfly<L, B, INV, DELTA, T, 3>(x, y); break;
+      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); break;
+      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y); break;
+      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2>(x, y, upd_y); break;
+      default: x8_bfly<Lay, B, INV, DELTA, T, 3>(x, y, upd_y); break;
     }
   } else {
     switch (v) {
-      case 0: x8_bfly<L, B, INV, DELTA, T, 0>(x, y); break;
-      case 1: x8_bfly<L, B, INV, DELTA, T, 1>(x, y); break;
-      case 2: x8_bfly<L, B, INV, DELTA, T, 2>(x, y); break;
-      case 3: x8_bfly<L, B, INV, DELTA, T, 3>(x, y); break;
-      case 4: x8_bfly<L, B, INV, DELTA, T, 4>(x, y); break;
-      case 5: x8_bfly<L, B, INV, DELTA, T, 5>(x, y); break;
-      case 6: x8_bfly<L, B, INV, DELTA, T, 6>(x, y); break;
-      default: x8_bfly<L, B, INV, DELTA, T, 7>(x, y); break;
+      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); break;
+      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y); break;
+      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2>(x, y, upd_y); break;
+      case 3: x8_bfly<Lay, B, INV, DELTA, T, 3>(x, y, upd_y); break;
+      case 4: x8_bfly<Lay, B, INV, DELTA, T, 4>(x, y, upd_y); break;
+      case 5: x8_bfly<Lay, B, INV, DELTA, T, 5>(x, y, upd_y); break;
+      case 6: x8_bfly<Lay, B, INV, DELTA, T, 6>(x, y, upd_y); break;
+      default: x8_bfly<Lay, B, INV, DELTA, T, 7>(x, y, upd_y); break;
     }
   }
 }
-// One butterfly layer on position bit B in layout L (skew delta DELTA).
-template <int L, int B, bool INV, int DELTA>
+// One butterfly layer on position bit B in layout L (skew delta DELTA).  LIVE: the slots
+// that still carry needed values (half-pruned FFT); UPD_Y false: FFT x updates only.
+template <int L, int B, bool INV, int DELTA, int LIVE = 0xF, bool UPD_Y = true>
 __device__ __forceinline__ void x8_layer(int wave, Regs4& r) {
-  constexpr int i = X8Layout<L>::slot_of(B);
+  using Lay = X8Layout<L>;
+  constexpr int i = Lay::slot_of(B);
   static_assert(i >= 0, "layer bit must be a slot bit");
-  const int v = x8_compress<X8Layout<L>::rel(B)>(wave);
+  const int v = x8_compress<Lay::rel(B)>(wave);
   constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;  // the slots with bit i clear
-  x8_bfly_w<L, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)]);
-  x8_bfly_w<L, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)]);
+  if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)], UPD_Y);
+  if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)], UPD_Y);
+}
+template <typename Lay, int B, int DELTA, int LIVE>
+__device__ __forceinline__ void x8_layer_lay(int wave, Regs4& r) {
+  constexpr int i = Lay::slot_of(B);
+  static_assert(i >= 0, "layer bit must be a slot bit");
+  const int v = x8_compress<Lay::rel(B)>(wave);
+  constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;
+  if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, false, DELTA, t0>(v, r[t0], r[t0 | (1 << i)]);
+  if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, false, DELTA, t1>(v, r[t1], r[t1 | (1 << i)]);
 }
 
 // Slot bit I <-> wave bit J.  Slot t of wave w moves iff t_I != w_J: to slot t ^ 2^I of
@@ -509,7 +540,7 @@ __device__ __forceinline__ void x8_signal(uint32_t* f, uint32_t e, int lane) {
   if (lane == 0) __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int I, int J, int EP>
+template <int I, int J, int EP, int LIVE = 0xF>
 __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, X8Flags* fl, Regs4& r) {
   const int wj = (wave >> J) & 1;
   const int partner = wave ^ (1 << J);
@@ -520,7 +551,7 @@ __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, X8Flags*
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     constexpr int k = (t >> (1 - I)) & 1;  // the other slot bit: index within the pair
-    if (((t >> I) & 1) != wj) {
+    if (((LIVE >> t) & 1) && ((t >> I) & 1) != wj) {
       lds_put(lds, 2 * partner + k, lane, r[t]);
       __asm__ volatile("; x8_swap put %0" ::"n"(t));
     }
@@ -534,7 +565,7 @@ __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, X8Flags*
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     constexpr int k = (t >> (1 - I)) & 1;
-    if (((t >> I) & 1) != wj) {
+    if (((LIVE >> t) & 1) && ((t >> I) & 1) != wj) {
       lds_get(lds, 2 * wave + k, lane, r[t]);
       __asm__ volatile("; x8_swap get %0" ::"n"(t));
     }
@@ -549,7 +580,15 @@ __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, X8Flags*
 #ifndef AG_X8_WAVES_PER_EU
 #define AG_X8_WAVES_PER_EU 4
 #endif
-template <int DIN, int DOUT>
+// HALF: every stored output has position bit 4 clear (a decode whose erased originals all
+// lie in shards 0..15).  After FFT layer 4 only the x halves are needed (no y update),
+// and the remaining 16-point FFT runs on the two live slots per wave (slot bit 0 = p4 = 0)
+// with one slot moved per exchange; the stores are two shards per wave:
+//   H3 slots p4 p3 | waves p0 p1 p2   FFT b4 (x only), b3
+//   H2 slots p4 p2 | waves p0 p1 p3   FFT b2
+//   H1 slots p4 p1 | waves p0 p2 p3   FFT b1
+//   H0 slots p4 p0 | waves p1 p2 p3   FFT b0, store shards 2w, 2w + 1
+template <int DIN, int DOUT, bool HALF = false>
 __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const XformParams p) {
   __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
   __shared__ X8Flags flags;
@@ -602,6 +641,44 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
 #if !(AG_XF_DIAG & 4)
   x8_swap<0, 2, 3>(wave, lane, lds, &flags, r);
 #endif
+  if constexpr (HALF) {
+    using H3 = X8Lay<4, 3, 0, 1, 2>;
+    using H2 = X8Lay<4, 2, 0, 1, 3>;
+    using H1 = X8Lay<4, 1, 0, 2, 3>;
+    using H0 = X8Lay<4, 0, 1, 2, 3>;
+    static_assert(std::is_same_v<H3, X8Layout<3>>, "H3 is layout L3");
+    x8_layer<3, 4, true, DIN>(wave, r);
+    x8_layer<3, 4, false, DOUT, 0x5, false>(wave, r);
+    x8_layer_lay<H3, 3, DOUT, 0x5>(wave, r);
+    x8_swap<1, 2, 4, 0x5>(wave, lane, lds, &flags, r);
+    x8_layer_lay<H2, 2, DOUT, 0x5>(wave, r);
+    x8_swap<1, 1, 5, 0x5>(wave, lane, lds, &flags, r);
+    x8_layer_lay<H1, 1, DOUT, 0x5>(wave, r);
+    x8_swap<1, 0, 6, 0x5>(wave, lane, lds, &flags, r);
+    const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
+    uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    if (p.out_mask) {
+      if (!p.pattern_per_block) {
+        const uint64_t m = p.out_mask[0];
+        mask[0] = mask[1] = mask[2] = mask[3] = m;
+      } else {
+        static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[out_io.blk[decltype(Q)::value]]; });
+      }
+    }
+    uint32_t need = 0;
+    static_for<2>([&](auto U) {
+      const uint32_t sh = 2 * wave + decltype(U)::value;
+      if (sh < p.n_out && store_qmask(out_io, mask, sh)) need = 1;
+    });
+    if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+    x8_layer_lay<H0, 0, DOUT, 0x5>(wave, r);
+    static_for<2>([&](auto U) {
+      constexpr int t = 2 * decltype(U)::value;
+      const uint32_t sh = 2 * wave + (t >> 1);  // H0 position of live slot t
+      if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, store_qmask(out_io, mask, sh), r[t]);
+    });
+    return;
+  }
 #if !(AG_XF_DIAG & 8)
   x8_layer<3, 4, true, DIN>(wave, r);
   x8_layer<3, 4, false, DOUT>(wave, r);
@@ -1787,8 +1864,11 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
         hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);
       break;
     case XformKind::kDecode32:
+      // variant 5: no output pruning (A/B)
       if (xform_variant() == 3)
         hipLaunchKernelGGL((xform_kernel<4, 0, 32>), grid, dim3(256), 0, stream, p);
+      else if (p.out_low_half && xform_variant() != 5)
+        hipLaunchKernelGGL((xform8_kernel<0, 32, true>), grid, dim3(512), 0, stream, p);
       else
         hipLaunchKernelGGL((xform8_kernel<0, 32>), grid, dim3(512), 0, stream, p);
       break;

@@ -37,7 +37,7 @@ def parse():
     ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--nblocks", type=int, default=4096, help="blocks per GPU (weak scaling)")
     ap.add_argument("--stream-blocks", type=int, default=0,
                     help="strong scaling: split one stream of this many blocks over the GPUs "
@@ -58,6 +58,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time host-buffer calls")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-settle", action="store_true",
+                    help="skip the untimed clock-settle steps that follow the W warmup steps")
     return ap.parse_args()
 
 
@@ -120,12 +122,16 @@ def main():
 
     do_enc = args.only in ("both", "encode")
     do_dec = args.only in ("both", "decode")
-    encode()  # parity must exist before the first reconstruct
-    for _ in range(args.warmup):
+    def step():
         if do_enc:
             encode()
         if do_dec:
             reconstruct()
+
+    encode()  # parity must exist before the first reconstruct
+    for _ in range(args.warmup):
+        step()
+    settle = _settle(step, stream, torch) if not args.no_settle else 0
 
     ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     barrier()
@@ -187,6 +193,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "settle_steps": settle,
             "ms_per_step": ms_per_step,
             "higher_is_better": True,
             "scaling": plan.scaling,
@@ -225,6 +232,27 @@ def main():
     ctx.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def _settle(step, stream, torch, max_steps=200, min_steps=3, tol=0.01, window=4):
+    """Untimed steps after the W warmup steps until the GPU has reached its steady state:
+    a fresh box runs the first ~10-20 launches of each kernel 5-15% slower (clock ramp, cold
+    TLBs; profiles/r01_kernel_trace_steady.txt).  Stops once the last `window` step times
+    agree within `tol` (each step timed alone with HIP events on the launch stream), at
+    most `max_steps` steps (about 0.6 s at the headline shape).  Returns the steps run."""
+    times = []
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for i in range(max_steps):
+        ev0.record(stream)
+        step()
+        ev1.record(stream)
+        ev1.synchronize()
+        times.append(ev0.elapsed_time(ev1))
+        if i + 1 >= max(min_steps, window):
+            last = times[-window:]
+            if (max(last) - min(last)) <= tol * min(last):
+                return i + 1
+    return max_steps
 
 
 def _pmc_traffic(kernel, k, m, S, n):

@@ -710,3 +710,29 @@ def test_c4_large_shard_sizes(ctx, dev, k, m, S, n):
     for mode in (rs.DECODE_ANY_K, rs.DECODE_EXACT):
         got = gpu_decode(ctx, dev, damaged, rec2, op, rp, mode)
         assert np.array_equal(got, blocks), mode
+
+
+def test_fast_decode_low_half_pruned(ctx, dev):
+    """32:32 from the full recovery set with every erased original among shards 0..15: the
+    output-pruned transform (16-point FFT tail).  Per-block random subsets (1..16 erased,
+    incl. single shards), S = 4096 (whole tiles per block) and S = 64 (tiles straddle
+    blocks), against the original data."""
+    rng = random.Random(77)
+    k, m = 32, 32
+    for S, n in [(4096, 13), (64, 200)]:
+        blocks = np.stack([np.frombuffer(o.block_bytes(700 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+        rec = ro_c.encode_blocks(blocks, m, threads=8)
+        damaged = blocks.copy()
+        op = []
+        for b in range(n):
+            lost = set(rng.sample(range(16), rng.randint(1, 16)))
+            op += [0 if i in lost else 1 for i in range(k)]
+            for i in lost:
+                damaged[b, i] = 0xC3
+        got = gpu_decode(ctx, dev, damaged, rec, op, [1] * (m * n), rs.DECODE_ANY_K)
+        assert np.array_equal(got, blocks), S
+        # one shared pattern: shards 15 and 0 only
+        d1 = blocks.copy()
+        d1[:, [0, 15]] = 0
+        got = gpu_decode(ctx, dev, d1, rec, [0] + [1] * 14 + [0] + [1] * 16, [1] * m, rs.DECODE_ANY_K)
+        assert np.array_equal(got, blocks), S
