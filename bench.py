@@ -54,7 +54,7 @@ def parse():
     ap.add_argument("--only", choices=["both", "encode", "decode"], default="both",
                     help="profiling aid: time only one of the two kernels")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, cpus)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time host-buffer calls")
     ap.add_argument("--no-verify", action="store_true")
@@ -270,54 +270,105 @@ def _pmc_traffic(kernel, k, m, S, n):
         return None
 
 
+def _host_cpus():
+    """CPUs this process may use: the affinity set, capped by a cgroup CPU quota."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def _cpu_baseline(args, cw, k, m, S, e):
+    """The reference's CPU path timed on this host: oracle/rs_cpu_avx2.c restates the
+    crate's Avx2 engine (nibble-table vpshufb multiplies over the crate's chunk layout,
+    the per-call FWHT erasure locator of its decoder).  1 thread and all host CPUs, one
+    block per thread, on a bounded sample of the same device blocks (bit-exact against the
+    GPU's parity and restored shards), plus BASELINE configs[0] (one 64 KiB block) and the
+    reference's own benches/shredder.rs slice shape, single-threaded."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import numpy as np
 
     import ro_c
 
-    threads = args.cpu_threads or max(1, min(16, len(os.sched_getaffinity(0))))
-    n_probe = max(1, threads)
-    host = cw[: n_probe].cpu().numpy().reshape(n_probe, k + m, S)
-    data = np.ascontiguousarray(host[:, :k])
-    t = time.perf_counter()
-    rec = ro_c.encode_blocks(data, m, threads=threads)
-    te = time.perf_counter() - t
+    engine = "avx2" if ro_c.avx2_available() and S % 64 == 0 else "scalar"
+    nall = args.cpu_threads or _host_cpus()
     op = np.array([0] * e + [1] * (k - e), np.uint8)
     rp = np.array([0] * args.lose_coding + [1] * (m - args.lose_coding), np.uint8)
-    cwh = np.concatenate([data, rec], axis=1)
-    t = time.perf_counter()
-    out = ro_c.decode_blocks(cwh, k, op, rp, threads=threads)
-    td = time.perf_counter() - t
-    per_block = (te + td) / n_probe
-    nsample = int(min(cw.shape[0], max(n_probe, args.cpu_seconds / max(per_block, 1e-6))))
-    nsample = max(n_probe, nsample // n_probe * n_probe)
-    parity_ok = bool(np.array_equal(rec, host[:, k:])) and bool(np.array_equal(out, data))
-    if nsample > n_probe:
-        host = cw[:nsample].cpu().numpy().reshape(nsample, k + m, S)
+    B = k * S
+
+    def run(nblk, threads):
+        host = cw[:nblk].cpu().numpy().reshape(nblk, k + m, S)
         data = np.ascontiguousarray(host[:, :k])
         t = time.perf_counter()
-        rec = ro_c.encode_blocks(data, m, threads=threads)
+        rec = ro_c.encode_blocks(data, m, threads=threads, engine=engine)
         te = time.perf_counter() - t
         cwh = np.concatenate([data, rec], axis=1)
         t = time.perf_counter()
-        out = ro_c.decode_blocks(cwh, k, op, rp, threads=threads)
+        out = ro_c.decode_blocks(cwh, k, op, rp, threads=threads, engine=engine)
         td = time.perf_counter() - t
-        parity_ok = parity_ok and bool(np.array_equal(rec, host[:, k:])) and bool(np.array_equal(out, data))
-    B = k * S
+        ok = bool(np.array_equal(rec, host[:, k:])) and bool(np.array_equal(out, data))
+        return {"blocks": nblk, "threads": threads, "encode_GiBps": nblk * B / te / GIB,
+                "reconstruct_GiBps": nblk * B / td / GIB, "value": nblk * B / (te + td) / GIB,
+                "seconds": te + td, "gpu_parity_matches_cpu": ok}
+
+    # 1 thread: probe, then a sample of about a third of the budget
+    probe = run(2, 1)
+    n1 = int(max(2, min(cw.shape[0], args.cpu_seconds / 3 / max(probe["seconds"] / 2, 1e-6))))
+    t1 = run(n1, 1)
+    # all CPUs: one block per thread, about half the budget
+    per_block = t1["seconds"] / n1
+    nn = int(max(nall, min(cw.shape[0], args.cpu_seconds / 2 * nall / max(per_block, 1e-6))))
+    nn = max(nall, nn // nall * nall)
+    ta = run(min(nn, cw.shape[0]), nall)
+    extra = _cpu_reference_shapes(ro_c, np, engine)
     return {
-        "value": nsample * B / (te + td) / GIB,
+        "value": ta["value"],
         "unit": "GiB/s",
-        "cores": threads,
+        "cores": nall,
         "kind": "port",
-        "sample": f"{nsample} of the same {B >> 20} MiB blocks, {k}:{m} encode + reconstruct with "
-                  f"{e} data shreds erased, C oracle (scalar log/exp tables, crate algorithm), "
-                  f"{threads} threads one block each",
-        "encode_GiBps": nsample * B / te / GIB,
-        "reconstruct_GiBps": nsample * B / td / GIB,
-        "gpu_parity_matches_cpu": parity_ok,
+        "sample": f"{ta['blocks']} (all CPUs) and {t1['blocks']} (1 thread) of the same {B >> 20} MiB blocks, "
+                  f"{k}:{m} encode + reconstruct with {e} data shreds erased; oracle/rs_cpu_avx2.c, the "
+                  f"crate's {'Avx2' if engine == 'avx2' else 'scalar'} engine restated, one block per thread",
+        "encode_GiBps": ta["encode_GiBps"],
+        "reconstruct_GiBps": ta["reconstruct_GiBps"],
+        "threads_1": t1,
+        "threads_all": ta,
+        "host_cpus": nall,
+        "gpu_parity_matches_cpu": t1["gpu_parity_matches_cpu"] and ta["gpu_parity_matches_cpu"],
         "cpu": _cpu_model(),
+        **extra,
     }
+
+
+def _cpu_reference_shapes(ro_c, np, engine, seconds=1.0):
+    """Single-threaded rates of BASELINE configs[0] (one 64 KiB block, 32:32, S = 2 KiB:
+    encode + reconstruct of 16 erased data shreds) and of benches/shredder.rs's slice
+    (/root/reference/benches/shredder.rs:19-61: a maximum 32 767-byte payload -> 32 data
+    shreds of 1 KiB; deshred from the 32 coding shreds only), RS work only."""
+    out = {}
+    rng = np.random.default_rng(5)
+    for name, S, erased in (("config0_64KiB_block", 2048, 16), ("shredder_bench_slice", 1024, 32)):
+        data = rng.integers(0, 256, size=(1, 32, S), dtype=np.uint8)
+        op = np.array([0] * erased + [1] * (32 - erased), np.uint8)
+        rp = np.ones(32, np.uint8)
+        n, te, td = 0, 0.0, 0.0
+        while te + td < seconds:
+            t = time.perf_counter()
+            rec = ro_c.encode_blocks(data, 32, threads=1, engine=engine)
+            te += time.perf_counter() - t
+            cwh = np.concatenate([data, rec], axis=1)
+            t = time.perf_counter()
+            ro_c.decode_blocks(cwh, 32, op, rp, threads=1, engine=engine)
+            td += time.perf_counter() - t
+            n += 1
+        out[name] = {"calls": n, "encode_us": te / n * 1e6, "reconstruct_us": td / n * 1e6,
+                     "encode_plus_reconstruct_GiBps": n * 32 * S / (te + td) / GIB, "threads": 1,
+                     "erased_data_shreds": erased}
+    return out
 
 
 def _cpu_model():

@@ -35,6 +35,10 @@ def lib():
         L.ro_decode_blocks.argtypes = [sz, sz, sz, sz, p, sz, p, p, p, sz, ctypes.c_int]
         L.ro_use_high_rate.argtypes = [sz, sz]
         L.ro_tables.argtypes = [p, p, p, p]
+        L.rb_encode.argtypes = [sz, sz, sz, p, p]
+        L.rb_decode.argtypes = [sz, sz, sz, p, p, p, p, p]
+        L.rb_encode_blocks.argtypes = [sz, sz, sz, sz, p, sz, p, sz, ctypes.c_int]
+        L.rb_decode_blocks.argtypes = [sz, sz, sz, sz, p, sz, p, p, p, sz, ctypes.c_int]
         _lib = L
     return _lib
 
@@ -70,27 +74,33 @@ def decode(orig: np.ndarray, orig_present, rec: np.ndarray, rec_present) -> np.n
     return out
 
 
-def encode_blocks(blocks: np.ndarray, m: int, threads: int = 1) -> np.ndarray:
-    """blocks: (n, k, S) uint8 -> (n, m, S) recovery."""
+def avx2_available() -> bool:
+    return bool(lib().rb_avx2_available())
+
+
+def encode_blocks(blocks: np.ndarray, m: int, threads: int = 1, engine: str = "scalar") -> np.ndarray:
+    """blocks: (n, k, S) uint8 -> (n, m, S) recovery.  engine "avx2": the crate's Avx2
+    engine restated (rs_cpu_avx2.c; S % 64 == 0), "scalar": the log/exp-table oracle."""
     blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
     n, k, S = blocks.shape
     out = np.zeros((n, m, S), dtype=np.uint8)
-    st = lib().ro_encode_blocks(k, m, S, n, _ptr(blocks), k * S, _ptr(out), m * S, threads)
+    f = lib().rb_encode_blocks if engine == "avx2" else lib().ro_encode_blocks
+    st = f(k, m, S, n, _ptr(blocks), k * S, _ptr(out), m * S, threads)
     if st:
         raise RuntimeError(f"ro_encode_blocks status {st}")
     return out
 
 
 def decode_blocks(codewords: np.ndarray, k: int, orig_present, rec_present,
-                  threads: int = 1) -> np.ndarray:
+                  threads: int = 1, engine: str = "scalar") -> np.ndarray:
     """codewords: (n, k+m, S) -> (n, k, S) originals with absent ones restored."""
     codewords = np.ascontiguousarray(codewords, dtype=np.uint8)
     n, km, S = codewords.shape
     out = np.ascontiguousarray(codewords[:, :k, :]).copy()
     op = np.ascontiguousarray(orig_present, dtype=np.uint8)
     rp = np.ascontiguousarray(rec_present, dtype=np.uint8)
-    st = lib().ro_decode_blocks(k, km - k, S, n, _ptr(codewords), km * S, _ptr(op), _ptr(rp),
-                                _ptr(out), k * S, threads)
+    f = lib().rb_decode_blocks if engine == "avx2" else lib().ro_decode_blocks
+    st = f(k, km - k, S, n, _ptr(codewords), km * S, _ptr(op), _ptr(rp), _ptr(out), k * S, threads)
     if st:
         raise RuntimeError(f"ro_decode_blocks status {st}")
     return out

@@ -116,6 +116,16 @@ void ro_tables(uint16_t *exp, uint16_t *log, uint16_t *skew, uint16_t *log_walsh
   if (log_walsh) memcpy(log_walsh, g_log_walsh, sizeof g_log_walsh);
 }
 
+/* read-only table access for the crate-engine baseline (rs_cpu_avx2.c) */
+void ro_internal_tables(const uint16_t **exp, const uint16_t **log, const uint16_t **skew,
+                        const uint16_t **log_walsh) {
+  ensure_tables();
+  *exp = g_exp;
+  *log = g_log;
+  *skew = g_skew;
+  *log_walsh = g_log_walsh;
+}
+
 /* ---- rows of u16 symbols: work[row * nsym + j] ---- */
 static void mul_row(uint16_t *dst, const uint16_t *src, size_t nsym, uint16_t log_m) {
   for (size_t j = 0; j < nsym; ++j) dst[j] = gf_mul(src[j], log_m);

@@ -92,6 +92,37 @@ def test_highrate_encode_is_lagrange_interpolation():
         assert got == want
 
 
+@pytest.mark.parametrize("k,m", [(32, 32), (16, 4), (16, 3), (13, 4), (64, 4), (5, 2), (17, 2), (9, 1), (3, 1),
+                                 (100, 3), (48, 16), (20, 30), (64, 64), (32, 64), (32, 33), (20, 100),
+                                 (64, 33), (17, 128)])
+def test_encoder_is_rs_interpolation(k, m):
+    """Every geometry's encoder, pinned to a closed-form Reed-Solomon definition that does
+    not use the FFT, skew factors, chunk accumulation or truncation rules of the restatement:
+      HighRate (C = next_pow2(m), N = next_pow2(C + k)): recovery j = P(omega_j), P the unique
+        polynomial of degree < N - C with P(omega_{C+i}) = data_i and P(omega_x) = 0 for
+        C + k <= x < N (the zero padding up to a whole power-of-two point set);
+      LowRate (C = next_pow2(k)): recovery i = P(omega_{C+i}), P of degree < C with
+        P(omega_i) = data_i (i < k) and P(omega_x) = 0 for k <= x < C.
+    Together with the 32:32 case above this pins multi-chunk HighRate (16:4), the k < m
+    tails (20:30), 64:64 and the LowRate shredders (CodingOnly 32:64, PETS 32:33)."""
+    rng = np.random.default_rng(k * 1000 + m)
+    data = [int(v) for v in rng.integers(0, 65536, size=k)]
+    rec = o.encode([bytes([v & 0xFF, v >> 8]) for v in data], m)
+    got = [r[0] | (r[1] << 8) for r in rec]
+    if o.use_high_rate(k, m):
+        C = o.next_pow2(m)
+        N = o.next_pow2(C + k)
+        xs = [C + i for i in range(k)] + list(range(C + k, N))
+        ys = data + [0] * (N - C - k)
+        pts = list(range(m))
+    else:
+        C = o.next_pow2(k)
+        xs = list(range(C))
+        ys = data + [0] * (C - k)
+        pts = [C + i for i in range(m)]
+    assert got == [lagrange_eval(xs, ys, x) for x in pts]
+
+
 @pytest.mark.parametrize("size,delta", [(8, 0), (8, 8), (32, 0), (32, 32), (64, 64)])
 def test_ifft_inverts_fft(size, delta):
     rng = np.random.default_rng(size + delta)
@@ -288,3 +319,27 @@ def test_random_erasure_roundtrips(k, m):
         ob = np.frombuffer(b"".join(orig), np.uint8).reshape(k, S) * op[:, None]
         rb = np.frombuffer(b"".join(rec), np.uint8).reshape(m, S)
         assert ro_c.decode(ob.astype(np.uint8), op, rb, rp).tobytes() == b"".join(orig)
+
+
+# ------------------------------------------------- the CPU baseline engine (bench.py)
+
+@pytest.mark.skipif(not ro_c.avx2_available(), reason="host without AVX2")
+@pytest.mark.parametrize("k,m,S", [(32, 32, 1024), (32, 32, 2048), (16, 4, 4096), (64, 64, 128), (32, 64, 1024),
+                                   (32, 33, 192), (20, 30, 128), (100, 3, 64), (3, 1, 64)])
+def test_avx2_engine_matches_scalar_oracle(k, m, S):
+    """oracle/rs_cpu_avx2.c (the crate's Avx2 engine restated: nibble-table multiplies, the
+    FWHT eval_poly locator, every received shard used) gives the scalar oracle's bytes."""
+    rng = np.random.default_rng(k * 7 + m * 3 + S)
+    blocks = rng.integers(0, 256, size=(3, k, S), dtype=np.uint8)
+    rec = ro_c.encode_blocks(blocks, m, engine="avx2")
+    assert np.array_equal(rec, ro_c.encode_blocks(blocks, m))
+    cw = np.concatenate([blocks, rec], axis=1)
+    r = random.Random(S)
+    for _ in range(3):
+        keep = set(r.sample(range(k + m), k + r.randint(0, min(m, 3))))
+        op = np.array([i in keep for i in range(k)], np.uint8)
+        rp = np.array([k + j in keep for j in range(m)], np.uint8)
+        damaged = cw.copy()
+        damaged[:, :k][:, op == 0] = 0
+        got = ro_c.decode_blocks(damaged, k, op, rp, engine="avx2")
+        assert np.array_equal(got, blocks)
