@@ -21,6 +21,7 @@
 #include "gf16.hpp"
 #include "cipher.hpp"
 #include "ed25519.hpp"
+#include "slice.hpp"
 #include "wire.hpp"
 #include "merkle.hpp"
 #include "rs_launch.hpp"
@@ -113,6 +114,7 @@ struct ag_rs_ctx {
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
   DevBuf d_merkle_nodes;                    // Merkle node scratch (callers without a nodes buffer)
   DevBuf d_aon_lens, d_aon_digests, d_aon_keys;  // all-or-nothing transforms
+  DevBuf d_slice_meta;                           // slice framing / parsing metadata
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
   DevBuf d_sh_roots, d_sh_commit, d_sh_onvalid, d_sh_list;  // shred validation scratch
@@ -1713,6 +1715,93 @@ int ag_shred_serialize_batch(ag_rs_ctx* c, size_t n, const ag_shred_columns* col
                  hipSuccess
              ? AG_RS_OK
              : AG_RS_ERR_DEVICE;
+}
+
+int ag_slice_frame_batch(ag_rs_ctx* c, size_t nslices, size_t shred_bytes, const uint8_t* parent_flags,
+                         const uint8_t* parent_ids, const uint8_t* data, size_t data_stride, const uint32_t* data_lens,
+                         uint8_t* codewords, size_t codeword_stride, uint32_t* payload_lens_out) {
+  if (!c) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (nslices == 0) return AG_RS_OK;
+  if (!parent_flags || !parent_ids || !data_lens || !codewords || !payload_lens_out || nslices > 0x7FFFFFFFull ||
+      shred_bytes == 0 || reinterpret_cast<uintptr_t>(codewords) % 4 || codeword_stride % 4 ||
+      (nslices > 1 && codeword_stride < 32 * shred_bytes))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  size_t max_len = 0;
+  for (size_t b = 0; b < nslices; ++b) {
+    if (parent_flags[b] > 1) return AG_RS_ERR_INVALID_ARGUMENT;
+    const size_t framed = 1 + (parent_flags[b] ? AG_SLICE_BLOCK_ID_BYTES : 0) + 8 + size_t{data_lens[b]};
+    if (framed > AG_SLICE_MAX_DATA || framed >= 32 * shred_bytes) return AG_RS_ERR_TOO_MUCH_DATA;
+    max_len = std::max<size_t>(max_len, data_lens[b]);
+  }
+  if (max_len && (!data || (nslices > 1 && data_stride < max_len))) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  // metadata: flags | ids | lens, one upload
+  const size_t off_ids = (nslices + 15) / 16 * 16, off_lens = off_ids + (nslices * AG_SLICE_BLOCK_ID_BYTES + 15) / 16 * 16;
+  const size_t bytes = off_lens + 4 * nslices;
+  int st = c->d_slice_meta.ensure(bytes, c->stream);
+  if (st) return st;
+  std::vector<uint8_t> meta(bytes, 0);
+  std::memcpy(meta.data(), parent_flags, nslices);
+  std::memcpy(meta.data() + off_ids, parent_ids, nslices * AG_SLICE_BLOCK_ID_BYTES);
+  std::memcpy(meta.data() + off_lens, data_lens, 4 * nslices);
+  AG_HIP(hipMemcpyAsync(c->d_slice_meta.ptr, meta.data(), bytes, hipMemcpyHostToDevice, c->stream));
+  ag::SliceFrameParams p{};
+  uint8_t* d = c->d_slice_meta.as<uint8_t>();
+  p.parent_flags = d;
+  p.parent_ids = d + off_ids;
+  p.data_lens = reinterpret_cast<const uint32_t*>(d + off_lens);
+  p.data = data;
+  p.data_stride = data_stride;
+  p.cw = codewords;
+  p.cw_stride = codeword_stride;
+  p.n = nslices;
+  if (ag::launch_slice_frame(p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  AG_HIP(hipStreamSynchronize(c->stream));  // the host metadata buffer goes out of scope
+  for (size_t b = 0; b < nslices; ++b)
+    payload_lens_out[b] = static_cast<uint32_t>(1 + (parent_flags[b] ? AG_SLICE_BLOCK_ID_BYTES : 0) + 8 + data_lens[b]);
+  return AG_RS_OK;
+}
+
+int ag_slice_parse_batch(ag_rs_ctx* c, size_t nslices, const uint8_t* codewords, size_t codeword_stride,
+                         const int64_t* payload_lens, uint8_t* status, uint8_t* parent_flags, uint8_t* parent_ids,
+                         uint32_t* data_offsets, uint32_t* data_lens) {
+  if (!c) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (nslices == 0) return AG_RS_OK;
+  if (!codewords || !payload_lens || !status || !parent_flags || !parent_ids || !data_offsets || !data_lens ||
+      nslices > 0x7FFFFFFFull)
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  for (size_t b = 0; b < nslices; ++b)  // the bytes parsed must lie inside the codeword
+    if (nslices > 1 && payload_lens[b] > 0 && static_cast<uint64_t>(payload_lens[b]) > codeword_stride)
+      return AG_RS_ERR_INVALID_ARGUMENT;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  // device layout: lens (8n) | status (n) | flags (n) | ids (40n) | offsets (4n) | data lens (4n)
+  const size_t o_st = 8 * nslices, o_fl = o_st + nslices, o_id = o_fl + nslices,
+               o_off = (o_id + AG_SLICE_BLOCK_ID_BYTES * nslices + 3) / 4 * 4, o_len = o_off + 4 * nslices;
+  const size_t bytes = o_len + 4 * nslices;
+  int st = c->d_slice_meta.ensure(bytes, c->stream);
+  if (st) return st;
+  uint8_t* d = c->d_slice_meta.as<uint8_t>();
+  AG_HIP(hipMemcpyAsync(d, payload_lens, 8 * nslices, hipMemcpyHostToDevice, c->stream));
+  ag::SliceParseParams p{};
+  p.cw = codewords;
+  p.cw_stride = codeword_stride;
+  p.payload_lens = reinterpret_cast<const int64_t*>(d);
+  p.status = d + o_st;
+  p.parent_flags = d + o_fl;
+  p.parent_ids = d + o_id;
+  p.data_offsets = reinterpret_cast<uint32_t*>(d + o_off);
+  p.data_lens = reinterpret_cast<uint32_t*>(d + o_len);
+  p.n = nslices;
+  if (ag::launch_slice_parse(p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  std::vector<uint8_t> out(bytes - o_st);
+  AG_HIP(hipMemcpyAsync(out.data(), d + o_st, bytes - o_st, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipStreamSynchronize(c->stream));
+  std::memcpy(status, out.data(), nslices);
+  std::memcpy(parent_flags, out.data() + (o_fl - o_st), nslices);
+  std::memcpy(parent_ids, out.data() + (o_id - o_st), AG_SLICE_BLOCK_ID_BYTES * nslices);
+  std::memcpy(data_offsets, out.data() + (o_off - o_st), 4 * nslices);
+  std::memcpy(data_lens, out.data() + (o_len - o_st), 4 * nslices);
+  return AG_RS_OK;
 }
 
 }  // extern "C"

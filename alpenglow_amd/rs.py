@@ -78,6 +78,7 @@ EXPORTS = (
     "ag_aon_decrypt_batch",
     "ag_ed25519_public_key_batch", "ag_ed25519_sign_batch", "ag_ed25519_verify_batch", "ag_shred_validate_batch",
     "ag_slice_sign_batch", "ag_shred_deserialize_batch", "ag_shred_serialize_batch",
+    "ag_slice_frame_batch", "ag_slice_parse_batch",
 )
 
 
@@ -154,6 +155,8 @@ def load():
         "ag_slice_sign_batch": ([p, sz, p, p, p, p, p, p, p, p], i),
         "ag_shred_deserialize_batch": ([p, sz, p, sz, p, p, p], i),
         "ag_shred_serialize_batch": ([p, sz, p, p, sz, p], i),
+        "ag_slice_frame_batch": ([p, sz, sz, p, p, p, sz, p, p, sz, p], i),
+        "ag_slice_parse_batch": ([p, sz, p, sz, p, p, p, p, p, p], i),
     }
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
@@ -624,3 +627,55 @@ def shred_serialize_batch(ctx: Context, n: int, cols: ShredColumns, packets, pac
     """wincode::serialize(&Shred) for n shreds (device columns -> device packets)."""
     _check(load().ag_shred_serialize_batch(ctx.handle, n, ctypes.byref(cols), _ptr(packets), packet_stride,
                                            _ptr(packet_lens)), "ag_shred_serialize_batch")
+
+
+# ---- slice payload framing (types/slice.rs:73-84, :211-218) ----------------------------
+
+SLICE_OK, SLICE_TOO_LARGE, SLICE_BAD_ENCODING, SLICE_NO_PAYLOAD = 0, 1, 2, 3
+BLOCK_ID_BYTES = 40
+
+
+def slice_frame_batch(ctx: Context, nslices: int, shred_bytes: int, parents, data, data_stride: int, data_lens,
+                      codewords, codeword_stride: int):
+    """Slice::payload_bytes for a batch, written into the codewords' data regions.
+
+    parents: one entry per slice, None or (slot, 32-byte block hash); data: device bytes,
+    slice b at data + b * data_stride; returns the framed payload lengths (numpy u32) to
+    pass to ``coder_shred_batch(..., payloads=None, payload_lens=...)``."""
+    import numpy as np
+
+    flags = np.zeros(nslices, np.uint8)
+    ids = np.zeros((nslices, BLOCK_ID_BYTES), np.uint8)
+    for b, par in enumerate(parents):
+        if par is not None:
+            slot, h = par
+            flags[b] = 1
+            ids[b, :8] = np.frombuffer(int(slot).to_bytes(8, "little"), np.uint8)
+            ids[b, 8:] = np.frombuffer(bytes(h), np.uint8)
+    lens = np.ascontiguousarray(np.asarray(data_lens, dtype=np.uint32))
+    out = np.zeros(nslices, np.uint32)
+    if len(parents) != nslices or lens.size != nslices:
+        raise ValueError("parents / data_lens do not match the batch")
+    _check(load().ag_slice_frame_batch(ctx.handle, nslices, shred_bytes, flags.ctypes.data, ids.ctypes.data,
+                                       _ptr(data) if data is not None else None, data_stride, lens.ctypes.data,
+                                       _ptr(codewords), codeword_stride, out.ctypes.data), "ag_slice_frame_batch")
+    return out
+
+
+def slice_parse_batch(ctx: Context, nslices: int, codewords, codeword_stride: int, payload_lens):
+    """SlicePayload::try_from over the payloads deshred left in the codewords.  Returns
+    (status, parents, data_offsets, data_lens): parents[b] None or (slot, hash bytes)."""
+    import numpy as np
+
+    lens = np.ascontiguousarray(np.asarray(payload_lens, dtype=np.int64))
+    st = np.zeros(nslices, np.uint8)
+    flags = np.zeros(nslices, np.uint8)
+    ids = np.zeros((nslices, BLOCK_ID_BYTES), np.uint8)
+    offs = np.zeros(nslices, np.uint32)
+    dl = np.zeros(nslices, np.uint32)
+    _check(load().ag_slice_parse_batch(ctx.handle, nslices, _ptr(codewords), codeword_stride, lens.ctypes.data,
+                                       st.ctypes.data, flags.ctypes.data, ids.ctypes.data, offs.ctypes.data,
+                                       dl.ctypes.data), "ag_slice_parse_batch")
+    parents = [(int.from_bytes(ids[b, :8].tobytes(), "little"), ids[b, 8:].tobytes()) if flags[b] else None
+               for b in range(nslices)]
+    return st, parents, offs, dl

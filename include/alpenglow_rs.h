@@ -223,6 +223,42 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* ctx, size_t num_coding, size_t nslices,
                               const uint8_t* data_present, const uint8_t* coding_present,
                               int mode, int64_t* payload_len_out);
 
+/* ---- 4b. slice payload framing ---------------------------------------------------------
+ * Slice::payload_bytes (types/slice.rs:73-84) and SlicePayload::try_from (slice.rs:211-218)
+ * on the batched coder's codeword buffers (device), the data region of codeword b being
+ * its 32 data shards.  Metadata arrays are HOST memory; synchronous.
+ * Framing: wincode(parent: Option<BlockId>) || u64 LE data length || data, BlockId = (Slot
+ * u64, BlockHash [u8; 32]) = 40 bytes (lib.rs:65).  The framed payload then goes through
+ * ag_rs_coder_shred_batch with payloads = NULL (padded and encoded in place). */
+#define AG_SLICE_MAX_DATA 32767      /* MAX_DATA_PER_SLICE (shredder.rs:54) */
+#define AG_SLICE_BLOCK_ID_BYTES 40
+enum {
+  AG_SLICE_OK = 0,
+  AG_SLICE_TOO_LARGE = 1,    /* SlicePayloadError::TooLarge (slice.rs:195) */
+  AG_SLICE_BAD_ENCODING = 2, /* SlicePayloadError::BadEncoding (slice.rs:198) */
+  AG_SLICE_NO_PAYLOAD = 3    /* the slice's deshred failed (payload_len < 0) */
+};
+
+/* frame_batch: parent_flags [nslices] (0 None / 1 Some), parent_ids [nslices][40] (slot LE,
+ * then the block hash), data_lens [nslices]: HOST.  data: device, slice b at data +
+ * b * data_stride.  codewords: device, 4-byte aligned, codeword_stride % 4 == 0.
+ * payload_lens_out (HOST, nslices): framed length = ag_rs_coder_shred_batch's payload_lens.
+ * shred_bytes: the coder batch's shred size; every framed payload must be <=
+ * AG_SLICE_MAX_DATA and < 32 * shred_bytes (ReedSolomonCoder::shred's TooMuchData,
+ * reed_solomon.rs:89-91), else AG_RS_ERR_TOO_MUCH_DATA with nothing written. */
+int ag_slice_frame_batch(ag_rs_ctx* ctx, size_t nslices, size_t shred_bytes, const uint8_t* parent_flags,
+                         const uint8_t* parent_ids, const uint8_t* data, size_t data_stride,
+                         const uint32_t* data_lens, uint8_t* codewords, size_t codeword_stride,
+                         uint32_t* payload_lens_out);
+
+/* parse_batch: SlicePayload::try_from on the first payload_lens[b] bytes of codeword b
+ * (payload_lens HOST, as ag_rs_coder_deshred_batch returns them; < 0 = failed slice).
+ * Outputs HOST: status AG_SLICE_*, parent_flags, parent_ids [nslices][40], and the data
+ * (left in place) as codeword + data_offsets[b], data_lens[b] bytes. */
+int ag_slice_parse_batch(ag_rs_ctx* ctx, size_t nslices, const uint8_t* codewords, size_t codeword_stride,
+                         const int64_t* payload_lens, uint8_t* status, uint8_t* parent_flags,
+                         uint8_t* parent_ids, uint32_t* data_offsets, uint32_t* data_lens);
+
 /* ---- 5. slice Merkle trees -----------------------------------------------------------
  * The SHA-256 Merkle tree the shredder builds over each slice's 64 shreds (data shreds,
  * then coding shreds; shredder.rs:628-632) -- crypto/merkle.rs MerkleTree:
