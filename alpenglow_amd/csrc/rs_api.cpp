@@ -348,8 +348,10 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   const size_t xw = hr == 1 ? next_pow2(xchunk + k) : 0;
   const size_t cps = S / 64;
   // decode_x: HighRate, W in {32, 64}; one pattern per tile (single pattern, or tiles
-  // that never straddle blocks)
-  const bool x_geo = hr == 1 && S % 64 == 0 && (xw == 32 || xw == 64) && aligned && (npat == 1 || cps % 64 == 0);
+  // that never straddle blocks), else per-lane patterns (each lane one chunk of one block:
+  // the follower's per-slice patterns on 1 KiB shreds)
+  const bool x_geo = hr == 1 && S % 64 == 0 && (xw == 32 || xw == 64) && aligned;
+  const bool x_per_lane = npat > 1 && cps % 64 != 0;
   // decode_syn: the encode_mc geometries (chunk <= 4), any k survivors, same tiling rule
   const unsigned syn_chunk = mode == AG_RS_DECODE_ANY_K && aligned && (npat == 1 || cps % 64 == 0)
                                  ? mc_chunk(k, m, S) : 0;
@@ -520,9 +522,20 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     for (size_t p = 0; p < npat; ++p) {
       if (cls[p] != 3) continue;
       uint64_t e = 0, in = 0, out = 0;
+      // ANY_K: exactly k survivors -- the present originals, then recovery shards in index
+      // order; surplus recovery shards count as erased (MDS: any k survivors determine the
+      // originals), so only k input multiplies remain.  EXACT: every present shard, as
+      // the crate's decoder
+      size_t budget = k;
+      for (size_t i = 0; i < k; ++i) budget -= opres[p * k + i] ? 1 : 0;
       for (size_t j = 0; j < xchunk; ++j) {
-        if (j < m && rpres[p * m + j]) in |= uint64_t{1} << j;
-        else e |= uint64_t{1} << j;  // lost recovery or virtual point m..chunk-1
+        const bool use = j < m && rpres[p * m + j] && (mode != AG_RS_DECODE_ANY_K || budget > 0);
+        if (use) {
+          in |= uint64_t{1} << j;
+          if (budget) --budget;
+        } else {
+          e |= uint64_t{1} << j;  // lost / surplus recovery or virtual point m..chunk-1
+        }
       }
       for (size_t i = 0; i < k; ++i) {
         const uint64_t bit = uint64_t{1} << (xchunk + i);
@@ -560,6 +573,9 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     p.total_columns = static_cast<uint64_t>(nblocks) * cps;
     uint64_t ntiles;
     if (npat == 1) {
+      ntiles = (p.total_columns + 63) / 64;
+    } else if (x_per_lane) {
+      p.per_lane = 1;  // lanes of blocks outside class 3 find all-zero masks: no loads, no stores
       ntiles = (p.total_columns + 63) / 64;
     } else {
       p.per_block = 1;

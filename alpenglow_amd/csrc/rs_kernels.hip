@@ -1063,36 +1063,87 @@ __device__ __forceinline__ void xf_derivative(int wave, int lane, uint4* lds, Re
   });
 }
 
-template <int NW>
+// x <- M x for a runtime matrix that differs per lane (per-lane erasure patterns): rows
+// are this lane's 16 row words; every term is one v_bitop3 with a v_bfe_i32 mask.
+__device__ __forceinline__ void mul_rt_lane(uint32_t* x, const uint32_t* __restrict__ rows) {
+  uint32_t r[16];
+  static_for<4>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    const uint4 v = reinterpret_cast<const uint4*>(rows)[q];
+    r[4 * q] = v.x;
+    r[4 * q + 1] = v.y;
+    r[4 * q + 2] = v.z;
+    r[4 * q + 3] = v.w;
+  });
+  uint32_t y[16];
+  static_for<16>([&](auto O) {
+    constexpr int o = decltype(O)::value;
+    uint32_t acc = 0;
+    static_for<16>([&](auto I) {
+      constexpr int i = decltype(I)::value;
+      const uint32_t msk = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(r[o]), i, 1));
+      acc = __builtin_amdgcn_bitop3_b32(acc, x[i], msk, 0x78);  // acc ^ (x & msk)
+    });
+    y[o] = acc;
+  });
+  static_for<16>([&](auto O) { x[decltype(O)::value] = y[decltype(O)::value]; });
+}
+
+// PL: per-lane patterns (tiles straddle blocks: shard sizes below 4 KiB, e.g. the 1 KiB
+// shreds of the reference's slices).  Every lane then owns one whole 64-byte chunk of one
+// block (four 16-byte loads of its own chunk, no lane exchange), reads its block's pattern
+// masks and matrices, and multiplies with mul_rt_lane; the transform itself is unchanged
+// (its skew constants never depend on the pattern).
+template <int NW, bool PL = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(const DecodeXParams p) {
   constexpr int W = 8 * NW;
   __shared__ uint4 lds[4 * NW * 4 * kXfLanes];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  // tile -> (pattern, address tile)
   const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
-  uint64_t vtile = tile, pat = 0;
-  if (p.per_block) {
-    const uint64_t bi = tile / p.tiles_per_block;
-    const uint64_t blk = p.block_ids ? p.block_ids[bi] : bi;
-    vtile = blk * p.tiles_per_block + (tile - bi * p.tiles_per_block);
-    pat = blk;
+  uint64_t in_mask, out_mask;
+  const uint32_t* rows;
+  TileIO io_r, io_o;
+  uint64_t off_r = 0, off_o = 0;
+  if constexpr (PL) {
+    const uint64_t gc = static_cast<uint64_t>(tile) * kXfLanes + lane;
+    const bool ok = gc < p.total_columns;
+    const uint64_t blk = ok ? gc / p.chunks_per_shard : 0;
+    const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
+    in_mask = ok ? p.pmask[2 * blk] : 0;
+    out_mask = ok ? p.pmask[2 * blk + 1] : 0;
+    rows = p.rows + blk * (W * 16);
+    off_r = blk * p.rec_block_stride + col * 64;
+    off_o = blk * p.orig_block_stride + col * 64;
+  } else {
+    // tile -> (pattern, address tile)
+    uint64_t vtile = tile, pat = 0;
+    if (p.per_block) {
+      const uint64_t bi = tile / p.tiles_per_block;
+      const uint64_t blk = p.block_ids ? p.block_ids[bi] : bi;
+      vtile = blk * p.tiles_per_block + (tile - bi * p.tiles_per_block);
+      pat = blk;
+    }
+    in_mask = p.pmask[2 * pat];
+    out_mask = p.pmask[2 * pat + 1];
+    rows = p.rows + pat * (W * 16);
+    io_r = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.rec_block_stride);
+    io_o = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.orig_block_stride);
   }
-  const uint64_t in_mask = p.pmask[2 * pat], out_mask = p.pmask[2 * pat + 1];
-  const uint32_t* rows = p.rows + pat * (W * 16);
-  const TileIO io_r = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.rec_block_stride);
-  const TileIO io_o = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.orig_block_stride);
 
   Regs8 ra;
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = 8 * wave + t;  // wave-uniform
-    if ((in_mask >> j) & 1) {
+    if ((in_mask >> j) & 1) {          // PL: per lane
       const bool is_rec = j < p.chunk;
       const uint8_t* base = is_rec ? p.rec + j * p.rec_shard_stride : p.orig + (j - p.chunk) * p.orig_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(base + (is_rec ? io_r.off[q] : io_o.off[q]));
+        const uint8_t* src;
+        if constexpr (PL) src = base + (is_rec ? off_r : off_o) + 16 * q;
+        else src = base + (is_rec ? io_r.off[q] : io_o.off[q]);
+        const uint4 x = *reinterpret_cast<const uint4*>(src);
         ra[t][4 * q] = x.x;
         ra[t][4 * q + 1] = x.y;
         ra[t][4 * q + 2] = x.z;
@@ -1106,10 +1157,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     constexpr int t = decltype(T)::value;
     const uint32_t j = 8 * wave + t;
     if ((in_mask >> j) & 1) {
-      swap_halves(ra[t]);
+      if constexpr (!PL) swap_halves(ra[t]);
       dev::planes_from_raw(ra[t]);
 #if !(AG_DX_DIAG & 1)
-      mul_rt_dx(ra[t], rows + j * 16);
+      if constexpr (PL) mul_rt_lane(ra[t], rows + j * 16); else mul_rt_dx(ra[t], rows + j * 16);
 #endif
     }
   });
@@ -1122,16 +1173,29 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
 #endif
   xf_pass_b_fft<NW, 0>(rb);
   xf_exchange_bc<NW>(wave, lane, lds, rb, ra);
-  if (((out_mask >> (8 * wave)) & 0xFF) == 0) return;  // nothing to restore in this wave
+  const uint32_t mine = static_cast<uint32_t>(out_mask >> (8 * wave)) & 0xFF;
+  if constexpr (PL) {
+    if (__builtin_amdgcn_ballot_w64(mine != 0) == 0) return;  // nothing to restore in this wave
+  } else {
+    if (mine == 0) return;
+  }
   xf_pass_c<NW, 0>(wave, ra);
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = 8 * wave + t;
     if ((out_mask >> j) & 1) {
+      uint8_t* dst = p.orig + (j - p.chunk) * p.orig_shard_stride;
+      if constexpr (PL) {
 #if !(AG_DX_DIAG & 2)
-      mul_rt_dx(ra[t], rows + j * 16);
+        mul_rt_lane(ra[t], rows + j * 16);
 #endif
-      store_shard(p.orig + (j - p.chunk) * p.orig_shard_stride, io_o, io_o.valid, ra[t]);
+        dev::store_chunk(dst + off_o, ra[t]);
+      } else {
+#if !(AG_DX_DIAG & 2)
+        mul_rt_dx(ra[t], rows + j * 16);
+#endif
+        store_shard(dst, io_o, io_o.valid, ra[t]);
+      }
     }
   });
 }
@@ -1802,9 +1866,16 @@ hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, 
   if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
   if (p.k + p.chunk > W || p.m > p.chunk) return hipErrorInvalidValue;
   const dim3 grid(static_cast<unsigned>(ntiles));
+  const bool pl = p.per_lane != 0;
   switch (W) {
-    case 32: hipLaunchKernelGGL((decode_x_kernel<4>), grid, dim3(256), 0, stream, p); break;
-    case 64: hipLaunchKernelGGL((decode_x_kernel<8>), grid, dim3(512), 0, stream, p); break;
+    case 32:
+      if (pl) hipLaunchKernelGGL((decode_x_kernel<4, true>), grid, dim3(256), 0, stream, p);
+      else hipLaunchKernelGGL((decode_x_kernel<4>), grid, dim3(256), 0, stream, p);
+      break;
+    case 64:
+      if (pl) hipLaunchKernelGGL((decode_x_kernel<8, true>), grid, dim3(512), 0, stream, p);
+      else hipLaunchKernelGGL((decode_x_kernel<8>), grid, dim3(512), 0, stream, p);
+      break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

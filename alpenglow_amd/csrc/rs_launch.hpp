@@ -92,6 +92,7 @@ struct DecodeXParams {
   const uint32_t* block_ids;  // per_block: blocks processed (null = 0..)
   uint32_t per_block;         // 1: pattern = block, tiles_per_block tiles per block
   uint32_t tiles_per_block;   // chunks_per_shard / 64 (per_block mode)
+  uint32_t per_lane;          // 1: pattern = block of each lane's chunk (tiles straddle blocks)
   uint32_t k, m, chunk;
   uint32_t chunks_per_shard;
   uint64_t total_columns;  // batch blocks * chunks_per_shard

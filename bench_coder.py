@@ -33,6 +33,10 @@ def main():
     ap.add_argument("--coding-only", action="store_true",
                     help="CodingOnlyShredder shape: 32:64, deshred from coding shreds 32..63 (the "
                          "reference bench drops the first 32 output shreds)")
+    ap.add_argument("--random-patterns", action="store_true",
+                    help="the follower's real deshred: per slice, the first 32 of its 64 shreds to arrive "
+                         "in a seeded random order (slot_block_data.rs:331-370 deshreds at the 32nd), so data "
+                         "and coding shreds are lost in arbitrary per-slice patterns")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     import numpy as np
@@ -54,6 +58,15 @@ def main():
     dpres, cpres = np.zeros(32 * n, np.uint8), np.ones(m * n, np.uint8)
     if args.coding_only:  # output shreds are the 64 coding shreds; the first 32 are dropped
         cpres = np.tile(np.array([0] * 32 + [1] * 32, np.uint8), n)
+    if args.random_patterns:
+        if args.coding_only:
+            raise SystemExit("--random-patterns is for the RegularShredder shape")
+        rng = np.random.default_rng(0xA221)
+        arrived = np.argsort(rng.random((n, 64)), axis=1)[:, :32]  # first 32 arrivals per slice
+        present = np.zeros((n, 64), np.uint8)
+        np.put_along_axis(present, arrived, 1, axis=1)
+        dpres = np.ascontiguousarray(present[:, :32]).reshape(-1)
+        cpres = np.ascontiguousarray(present[:, 32:]).reshape(-1)
     mode = rs.DECODE_EXACT if args.exact else rs.DECODE_ANY_K
 
     def shred():
@@ -80,6 +93,15 @@ def main():
         t_de += c - b
     wall = time.perf_counter() - t0
     ok = bool((res == L).all())
+    if args.random_patterns:
+        # zero every absent shred, deshred once more, compare with the original codewords
+        want = cw.clone()
+        pres = torch.from_numpy(np.concatenate([dpres.reshape(n, 32), cpres.reshape(n, m)], axis=1)).to(dev)
+        view = cw.view(n, 32 + m, S)
+        view.mul_(pres.unsqueeze(-1))
+        res2 = deshred()
+        ok = ok and bool((res2 == L).all()) and bool(torch.equal(cw, want))
+        del want
     # spot check vs the oracle's ReedSolomonCoder (checker only)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import rs_oracle as o
@@ -90,7 +112,9 @@ def main():
         spot &= host[i, :32 * S].tobytes() == b"".join(raw.data)
         spot &= host[i, 32 * S:].tobytes() == b"".join(raw.coding)
     line = {
-        "metric": "slices/s ReedSolomonCoder shred + deshred (first 32 output shreds lost), max slices",
+        "metric": ("slices/s ReedSolomonCoder shred + deshred (random 32 of 64 shreds per slice), max slices"
+                   if args.random_patterns else
+                   "slices/s ReedSolomonCoder shred + deshred (first 32 output shreds lost), max slices"),
         "value": n * args.steps / wall,
         "unit": "slices/s",
         "n_gpus": 1,
@@ -104,13 +128,14 @@ def main():
         "data": "synthetic (splitmix64 payloads, device-generated)",
         "config": {"workload": f"{n} slices x {L} B payload, 32:{m} shreds of {S} B, deshred from "
                                + ("coding shreds 32..63 (CodingOnlyShredder)" if args.coding_only else
-                                  "the 32 coding shreds (RegularShredder)"),
+                                  "a random 32 of the 64 shreds per slice (RegularShredder)" if args.random_patterns
+                                  else "the 32 coding shreds (RegularShredder)"),
                    "mode": "EXACT" if args.exact else "ANY_K"},
         "payload_GiBps": n * L * args.steps / wall / GIB,
         "calls_ms": {"shred_batch": t_sh * 1e3 / args.steps, "deshred_batch": t_de * 1e3 / args.steps},
         "verify": {"all_slices_restored": ok, "shreds_match_oracle": bool(spot)},
     }
-    if not args.no_cpu_baseline and not args.coding_only:
+    if not args.no_cpu_baseline and not args.coding_only and not args.random_patterns:
         import ro_c
         threads = max(1, min(16, len(os.sched_getaffinity(0))))
         ns = min(n, 2048)

@@ -736,3 +736,31 @@ def test_fast_decode_low_half_pruned(ctx, dev):
         d1[:, [0, 15]] = 0
         got = gpu_decode(ctx, dev, d1, rec, [0] + [1] * 14 + [0] + [1] * 16, [1] * m, rs.DECODE_ANY_K)
         assert np.array_equal(got, blocks), S
+
+
+@pytest.mark.parametrize("S,n", [(1024, 40), (96, 30), (192, 25), (64, 70), (2048, 9)])
+@pytest.mark.parametrize("mode", [rs.DECODE_ANY_K, rs.DECODE_EXACT])
+def test_decode_per_slice_random_patterns(ctx, dev, S, n, mode):
+    """The follower's deshred shape (slot_block_data.rs:331-370): 32:32, every slice loses
+    an arbitrary set of data AND coding shreds (here: keeps a random 32..40 of 64).  With
+    S < 4 KiB the tiles straddle slices: the per-lane-pattern general decoder.  Compared
+    with the original data; ANY_K uses exactly 32 survivors, EXACT all present shards."""
+    rng = random.Random(S * 31 + n + mode)
+    k = m = 32
+    blocks = np.stack([np.frombuffer(o.block_bytes(900 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    d_o, d_r, op, rp = blocks.copy(), rec.copy(), [], []
+    for b in range(n):
+        keep = set(rng.sample(range(64), rng.randint(32, 40)))
+        if b % 7 == 0:
+            keep = set(range(32, 64))  # all coding present: the transform path, mixed in
+        op += [1 if i in keep else 0 for i in range(k)]
+        rp += [1 if 32 + j in keep else 0 for j in range(m)]
+        for i in range(k):
+            if i not in keep:
+                d_o[b, i] = 0x77
+        for j in range(m):
+            if 32 + j not in keep:
+                d_r[b, j] = 0x99
+    got = gpu_decode(ctx, dev, d_o, d_r, op, rp, mode)
+    assert np.array_equal(got, blocks)
