@@ -323,6 +323,28 @@ int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
   return AG_RS_OK;
 }
 
+// Host flag arrays (0 / nonzero bytes, one per shard) -> bit masks, 8 flags per step:
+// the per-pattern bookkeeping of a 65 536-slice batch stays well under a millisecond.
+inline uint64_t pack_flags(const uint8_t* f, size_t n) {  // n <= 64
+  uint64_t bits = 0;
+  size_t i = 0;
+  for (; i + 8 <= n; i += 8) {
+    uint64_t x;
+    std::memcpy(&x, f + i, 8);
+    // high bit of each byte <- byte != 0, then gather the 8 high bits (multiply trick)
+    const uint64_t nz = ((((x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | x) & 0x8080808080808080ull) >> 7;
+    bits |= ((nz * 0x0102040810204080ull) >> 56) << i;
+  }
+  for (; i < n; ++i) bits |= uint64_t{f[i] != 0} << i;
+  return bits;
+}
+inline size_t count_flags(const uint8_t* f, size_t n) {
+  if (n <= 64) return static_cast<size_t>(__builtin_popcountll(pack_flags(f, n)));
+  size_t c = 0;
+  for (size_t i = 0; i < n; ++i) c += f[i] != 0;
+  return c;
+}
+
 int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
                   const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
                   int mode) {
@@ -370,9 +392,7 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   bool any_lr = false;
   bool any_fast = false, any_generic = false, any_x = false, any_syn = false;
   for (size_t p = 0; p < npat; ++p) {
-    size_t no = 0, nr = 0;
-    for (size_t i = 0; i < k; ++i) no += opres[p * k + i] != 0;
-    for (size_t i = 0; i < m; ++i) nr += rpres[p * m + i] != 0;
+    const size_t no = count_flags(opres + p * k, k), nr = count_flags(rpres + p * m, m);
     if (no + nr < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;  // nothing launched yet
     if (no == k) {
       cls[p] = 0;
@@ -407,10 +427,9 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   if (any_fast) {
     // store mask word per pattern: restore original i iff the pattern is fast and i is absent
     std::vector<uint64_t> mask(npat, 0);
+    const uint64_t kmask = k >= 64 ? ~uint64_t{0} : (uint64_t{1} << k) - 1;  // npts <= 64: k <= 64
     for (size_t p = 0; p < npat; ++p)
-      if (cls[p] == 1)
-        for (size_t i = 0; i < k; ++i)
-          if (!opres[p * k + i]) mask[p] |= uint64_t{1} << i;
+      if (cls[p] == 1) mask[p] = ~pack_flags(opres + p * k, k) & kmask;
     // upload only when the pattern set changed (steady-state batches reuse it, no sync)
     if (mask != c->mask_host) {
       AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read mask_host
@@ -521,26 +540,21 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     std::vector<uint64_t> xm(3 * npat, 0);
     for (size_t p = 0; p < npat; ++p) {
       if (cls[p] != 3) continue;
-      uint64_t e = 0, in = 0, out = 0;
+      // window positions: recovery j < xchunk, original i at xchunk + i (xchunk + k <= 64)
+      const uint64_t ob = pack_flags(opres + p * k, k), kmask = (uint64_t{1} << k) - 1;
+      uint64_t rb = pack_flags(rpres + p * m, m);
       // ANY_K: exactly k survivors -- the present originals, then recovery shards in index
       // order; surplus recovery shards count as erased (MDS: any k survivors determine the
       // originals), so only k input multiplies remain.  EXACT: every present shard, as
       // the crate's decoder
-      size_t budget = k;
-      for (size_t i = 0; i < k; ++i) budget -= opres[p * k + i] ? 1 : 0;
-      for (size_t j = 0; j < xchunk; ++j) {
-        const bool use = j < m && rpres[p * m + j] && (mode != AG_RS_DECODE_ANY_K || budget > 0);
-        if (use) {
-          in |= uint64_t{1} << j;
-          if (budget) --budget;
-        } else {
-          e |= uint64_t{1} << j;  // lost / surplus recovery or virtual point m..chunk-1
-        }
+      if (mode == AG_RS_DECODE_ANY_K) {
+        const size_t budget = k - static_cast<size_t>(__builtin_popcountll(ob));
+        while (static_cast<size_t>(__builtin_popcountll(rb)) > budget) rb &= ~(uint64_t{1} << (63 - __builtin_clzll(rb)));
       }
-      for (size_t i = 0; i < k; ++i) {
-        const uint64_t bit = uint64_t{1} << (xchunk + i);
-        if (opres[p * k + i]) in |= bit; else { e |= bit; out |= bit; }
-      }
+      const uint64_t cmask = (uint64_t{1} << xchunk) - 1;  // xchunk <= 32
+      const uint64_t in = rb | (ob << xchunk);
+      const uint64_t out = (~ob & kmask) << xchunk;
+      const uint64_t e = (~rb & cmask) | out;  // lost / surplus recovery, virtual points m..chunk-1
       xm[p] = e;
       xm[npat + 2 * p] = in;
       xm[npat + 2 * p + 1] = out;
@@ -1445,9 +1459,7 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   std::vector<uint8_t> op(dpres, dpres + n * kDataShreds);
   std::vector<uint8_t> ok(n, 1);
   for (size_t b = 0; b < n; ++b) {
-    size_t cnt = 0;
-    for (size_t i = 0; i < kDataShreds; ++i) cnt += dpres[b * kDataShreds + i] != 0;
-    for (size_t j = 0; j < m; ++j) cnt += cpres[b * m + j] != 0;
+    const size_t cnt = count_flags(dpres + b * kDataShreds, kDataShreds) + count_flags(cpres + b * m, m);
     if (cnt < kDataShreds) {
       ok[b] = 0;
       out[b] = -AG_RS_ERR_NOT_ENOUGH_SHARDS;
