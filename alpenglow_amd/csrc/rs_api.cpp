@@ -115,6 +115,7 @@ struct ag_rs_ctx {
   DevBuf d_merkle_nodes;                    // Merkle node scratch (callers without a nodes buffer)
   DevBuf d_aon_lens, d_aon_digests, d_aon_keys;  // all-or-nothing transforms
   DevBuf d_slice_meta;                           // slice framing / parsing metadata
+  DevBuf stage_pad, stage_mask;                  // restrided shards (sizes not whole 64-byte chunks)
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
   DevBuf d_sh_roots, d_sh_commit, d_sh_onvalid, d_sh_list;  // shred validation scratch
@@ -195,7 +196,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
                       &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -209,6 +210,9 @@ constexpr size_t kStageGroupBytes = size_t{64} << 20;
 
 // Scratch budget of the generic kernels (per launch).
 constexpr size_t kGenericScratchBytes = size_t{512} << 20;
+
+// Restrided shard buffer (shard sizes that are not whole 64-byte chunks), per group.
+constexpr size_t kRestrideGroupBytes = size_t{256} << 20;
 
 // Syndrome-decoder pattern (decode_syn_kernel): restore the erased originals from the
 // first e present recovery shards.  Returns false if the e x e system is singular (cannot
@@ -258,8 +262,45 @@ bool build_syn_pattern(size_t k, size_t m, const uint8_t* opres, const uint8_t* 
 }
 
 int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
+                  size_t ostride, uint8_t* rec, size_t rstride);
+
+// Shard sizes that are not whole 64-byte chunks (a slice's tail, reed_solomon.rs:94-95), or
+// unaligned buffers: restride groups of blocks into padded shards (restride_kernel), run
+// the bitsliced kernels there, restride the outputs back.  Taken when the padded geometry
+// has a bitsliced path.
+size_t padded_shard(size_t S) { return (S + 63) / 64 * 64; }
+bool restride_wanted(size_t S, const void* a, const void* b, size_t sa, size_t sb) {
+  return S % 64 != 0 || !aligned16(a) || !aligned16(b) || sa % 16 != 0 || sb % 16 != 0;
+}
+
+int encode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
+                     size_t ostride, uint8_t* rec, size_t rstride) {
+  const size_t Sp = padded_shard(S), per_block = (k + m) * Sp;
+  const size_t group = std::max<size_t>(1, kRestrideGroupBytes / per_block);
+  int st = c->stage_pad.ensure(std::min(group, nblocks) * per_block, c->stream);
+  if (st) return st;
+  uint8_t* pad = c->stage_pad.as<uint8_t>();
+  for (size_t b0 = 0; b0 < nblocks; b0 += group) {
+    const size_t nb = std::min(group, nblocks - b0);
+    if (ag::launch_restride(orig + b0 * ostride, ostride, S, pad, per_block, Sp, static_cast<uint32_t>(S),
+                            static_cast<uint32_t>(k), nb, false, nullptr, false, c->stream) != hipSuccess)
+      return AG_RS_ERR_DEVICE;
+    if ((st = encode_device(c, k, m, Sp, nb, pad, per_block, pad + k * Sp, per_block))) return st;
+    if (ag::launch_restride(pad + k * Sp, per_block, Sp, rec + b0 * rstride, rstride, S, static_cast<uint32_t>(S),
+                            static_cast<uint32_t>(m), nb, true, nullptr, false, c->stream) != hipSuccess)
+      return AG_RS_ERR_DEVICE;
+  }
+  return AG_RS_OK;
+}
+
+int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
                   size_t ostride, uint8_t* rec, size_t rstride) {
   if (nblocks == 0) return AG_RS_OK;
+  if (restride_wanted(S, orig, rec, ostride, rstride)) {
+    const size_t Sp = padded_shard(S);
+    if (xform_points(k, m, Sp) || mc_chunk(k, m, Sp) || lowrate_chunk(k, m, Sp))
+      return encode_restrided(c, k, m, S, nblocks, orig, ostride, rec, rstride);
+  }
   const unsigned npts = xform_points(k, m, S);
   const unsigned mc = mc_chunk(k, m, S);
   const unsigned lr = lowrate_chunk(k, m, S);
@@ -347,8 +388,58 @@ inline size_t count_flags(const uint8_t* f, size_t n) {
 
 int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
                   const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
+                  int mode);
+
+// The decode counterpart of encode_restrided: originals and recovery shards of a group of
+// blocks go to one padded buffer, the bitsliced decoders run there, and only the restored
+// originals are restrided back (a store mask per pattern).
+int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
+                     const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
+                     int mode) {
+  const size_t Sp = padded_shard(S), per_block = (k + m) * Sp;
+  for (size_t p = 0; p < npat; ++p)  // NotEnoughShards before anything is launched
+    if (count_flags(opres + p * k, k) + count_flags(rpres + p * m, m) < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
+  // store masks: the absent originals of each pattern (k <= 64 on every bitsliced path)
+  std::vector<uint64_t> mask(npat);
+  const uint64_t kmask = k >= 64 ? ~uint64_t{0} : (uint64_t{1} << k) - 1;
+  for (size_t p = 0; p < npat; ++p) mask[p] = ~pack_flags(opres + p * k, k) & kmask;
+  int st = c->stage_mask.ensure(npat * 8, c->stream);
+  if (st) return st;
+  AG_HIP(hipMemcpyAsync(c->stage_mask.ptr, mask.data(), npat * 8, hipMemcpyHostToDevice, c->stream));
+  const size_t group = std::max<size_t>(1, kRestrideGroupBytes / per_block);
+  if ((st = c->stage_pad.ensure(std::min(group, nblocks) * per_block, c->stream))) return st;
+  uint8_t* pad = c->stage_pad.as<uint8_t>();
+  for (size_t b0 = 0; b0 < nblocks; b0 += group) {
+    const size_t nb = std::min(group, nblocks - b0);
+    const size_t p0 = npat > 1 ? b0 : 0, np = npat > 1 ? nb : 1;
+    if (ag::launch_restride(orig + b0 * ostride, ostride, S, pad, per_block, Sp, static_cast<uint32_t>(S),
+                            static_cast<uint32_t>(k), nb, false, nullptr, false, c->stream) != hipSuccess ||
+        ag::launch_restride(rec + b0 * rstride, rstride, S, pad + k * Sp, per_block, Sp, static_cast<uint32_t>(S),
+                            static_cast<uint32_t>(m), nb, false, nullptr, false, c->stream) != hipSuccess)
+      return AG_RS_ERR_DEVICE;
+    if ((st = decode_device(c, k, m, Sp, nb, pad, per_block, pad + k * Sp, per_block, opres + p0 * k, rpres + p0 * m,
+                            np, mode)))
+      return st;
+    if (ag::launch_restride(pad, per_block, Sp, orig + b0 * ostride, ostride, S, static_cast<uint32_t>(S),
+                            static_cast<uint32_t>(k), nb, true, c->stage_mask.as<uint64_t>() + p0, npat > 1,
+                            c->stream) != hipSuccess)
+      return AG_RS_ERR_DEVICE;
+  }
+  AG_HIP(hipStreamSynchronize(c->stream));  // the host mask vector goes out of scope
+  return AG_RS_OK;
+}
+
+int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
+                  const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
                   int mode) {
   if (nblocks == 0) return AG_RS_OK;
+  if (k <= 64 && restride_wanted(S, orig, rec, ostride, rstride)) {
+    const size_t Sp = padded_shard(S);
+    const int hr = ag::use_high_rate(k, m);
+    const size_t xw = hr == 1 ? next_pow2(next_pow2(m) + k) : 0;
+    if (xform_points(k, m, Sp) || mc_chunk(k, m, Sp) || lowrate_chunk(k, m, Sp) || xw == 32 || xw == 64)
+      return decode_restrided(c, k, m, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
+  }
   const int hr = ag::use_high_rate(k, m);
   // one erasure pattern repeated for every block (a repair batch, a uniform loss) is one
   // pattern: uniform store masks, and the bitsliced kernels regardless of block alignment
@@ -366,13 +457,21 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   const bool aligned = aligned16(orig) && aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0;
   const unsigned npts = xform_points(k, m, S);
   const bool fast_geo = mode == AG_RS_DECODE_ANY_K && npts != 0 && m == npts && aligned;
-  const size_t xchunk = hr == 1 ? next_pow2(m) : 0;
-  const size_t xw = hr == 1 ? next_pow2(xchunk + k) : 0;
+  // decode_x window: HighRate, W = next_pow2(chunk + k) in {32, 64}; or the LowRate
+  // sub-window [0, 64) when next_pow2(k) = 32 (CodingOnly 32:64, PETS 32:33): originals
+  // at 0..k-1, their zero padding k..31 (known zeros, survivors for free), recovery
+  // 0..31 at 32..63.  The LowRate polynomial has degree < 32, so any 32 survivors inside
+  // the window decode it there (ANY_K; patterns with fewer survivors inside take another
+  // path).
+  const bool x_lr = hr == 0 && next_pow2(k) == 32 && mode == AG_RS_DECODE_ANY_K;
+  const size_t xchunk = hr == 1 ? next_pow2(m) : x_lr ? 32 : 0;
+  const size_t xw = hr == 1 ? next_pow2(xchunk + k) : x_lr ? 64 : 0;
+  const size_t xm_rec = hr == 1 ? m : std::min<size_t>(m, 32);  // recovery shards inside the window
   const size_t cps = S / 64;
-  // decode_x: HighRate, W in {32, 64}; one pattern per tile (single pattern, or tiles
-  // that never straddle blocks), else per-lane patterns (each lane one chunk of one block:
-  // the follower's per-slice patterns on 1 KiB shreds)
-  const bool x_geo = hr == 1 && S % 64 == 0 && (xw == 32 || xw == 64) && aligned;
+  // decode_x: one pattern per tile (single pattern, or tiles that never straddle blocks),
+  // else per-lane patterns (each lane one chunk of one block: the follower's per-slice
+  // patterns on 1 KiB shreds)
+  const bool x_geo = (hr == 1 || x_lr) && S % 64 == 0 && (xw == 32 || xw == 64) && aligned;
   const bool x_per_lane = npat > 1 && cps % 64 != 0;
   // decode_syn: the encode_mc geometries (chunk <= 4), any k survivors, same tiling rule
   const unsigned syn_chunk = mode == AG_RS_DECODE_ANY_K && aligned && (npat == 1 || cps % 64 == 0)
@@ -415,7 +514,7 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     } else if (syn_chunk && build_syn_pattern(k, m, opres + p * k, rpres + p * m, G.data(), &syn[p])) {
       cls[p] = 4;
       any_syn = true;
-    } else if (x_geo) {
+    } else if (x_geo && (hr == 1 || count_flags(opres + p * k, k) + count_flags(rpres + p * m, xm_rec) >= k)) {
       cls[p] = 3;
       any_x = true;
     } else {
@@ -540,9 +639,10 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     std::vector<uint64_t> xm(3 * npat, 0);
     for (size_t p = 0; p < npat; ++p) {
       if (cls[p] != 3) continue;
-      // window positions: recovery j < xchunk, original i at xchunk + i (xchunk + k <= 64)
+      // window positions: HighRate recovery j < xchunk, original i at xchunk + i (xchunk + k
+      // <= 64); LowRate original i at i, recovery j at xchunk + j (j < xm_rec)
       const uint64_t ob = pack_flags(opres + p * k, k), kmask = (uint64_t{1} << k) - 1;
-      uint64_t rb = pack_flags(rpres + p * m, m);
+      uint64_t rb = pack_flags(rpres + p * m, xm_rec);
       // ANY_K: exactly k survivors -- the present originals, then recovery shards in index
       // order; surplus recovery shards count as erased (MDS: any k survivors determine the
       // originals), so only k input multiplies remain.  EXACT: every present shard, as
@@ -552,9 +652,16 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
         while (static_cast<size_t>(__builtin_popcountll(rb)) > budget) rb &= ~(uint64_t{1} << (63 - __builtin_clzll(rb)));
       }
       const uint64_t cmask = (uint64_t{1} << xchunk) - 1;  // xchunk <= 32
-      const uint64_t in = rb | (ob << xchunk);
-      const uint64_t out = (~ob & kmask) << xchunk;
-      const uint64_t e = (~rb & cmask) | out;  // lost / surplus recovery, virtual points m..chunk-1
+      uint64_t in, out, e;
+      if (hr == 1) {
+        in = rb | (ob << xchunk);
+        out = (~ob & kmask) << xchunk;
+        e = (~rb & cmask) | out;  // lost / surplus recovery, virtual points m..chunk-1
+      } else {
+        in = ob | (rb << xchunk);
+        out = ~ob & kmask;       // the zero padding k..31 is neither loaded nor erased
+        e = out | ((~rb & cmask) << xchunk);  // lost / surplus recovery, positions past m
+      }
       xm[p] = e;
       xm[npat + 2 * p] = in;
       xm[npat + 2 * p + 1] = out;
@@ -581,8 +688,9 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     p.pmask = c->d_xmask.as<uint64_t>() + npat;
     p.rows = c->d_rows.as<uint32_t>();
     p.k = static_cast<uint32_t>(k);
-    p.m = static_cast<uint32_t>(m);
+    p.m = static_cast<uint32_t>(xm_rec);
     p.chunk = static_cast<uint32_t>(xchunk);
+    p.low_rate = hr == 1 ? 0u : 1u;
     p.chunks_per_shard = static_cast<uint32_t>(cps);
     p.total_columns = static_cast<uint64_t>(nblocks) * cps;
     uint64_t ntiles;
@@ -776,7 +884,10 @@ int ag_rs_use_high_rate(size_t k, size_t m) {
 }
 
 int ag_rs_has_fast_path(size_t k, size_t m, size_t S) {
-  return xform_points(k, m, S) || mc_chunk(k, m, S) || lowrate_chunk(k, m, S) ? 1 : 0;
+  // shard sizes that are not whole 64-byte chunks run restrided (padded) on the same kernels
+  if (S == 0 || S % 2) return 0;
+  const size_t Sp = padded_shard(S);
+  return xform_points(k, m, Sp) || mc_chunk(k, m, Sp) || lowrate_chunk(k, m, Sp) ? 1 : 0;
 }
 
 int ag_rs_encode_batch(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,

@@ -1136,8 +1136,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     constexpr int t = decltype(T)::value;
     const uint32_t j = 8 * wave + t;  // wave-uniform
     if ((in_mask >> j) & 1) {          // PL: per lane
-      const bool is_rec = j < p.chunk;
-      const uint8_t* base = is_rec ? p.rec + j * p.rec_shard_stride : p.orig + (j - p.chunk) * p.orig_shard_stride;
+      const uint32_t opos = p.low_rate ? 0 : p.chunk, rpos = p.low_rate ? p.chunk : 0;
+      const bool is_rec = p.low_rate ? j >= p.chunk : j < p.chunk;
+      const uint8_t* base = is_rec ? p.rec + (j - rpos) * p.rec_shard_stride : p.orig + (j - opos) * p.orig_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
         const uint8_t* src;
@@ -1184,7 +1185,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     constexpr int t = decltype(T)::value;
     const uint32_t j = 8 * wave + t;
     if ((out_mask >> j) & 1) {
-      uint8_t* dst = p.orig + (j - p.chunk) * p.orig_shard_stride;
+      uint8_t* dst = p.orig + (j - (p.low_rate ? 0 : p.chunk)) * p.orig_shard_stride;
       if constexpr (PL) {
 #if !(AG_DX_DIAG & 2)
         mul_rt_lane(ra[t], rows + j * 16);
@@ -1753,6 +1754,59 @@ __global__ __launch_bounds__(256) void coder_pad_kernel(const uint8_t* __restric
   for (int i = 0; i < 16; ++i) dst[i] = v[i];
 }
 
+// Shard restride for shard sizes that are not whole 64-byte chunks (the
+// crate stores the last T = S mod 64 bytes as T/2 low bytes then T/2 high bytes of T/2
+// symbols).  pack: shard (S bytes, any alignment) -> padded shard of Sp = ceil(S/64)*64
+// bytes whose last chunk holds the tail symbols in whole-chunk layout (low bytes at 0..,
+// high bytes at 32..) with zero symbols after them; unpack is the inverse and writes only
+// the shards selected by the store mask.  Zero symbols are zero columns of every linear
+// transform, so the bitsliced kernels run on the padded shards unchanged.  One thread per
+// 4 bytes of the padded shard.
+struct RestrideParams {
+  const uint8_t* src;
+  uint64_t src_block_stride, src_shard_stride;
+  uint8_t* dst;
+  uint64_t dst_block_stride, dst_shard_stride;
+  uint32_t S, Sp, nshards, unpack;
+  uint64_t nblocks;
+  const uint64_t* mask;  // unpack: store shard s of block b iff bit s of mask[per_block ? b : 0]
+  uint32_t mask_per_block;
+};
+// padded offset q -> offset in the crate-layout shard, or -1 (a zero symbol's byte)
+__device__ __forceinline__ int64_t restride_src(uint32_t q, uint32_t S) {
+  const uint32_t whole = S >> 6, h = (S & 63) >> 1;
+  if (q < 64 * whole) return q;
+  const uint32_t w = q - 64 * whole;
+  if (w < 32) return w < h ? static_cast<int64_t>(64 * whole + w) : -1;
+  return w - 32 < h ? static_cast<int64_t>(64 * whole + h + (w - 32)) : -1;
+}
+__global__ __launch_bounds__(256) void restride_kernel(const RestrideParams p) {
+  const uint64_t per_shard = p.Sp / 4, per_block = per_shard * p.nshards;
+  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (tid >= p.nblocks * per_block) return;
+  const uint64_t b = tid / per_block;
+  const uint32_t r = static_cast<uint32_t>(tid - b * per_block);
+  const uint32_t sh = r / static_cast<uint32_t>(per_shard), u = r - sh * static_cast<uint32_t>(per_shard);
+  const uint32_t q = 4 * u;
+  if (!p.unpack) {
+    const uint8_t* src = p.src + b * p.src_block_stride + sh * p.src_shard_stride;
+    uint32_t v = 0;
+    for (int i = 0; i < 4; ++i) {
+      const int64_t o = restride_src(q + i, p.S);
+      if (o >= 0) v |= static_cast<uint32_t>(src[o]) << (8 * i);
+    }
+    *reinterpret_cast<uint32_t*>(p.dst + b * p.dst_block_stride + sh * p.dst_shard_stride + q) = v;
+  } else {
+    if (p.mask && !((p.mask[p.mask_per_block ? b : 0] >> sh) & 1)) return;
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(p.src + b * p.src_block_stride + sh * p.src_shard_stride + q);
+    uint8_t* dst = p.dst + b * p.dst_block_stride + sh * p.dst_shard_stride;
+    for (int i = 0; i < 4; ++i) {
+      const int64_t o = restride_src(q + i, p.S);
+      if (o >= 0) dst[o] = static_cast<uint8_t>(v >> (8 * i));
+    }
+  }
+}
+
 // Per slice: payload length after stripping the bit padding (trailing zeros, then a 0x80
 // marker), or -1 when the padding is invalid.  One workgroup per slice.
 // Padding strip (reed_solomon.rs:191-203): the last non-zero byte of the data region must
@@ -1864,7 +1918,8 @@ hipError_t launch_xform_lowrate_decode(unsigned j, const XformParams& p, hipStre
 hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
   if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  if (p.k + p.chunk > W || p.m > p.chunk) return hipErrorInvalidValue;
+  if (p.k + p.chunk > W || p.m > p.chunk || (p.low_rate && (p.k > p.chunk || p.m + p.chunk > W)))
+    return hipErrorInvalidValue;
   const dim3 grid(static_cast<unsigned>(ntiles));
   const bool pl = p.per_lane != 0;
   switch (W) {
@@ -1991,6 +2046,31 @@ hipError_t launch_coder_pad(const uint8_t* payload, uint64_t payload_stride, con
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(coder_pad_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream, payload,
                      payload_stride, lens, cw, cw_stride, data_bytes, nslices);
+  return hipGetLastError();
+}
+
+hipError_t launch_restride(const uint8_t* src, uint64_t src_block_stride, uint64_t src_shard_stride, uint8_t* dst,
+                           uint64_t dst_block_stride, uint64_t dst_shard_stride, uint32_t S, uint32_t nshards,
+                           uint64_t nblocks, bool unpack, const uint64_t* mask, bool mask_per_block,
+                           hipStream_t stream) {
+  RestrideParams p{};
+  p.src = src;
+  p.src_block_stride = src_block_stride;
+  p.src_shard_stride = src_shard_stride;
+  p.dst = dst;
+  p.dst_block_stride = dst_block_stride;
+  p.dst_shard_stride = dst_shard_stride;
+  p.S = S;
+  p.Sp = (S + 63) / 64 * 64;
+  p.nshards = nshards;
+  p.unpack = unpack ? 1u : 0u;
+  p.nblocks = nblocks;
+  p.mask = mask;
+  p.mask_per_block = mask_per_block ? 1u : 0u;
+  const uint64_t n = nblocks * nshards * (p.Sp / 4);
+  if (n == 0) return hipSuccess;
+  if ((n + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(restride_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream, p);
   return hipGetLastError();
 }
 

@@ -93,7 +93,9 @@ struct DecodeXParams {
   uint32_t per_block;         // 1: pattern = block, tiles_per_block tiles per block
   uint32_t tiles_per_block;   // chunks_per_shard / 64 (per_block mode)
   uint32_t per_lane;          // 1: pattern = block of each lane's chunk (tiles straddle blocks)
-  uint32_t k, m, chunk;
+  uint32_t k, m, chunk;       // m: recovery shards inside the window
+  uint32_t low_rate;          // 0: recovery j at position j, original i at chunk + i (HighRate);
+                              // 1: original i at i, recovery j at chunk + j (LowRate sub-window)
   uint32_t chunks_per_shard;
   uint64_t total_columns;  // batch blocks * chunks_per_shard
 };
@@ -144,6 +146,14 @@ hipError_t launch_generic_decode(const GenericDecodeParams& p, hipStream_t strea
 // >= fill_from up to 65535 are also erased (LowRate virtual recovery); loc[p * W + x].
 hipError_t launch_locator(const uint8_t* erased, uint32_t npatterns, uint32_t W, uint32_t fill_from,
                           const uint16_t* log_walsh, uint16_t* loc, hipStream_t stream);
+
+// Shard restride (sizes that are not whole 64-byte chunks): pack = crate layout (tail chunk
+// split into low / high halves) -> padded shards of ceil(S/64)*64 bytes (whole-chunk
+// layout, zero symbols after the tail); unpack = the inverse, shards selected by mask.
+hipError_t launch_restride(const uint8_t* src, uint64_t src_block_stride, uint64_t src_shard_stride, uint8_t* dst,
+                           uint64_t dst_block_stride, uint64_t dst_shard_stride, uint32_t S, uint32_t nshards,
+                           uint64_t nblocks, bool unpack, const uint64_t* mask, bool mask_per_block,
+                           hipStream_t stream);
 
 // ReedSolomonCoder batches: padding writer (payload null = in place) and padding strip
 // (out[b] = payload length, or -1 for invalid padding).  data_bytes = 32 * S, % 16 == 0.

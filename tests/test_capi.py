@@ -69,7 +69,9 @@ def test_unsupported_counts(lib):
 def test_fast_path_geometry(lib):
     assert rs.has_fast_path(32, 32, 1024) and rs.has_fast_path(32, 32, 32768)
     assert rs.has_fast_path(20, 30, 64)
-    assert not rs.has_fast_path(32, 32, 62)      # tail chunk -> generic kernel
+    assert rs.has_fast_path(32, 32, 62)          # tail chunk: restrided onto the same kernels
+    assert rs.has_fast_path(32, 32, 1000) and rs.has_fast_path(32, 64, 1022) and rs.has_fast_path(16, 4, 2)
+    assert not rs.has_fast_path(32, 32, 63)      # odd: InvalidShardSize
     assert rs.has_fast_path(32, 64, 1024)        # LowRate: one transform launch per chunk
     assert rs.has_fast_path(32, 33, 1024)
     assert not rs.has_fast_path(16, 64, 1024)    # LowRate chunk 16 -> generic kernel

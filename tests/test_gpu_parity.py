@@ -764,3 +764,71 @@ def test_decode_per_slice_random_patterns(ctx, dev, S, n, mode):
                 d_r[b, j] = 0x99
     got = gpu_decode(ctx, dev, d_o, d_r, op, rp, mode)
     assert np.array_equal(got, blocks)
+
+
+# --------------------------------------------- shard sizes that are not whole 64-byte chunks
+
+@pytest.mark.parametrize("k,m,S", [(32, 32, 62), (32, 32, 1000), (32, 32, 1022), (32, 64, 1000), (32, 33, 1022),
+                                   (16, 4, 1000), (64, 64, 200), (20, 30, 66), (32, 32, 2)])
+def test_tail_chunk_encode_decode(ctx, dev, k, m, S):
+    """S mod 64 != 0 (reed_solomon.rs:94-95: every slice whose padded payload is not a
+    multiple of 2 KiB): restrided onto the bitsliced kernels.  Encode and decode (shared
+    pattern with lost coding shreds, per-block random patterns, both modes) against the C
+    oracle, which restates the crate's tail layout."""
+    assert rs.has_fast_path(k, m, S)
+    n = 7
+    blocks = np.stack([np.frombuffer(o.block_bytes(3100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = gpu_encode(ctx, dev, blocks, m)
+    assert np.array_equal(rec, ro_c.encode_blocks(blocks, m, threads=8))
+    rng = random.Random(k * 10007 + m * 101 + S)
+    for per_block in (False, True):
+        op, rp = [], []
+        d_o, d_r = blocks.copy(), rec.copy()
+        for b in range(n if per_block else 1):
+            keep = set(rng.sample(range(k + m), k + rng.randint(0, min(3, m))))
+            op += [1 if i in keep else 0 for i in range(k)]
+            rp += [1 if k + j in keep else 0 for j in range(m)]
+        for b in range(n):
+            pb = b if per_block else 0
+            for i in range(k):
+                if not op[pb * k + i]:
+                    d_o[b, i] = 0x3C
+            for j in range(m):
+                if not rp[pb * m + j]:
+                    d_r[b, j] = 0xC3
+        for mode in (rs.DECODE_ANY_K, rs.DECODE_EXACT):
+            got = gpu_decode(ctx, dev, d_o, d_r, op, rp, mode)
+            assert np.array_equal(got, blocks), (per_block, mode)
+
+
+@pytest.mark.parametrize("k,m,S", [(32, 64, 1024), (32, 33, 2048), (20, 40, 128), (32, 64, 4096), (25, 33, 192)])
+def test_lowrate_window_decode(ctx, dev, k, m, S):
+    """LowRate (CodingOnly 32:64, PETS 32:33, shredder.rs:362-446) with mixed losses and no
+    full recovery chunk: any 32 survivors among the originals (plus their zero padding)
+    and recovery shreds 0..31 decode in the 64-point sub-window; patterns that need
+    recovery shreds past 31 take the table-driven decoder.  Per-block random patterns
+    (tiles straddle blocks below 4 KiB), ANY_K, against the original data."""
+    n = 12
+    blocks = np.stack([np.frombuffer(o.block_bytes(4100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = gpu_encode(ctx, dev, blocks, m)
+    assert np.array_equal(rec, ro_c.encode_blocks(blocks, m, threads=8))
+    rng = random.Random(k * 7 + m + S)
+    d_o, d_r, op, rp = blocks.copy(), rec.copy(), [], []
+    for b in range(n):
+        if b % 4 == 3 and m > 32:   # k - 1 survivors inside the window, the rest past recovery 31
+            keep_o = set(rng.sample(range(k), 2))
+            keep_r = set(range(32, m)) | set(rng.sample(range(32), k - 3))
+        else:
+            w = min(m, 32)
+            keep_o = set(rng.sample(range(k), rng.randint(max(0, k - w), k)))
+            keep_r = set(rng.sample(range(w), min(w, k - len(keep_o) + rng.randint(0, 2))))
+        op += [1 if i in keep_o else 0 for i in range(k)]
+        rp += [1 if j in keep_r else 0 for j in range(m)]
+        for i in range(k):
+            if i not in keep_o:
+                d_o[b, i] = 0x11
+        for j in range(m):
+            if j not in keep_r:
+                d_r[b, j] = 0x22
+    got = gpu_decode(ctx, dev, d_o, d_r, op, rp, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
