@@ -14,6 +14,7 @@
 //   fill_splitmix     synthetic input blocks (bench / tests), generated on the device.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "rs_device.hpp"
@@ -1760,8 +1761,7 @@ __global__ __launch_bounds__(256) void coder_pad_kernel(const uint8_t* __restric
 // bytes whose last chunk holds the tail symbols in whole-chunk layout (low bytes at 0..,
 // high bytes at 32..) with zero symbols after them; unpack is the inverse and writes only
 // the shards selected by the store mask.  Zero symbols are zero columns of every linear
-// transform, so the bitsliced kernels run on the padded shards unchanged.  One thread per
-// 4 bytes of the padded shard.
+// transform, so the bitsliced kernels run on the padded shards unchanged.
 struct RestrideParams {
   const uint8_t* src;
   uint64_t src_block_stride, src_shard_stride;
@@ -1780,29 +1780,89 @@ __device__ __forceinline__ int64_t restride_src(uint32_t q, uint32_t S) {
   if (w < 32) return w < h ? static_cast<int64_t>(64 * whole + w) : -1;
   return w - 32 < h ? static_cast<int64_t>(64 * whole + h + (w - 32)) : -1;
 }
+// 16 bytes at a 2-byte-aligned (or better) address as 4 little-endian dwords
+__device__ __forceinline__ uint4 load16_a2(const uint8_t* src) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(src);
+  if ((a & 15) == 0) return *reinterpret_cast<const uint4*>(src);
+  if ((a & 7) == 0) {
+    const uint2 lo = reinterpret_cast<const uint2*>(src)[0], hi = reinterpret_cast<const uint2*>(src)[1];
+    return make_uint4(lo.x, lo.y, hi.x, hi.y);
+  }
+  if ((a & 3) == 0) {
+    const uint32_t* d = reinterpret_cast<const uint32_t*>(src);
+    return make_uint4(d[0], d[1], d[2], d[3]);
+  }
+  // a % 4 == 2: the middle three dwords are aligned; the outer half-dwords are read as
+  // 16-bit loads so that nothing outside [a, a + 16) is touched
+  const uint32_t* d = reinterpret_cast<const uint32_t*>(a + 2);
+  const uint32_t d0 = static_cast<uint32_t>(*reinterpret_cast<const uint16_t*>(src)) << 16;
+  const uint32_t d1 = d[0], d2 = d[1], d3 = d[2];
+  const uint32_t d4 = *reinterpret_cast<const uint16_t*>(src + 14);
+  return make_uint4(__builtin_amdgcn_alignbyte(d1, d0, 2), __builtin_amdgcn_alignbyte(d2, d1, 2),
+                    __builtin_amdgcn_alignbyte(d3, d2, 2), __builtin_amdgcn_alignbyte(d4, d3, 2));
+}
+__device__ __forceinline__ void store16_a2(uint8_t* dst, uint4 v) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(dst);
+  if ((a & 15) == 0) {
+    *reinterpret_cast<uint4*>(dst) = v;
+  } else if ((a & 7) == 0) {
+    reinterpret_cast<uint2*>(dst)[0] = make_uint2(v.x, v.y);
+    reinterpret_cast<uint2*>(dst)[1] = make_uint2(v.z, v.w);
+  } else if ((a & 3) == 0) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    d[0] = v.x;
+    d[1] = v.y;
+    d[2] = v.z;
+    d[3] = v.w;
+  } else {  // a % 4 == 2: a half-dword, three dwords, a half-dword
+    uint16_t* h = reinterpret_cast<uint16_t*>(dst);
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst + 2);
+    h[0] = static_cast<uint16_t>(v.x);
+    d[0] = __builtin_amdgcn_alignbyte(v.y, v.x, 2);
+    d[1] = __builtin_amdgcn_alignbyte(v.z, v.y, 2);
+    d[2] = __builtin_amdgcn_alignbyte(v.w, v.z, 2);
+    h[7] = static_cast<uint16_t>(v.w >> 16);
+  }
+}
+
+// One thread per 16 bytes of the padded shard.  Whole chunks move as 16-byte pieces (shard
+// sizes are even, so the crate-layout side is at least 2-byte aligned when its strides
+// are even); the tail chunk and odd strides go byte by byte.
 __global__ __launch_bounds__(256) void restride_kernel(const RestrideParams p) {
-  const uint64_t per_shard = p.Sp / 4, per_block = per_shard * p.nshards;
-  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (tid >= p.nblocks * per_block) return;
-  const uint64_t b = tid / per_block;
-  const uint32_t r = static_cast<uint32_t>(tid - b * per_block);
-  const uint32_t sh = r / static_cast<uint32_t>(per_shard), u = r - sh * static_cast<uint32_t>(per_shard);
-  const uint32_t q = 4 * u;
+  // grid: x = 16-byte pieces of one block (per_block <= 2^31), y = blocks of this launch
+  const uint32_t per_shard = p.Sp / 16, per_block = per_shard * p.nshards;
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= per_block) return;
+  const uint64_t b = blockIdx.y + static_cast<uint64_t>(blockIdx.z) * 65535;
+  if (b >= p.nblocks) return;
+  const uint32_t sh = r / per_shard, u = r - sh * per_shard;
+  const uint32_t q = 16 * u;
+  const bool whole = q + 16 <= 64 * (p.S >> 6);
   if (!p.unpack) {
     const uint8_t* src = p.src + b * p.src_block_stride + sh * p.src_shard_stride;
-    uint32_t v = 0;
-    for (int i = 0; i < 4; ++i) {
-      const int64_t o = restride_src(q + i, p.S);
-      if (o >= 0) v |= static_cast<uint32_t>(src[o]) << (8 * i);
+    uint4* dst = reinterpret_cast<uint4*>(p.dst + b * p.dst_block_stride + sh * p.dst_shard_stride + q);
+    if (whole && (reinterpret_cast<uintptr_t>(src) & 1) == 0) {
+      *dst = load16_a2(src + q);
+    } else {
+      uint32_t v[4] = {0, 0, 0, 0};
+      for (int i = 0; i < 16; ++i) {
+        const int64_t o = restride_src(q + i, p.S);
+        if (o >= 0) v[i >> 2] |= static_cast<uint32_t>(src[o]) << (8 * (i & 3));
+      }
+      *dst = make_uint4(v[0], v[1], v[2], v[3]);
     }
-    *reinterpret_cast<uint32_t*>(p.dst + b * p.dst_block_stride + sh * p.dst_shard_stride + q) = v;
   } else {
     if (p.mask && !((p.mask[p.mask_per_block ? b : 0] >> sh) & 1)) return;
-    const uint32_t v = *reinterpret_cast<const uint32_t*>(p.src + b * p.src_block_stride + sh * p.src_shard_stride + q);
+    const uint4 v = *reinterpret_cast<const uint4*>(p.src + b * p.src_block_stride + sh * p.src_shard_stride + q);
     uint8_t* dst = p.dst + b * p.dst_block_stride + sh * p.dst_shard_stride;
-    for (int i = 0; i < 4; ++i) {
-      const int64_t o = restride_src(q + i, p.S);
-      if (o >= 0) dst[o] = static_cast<uint8_t>(v >> (8 * i));
+    if (whole && (reinterpret_cast<uintptr_t>(dst) & 1) == 0) {
+      store16_a2(dst + q, v);
+    } else {
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+      for (int i = 0; i < 16; ++i) {
+        const int64_t o = restride_src(q + i, p.S);
+        if (o >= 0) dst[o] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+      }
     }
   }
 }
@@ -2067,10 +2127,12 @@ hipError_t launch_restride(const uint8_t* src, uint64_t src_block_stride, uint64
   p.nblocks = nblocks;
   p.mask = mask;
   p.mask_per_block = mask_per_block ? 1u : 0u;
-  const uint64_t n = nblocks * nshards * (p.Sp / 4);
-  if (n == 0) return hipSuccess;
-  if ((n + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(restride_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream, p);
+  const uint64_t per_block = static_cast<uint64_t>(nshards) * (p.Sp / 16);
+  if (per_block == 0 || nblocks == 0) return hipSuccess;
+  if (per_block > 0x7FFFFFFFull || nblocks > 65535ull * 65535ull) return hipErrorInvalidValue;
+  const dim3 grid(static_cast<unsigned>((per_block + 255) / 256), static_cast<unsigned>(std::min<uint64_t>(nblocks, 65535)),
+                  static_cast<unsigned>((nblocks + 65534) / 65535));
+  hipLaunchKernelGGL(restride_kernel, grid, dim3(256), 0, stream, p);
   return hipGetLastError();
 }
 

@@ -252,16 +252,30 @@ def decode_batch(ctx: Context, k: int, m: int, shard_bytes: int, nblocks: int, o
                  original_block_stride: int, recovery, recovery_block_stride: int,
                  original_present, recovery_present, mode: int = DECODE_ANY_K,
                  memory: int = MEM_DEVICE):
-    """original_present / recovery_present: bytes-like 0/1 flags, one pattern
-    (len k / m) or one per block (len nblocks*k / nblocks*m)."""
-    op = bytes(bytearray(original_present))
-    rp = bytes(bytearray(recovery_present))
+    """original_present / recovery_present: 0/1 flags (bytes, numpy uint8 or a list), one
+    pattern (len k / m) or one per block (len nblocks*k / nblocks*m).  bytes and uint8
+    arrays are passed without a copy (per-block patterns of large batches)."""
+    op, rp = _flags(original_present), _flags(recovery_present)
     npat = len(op) // k
     if len(op) != npat * k or len(rp) != npat * m:
         raise ValueError("present-flag arrays do not match the geometry")
     _check(load().ag_rs_decode_batch(ctx.handle, k, m, shard_bytes, nblocks, _ptr(original),
                                      original_block_stride, _ptr(recovery), recovery_block_stride,
-                                     op, rp, npat, mode, memory), "ag_rs_decode_batch")
+                                     _fptr(op), _fptr(rp), npat, mode, memory), "ag_rs_decode_batch")
+
+
+def _flags(f):
+    if isinstance(f, bytes):
+        return f
+    import numpy as np
+
+    if isinstance(f, np.ndarray) and f.dtype == np.uint8 and f.flags.c_contiguous:
+        return f
+    return bytes(bytearray(f))
+
+
+def _fptr(f):
+    return f if isinstance(f, bytes) else f.ctypes.data
 
 
 def coder_shred_batch(ctx: Context, num_coding: int, nslices: int, shred_bytes: int, payloads,

@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pcie", action="store_true", help="also time host-buffer calls")
+    ap.add_argument("--pcie-blocks", type=int, default=4096, help="blocks in the host-buffer run")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-settle", action="store_true",
                     help="skip the untimed clock-settle steps that follow the W warmup steps")
@@ -106,12 +107,13 @@ def main():
     rs.fill_splitmix(ctx, cw, n, k * S, cw_stride, seed_base)
     data_ptr, par_ptr = cw.data_ptr(), cw.data_ptr() + k * S
     opres, rpres = erasure_patterns(plan, k, m, e, lc, args.random_patterns)
+    opres_b, rpres_b = bytes(opres), bytes(rpres)  # converted once, outside the timed region
 
     def encode():
         rs.encode_batch(ctx, k, m, S, n, data_ptr, cw_stride, par_ptr, cw_stride)
 
     def reconstruct():
-        rs.decode_batch(ctx, k, m, S, n, data_ptr, cw_stride, par_ptr, cw_stride, opres, rpres,
+        rs.decode_batch(ctx, k, m, S, n, data_ptr, cw_stride, par_ptr, cw_stride, opres_b, rpres_b,
                         mode=rs.DECODE_ANY_K)
 
     def barrier():
@@ -387,7 +389,7 @@ def _pcie(args, ctx, cw, k, m, S, e, torch, dev):
     pinned-copy rates of the same bytes for context."""
     from alpenglow_amd import rs
 
-    nb = min(cw.shape[0], 1024)
+    nb = min(cw.shape[0], args.pcie_blocks)
     stride = (k + m) * S
     host = torch.empty((nb, stride), dtype=torch.uint8, pin_memory=True)
     host.copy_(cw[:nb])
