@@ -68,9 +68,28 @@ static void init(void) {
         g_mul128[lm][n][1][v] = (uint8_t)(prod >> 8);
       }
 }
+static pthread_key_t g_work_key;
+static void free_work(void *p) { free(p); }
+static void init_key(void) { pthread_key_create(&g_work_key, free_work); }
 static int ready(void) {
   pthread_once(&g_once, init);
   return g_mul128 != NULL;
+}
+
+/* Per-thread work buffer, kept across calls like the crate's encoder / decoder work
+ * buffers (reset() reuses them): [size_t capacity][64-byte aligned bytes...]. */
+static pthread_once_t g_key_once = PTHREAD_ONCE_INIT;
+static uint8_t *work_buffer(size_t bytes) {
+  pthread_once(&g_key_once, init_key);
+  uint8_t *p = pthread_getspecific(g_work_key);
+  if (p && *(size_t *)p >= bytes) return p + 64;
+  free(p);
+  const size_t cap = bytes + (bytes >> 2);
+  p = aligned_alloc(64, (cap + 64 + 63) / 64 * 64);
+  if (!p) return NULL;
+  *(size_t *)p = cap;
+  pthread_setspecific(g_work_key, p);
+  return p + 64;
 }
 
 int rb_avx2_available(void) { return __builtin_cpu_supports("avx2") ? 1 : 0; }
@@ -158,7 +177,7 @@ int rb_encode(size_t k, size_t m, size_t S, const uint8_t *orig, uint8_t *rec) {
   const size_t cover = hr ? k : m;
   size_t rows = ((cover + chunk - 1) / chunk) * chunk;
   if (rows < chunk) rows = chunk;
-  uint8_t *w = aligned_alloc(64, rows * S);
+  uint8_t *w = work_buffer(rows * S);
   if (!w) return RB_NO_MEMORY;
   memcpy(w, orig, k * S);
   memset(w + k * S, 0, (rows - k) * S);
@@ -183,7 +202,6 @@ int rb_encode(size_t k, size_t m, size_t S, const uint8_t *orig, uint8_t *rec) {
     if (m % chunk) fft(w, S, cs, chunk, m % chunk, cs + chunk);
   }
   memcpy(rec, w, m * S);
-  free(w);
   return RB_OK;
 }
 
@@ -252,13 +270,11 @@ int rb_decode(size_t k, size_t m, size_t S, const uint8_t *orig, const uint8_t *
   const size_t chunk = hr ? next_pow2(m) : next_pow2(k);
   const size_t end = hr ? chunk + k : chunk + m;
   const size_t W = next_pow2(end);
-  uint16_t *e = calloc(GF_ORDER, sizeof(uint16_t));
-  uint8_t *w = aligned_alloc(64, W * S);
-  if (!e || !w) {
-    free(e);
-    free(w);
-    return RB_NO_MEMORY;
-  }
+  uint8_t *buf = work_buffer(W * S + GF_ORDER * sizeof(uint16_t));
+  if (!buf) return RB_NO_MEMORY;
+  uint8_t *w = buf;
+  uint16_t *e = (uint16_t *)(buf + W * S);
+  memset(e, 0, GF_ORDER * sizeof(uint16_t));
   const size_t opos = hr ? chunk : 0, rpos = hr ? 0 : chunk;
   for (size_t i = 0; i < k; ++i) e[opos + i] = !orig_present[i];
   for (size_t i = 0; i < m; ++i) e[rpos + i] = !rec_present[i];
@@ -281,8 +297,6 @@ int rb_decode(size_t k, size_t m, size_t S, const uint8_t *orig, const uint8_t *
   fft(w, S, 0, W, hr ? end : k, 0);
   for (size_t i = 0; i < k; ++i)
     if (!orig_present[i]) mul_row(out + i * S, w + (opos + i) * S, S, (uint16_t)(GF_MODULUS - e[opos + i]), 0);
-  free(e);
-  free(w);
   return RB_OK;
 }
 
