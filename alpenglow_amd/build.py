@@ -27,13 +27,13 @@ ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else "hipcc")
 CXX = os.environ.get("CXX_HOST", "g++")
 
-SOURCES = ["rs_kernels.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hip", "slice.hip", "rs_api.cpp", "gf16.cpp"]
-HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_launch.hpp", "rs_consts.inc", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp", "slice.hpp"]
+SOURCES = ["rs_kernels.hip", "rs_decode_c.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hip", "slice.hip", "rs_api.cpp", "gf16.cpp"]
+HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_xform.hpp", "rs_launch.hpp", "rs_consts.inc", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp", "slice.hpp"]
 # -fno-slp-vectorize: the SLP vectoriser packs the bitsliced XOR networks into <2 x i32>
 # ops, which lengthens live ranges (measured +40 VGPRs on the transform kernel).
 # -amdgpu-promote-alloca-to-vector-limit: keeps the four-Russians tables of decode_x and
 # decode_syn (4 x 16 words, wave-uniform picks) in VGPRs (v_movrels) instead of scratch.
-# rs_kernels.hip needs 2048 (at 512 two of decode_syn's four tables land in scratch; no
+# rs_kernels.hip and rs_decode_c.hip need 2048 (at 512 two of decode_syn's four tables land in scratch; no
 # other RS kernel's VGPR or scratch use changes, checked with
 # -Rpass-analysis=kernel-resource-usage); the other sources keep 512, the setting their
 # kernels were measured with (2048 would change the Ed25519 kernels' scratch use).
@@ -95,7 +95,7 @@ def build(force: bool = False) -> str:
         obj = os.path.join(OBJDIR, s + ".o")
         objs.append(obj)
         deps = [os.path.join(CSRC, h) for h in _deps(s)] + [os.path.join(INCLUDE, "alpenglow_rs.h")]
-        limit = 2048 if s == "rs_kernels.hip" else 512
+        limit = 2048 if s in ("rs_kernels.hip", "rs_decode_c.hip") else 512
         cmd = [HIPCC, *HIP_FLAGS, "-mllvm", f"-amdgpu-promote-alloca-to-vector-limit={limit}", "-c", src, "-o", obj]
         # the stamp holds the full compile command: a flag change (AG_RS_EXTRA_HIPFLAGS
         # diagnostics, the promote-alloca limit) rebuilds the object even when no file changed

@@ -12,6 +12,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstddef>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <new>
@@ -111,6 +113,7 @@ struct ag_rs_ctx {
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
+  DevBuf d_corr, d_corrblocks;              // correction decoder: patterns, block ids
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
   DevBuf d_merkle_nodes;                    // Merkle node scratch (callers without a nodes buffer)
   DevBuf d_aon_lens, d_aon_digests, d_aon_keys;  // all-or-nothing transforms
@@ -131,6 +134,7 @@ struct ag_rs_ctx {
   std::vector<uint64_t> xmask_host;       // last general-decode masks (d_xmask), W = xmask_w
   size_t xmask_w = 0;
   std::vector<uint8_t> syn_key;             // (k, m, present flags) of the patterns in d_syn
+  std::vector<uint8_t> corr_key;            // (k, m, present flags) of the patterns in d_corr
 
   int enter() { return hipSetDevice(device) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE; }
 
@@ -196,7 +200,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_corr, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
                       &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -259,6 +263,120 @@ bool build_syn_pattern(size_t k, size_t m, const uint8_t* opres, const uint8_t* 
         for (unsigned o = 0; o < 16; ++o) sp->rows[a][b][o] |= ((prod >> o) & 1u) << i;
       }
   return true;
+}
+
+// In-place Gauss-Jordan inverse of an n x n matrix over GF(2^16) (row-major, stride n).
+// Returns false if singular.
+bool gf_invert(size_t n, uint16_t* A) {
+  const ag::Gf16Tables& t = ag::gf16_tables();
+  std::vector<uint16_t> M(n * 2 * n, 0);
+  for (size_t r = 0; r < n; ++r) {
+    for (size_t c = 0; c < n; ++c) M[r * 2 * n + c] = A[r * n + c];
+    M[r * 2 * n + n + r] = 1;
+  }
+  for (size_t col = 0; col < n; ++col) {
+    size_t piv = col;
+    while (piv < n && M[piv * 2 * n + col] == 0) ++piv;
+    if (piv == n) return false;
+    if (piv != col)
+      for (size_t x = 0; x < 2 * n; ++x) std::swap(M[piv * 2 * n + x], M[col * 2 * n + x]);
+    const uint16_t inv = ag::gf_inv(t, M[col * 2 * n + col]);
+    for (size_t x = 0; x < 2 * n; ++x) M[col * 2 * n + x] = ag::gf_mul_elem(t, M[col * 2 * n + x], inv);
+    for (size_t row = 0; row < n; ++row) {
+      const uint16_t f = M[row * 2 * n + col];
+      if (row == col || f == 0) continue;
+      for (size_t x = 0; x < 2 * n; ++x) M[row * 2 * n + x] ^= ag::gf_mul_elem(t, f, M[col * 2 * n + x]);
+    }
+  }
+  for (size_t r = 0; r < n; ++r)
+    for (size_t c = 0; c < n; ++c) A[r * n + c] = M[r * 2 * n + n + c];
+  return true;
+}
+
+// X = the 32-point full-recovery transform as a matrix (d_i = XOR_j X[i][j] * r_j): the
+// inverse of the 32:32 HighRate encoder.  A k < 32 code is the 32:32 code with originals
+// k..31 zero, so the same X serves every k <= 32 with m = 32.
+const uint16_t* full_window_x32() {
+  static const std::vector<uint16_t> X = [] {
+    std::vector<uint16_t> G(32 * 32);
+    ag::hr_generator(32, 32, G.data());
+    if (!gf_invert(32, G.data())) G.clear();  // cannot happen: the encoder is invertible
+    return G;
+  }();
+  return X.empty() ? nullptr : X.data();
+}
+
+// Correction-decoder pattern (decode_c_kernel): HighRate k <= 32, m = 32, lost recovery
+// shards L (1 <= |L| <= kCorrMaxSyn).  Syndrome points: virtual zeros k..31 first (no
+// load), then present originals in index order.  False if the pattern does not fit (the
+// caller takes another decoder).
+bool build_corr_pattern(size_t k, const uint8_t* opres, const uint8_t* rpres, ag::CorrPattern* cp) {
+  const uint16_t* X = full_window_x32();
+  if (!X || k > 32) return false;
+  const ag::Gf16Tables& t = ag::gf16_tables();
+  std::memset(cp, 0, offsetof(ag::CorrPattern, kmat));
+  uint8_t E[32], L[32], D[32];
+  size_t ne = 0, nl = 0, nd = 0;
+  for (size_t j = 0; j < 32; ++j) {
+    if (rpres[j]) cp->rmask |= uint64_t{1} << j;
+    else L[nl++] = static_cast<uint8_t>(j);
+  }
+  for (size_t i = 0; i < k; ++i)
+    if (!opres[i]) {
+      cp->emask |= uint64_t{1} << i;
+      E[ne++] = static_cast<uint8_t>(i);
+    }
+  if (nl == 0 || nl > static_cast<size_t>(ag::kCorrMaxSyn) || ne == 0 || ne * nl > ag::kCorrMaxPairs) return false;
+  for (size_t i = k; i < 32 && nd < nl; ++i) D[nd++] = static_cast<uint8_t>(i);
+  for (size_t i = 0; i < k && nd < nl; ++i)
+    if (opres[i]) D[nd++] = static_cast<uint8_t>(i);
+  if (nd < nl) return false;  // fewer than k survivors
+  for (size_t b = 0; b < nd; ++b) cp->smask |= uint64_t{1} << D[b];
+  // the syndrome rank b of point D[b] must follow position order (the kernel ranks by popcount)
+  std::sort(D, D + nd);
+  cp->ne = static_cast<uint32_t>(ne);
+  cp->ns = static_cast<uint32_t>(nl);
+  // N = X[D, L], K = X[E, L] N^-1
+  std::vector<uint16_t> N(nl * nl), K(ne * nl, 0);
+  for (size_t b = 0; b < nl; ++b)
+    for (size_t c = 0; c < nl; ++c) N[b * nl + c] = X[D[b] * 32 + L[c]];
+  if (!gf_invert(nl, N.data())) return false;
+  for (size_t a = 0; a < ne; ++a)
+    for (size_t b = 0; b < nl; ++b) {
+      uint16_t acc = 0;
+      for (size_t c = 0; c < nl; ++c) acc ^= ag::gf_mul_elem(t, X[E[a] * 32 + L[c]], N[c * nl + b]);
+      K[a * nl + b] = acc;
+    }
+  // bitsliced rows, two per dword
+  std::memset(cp->kmat, 0, ne * nl * 8 * sizeof(uint32_t));
+  for (size_t a = 0; a < ne; ++a)
+    for (size_t b = 0; b < nl; ++b) {
+      uint32_t rows[16] = {};
+      const uint16_t v = K[a * nl + b];
+      for (unsigned i = 0; i < 16; ++i) {
+        const uint16_t prod = ag::gf_mul_elem(t, v, static_cast<uint16_t>(1u << i));
+        for (unsigned o = 0; o < 16; ++o) rows[o] |= ((prod >> o) & 1u) << i;
+      }
+      uint32_t* dst = cp->kmat + 8 * (a * nl + b);
+      for (unsigned q = 0; q < 8; ++q) dst[q] = rows[2 * q] | (rows[2 * q + 1] << 16);
+    }
+  return true;
+}
+
+// The correction decoder takes a 32:m=32 pattern when 1 <= |L| <= kCorrMaxSyn recovery
+// shards are lost and some original is erased (no = present originals, nr = present
+// recovery shards; no + nr >= k is checked first).
+bool corr_fits(size_t k, size_t no, size_t nr) {
+  const size_t nl = 32 - nr, ne = k - no;
+  return nl >= 1 && nl <= static_cast<size_t>(ag::kCorrMaxSyn) && ne >= 1 && ne * nl <= ag::kCorrMaxPairs;
+}
+// AG_RS_NO_CORR=1 routes those patterns to decode_x instead (A/B timing).
+bool corr_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("AG_RS_NO_CORR");
+    return !(e && e[0] == '1');
+  }();
+  return on;
 }
 
 int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
@@ -489,7 +607,11 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   const bool lr_geo = mode == AG_RS_DECODE_ANY_K && hr == 0 && next_pow2(k) == 32 && S % 64 == 0 && aligned;
   std::vector<uint8_t> lr_chunk(npat, 0xFF);
   bool any_lr = false;
-  bool any_fast = false, any_generic = false, any_x = false, any_syn = false;
+  // decode_c: the 32-point full-window geometries (HighRate, m = 32, k <= 32) with lost
+  // recovery shards; any k survivors, same tiling rule
+  const bool corr_geo = mode == AG_RS_DECODE_ANY_K && hr == 1 && m == 32 && k <= 32 && S % 64 == 0 && aligned &&
+                        (npat == 1 || cps % 64 == 0) && corr_enabled();
+  bool any_fast = false, any_generic = false, any_x = false, any_syn = false, any_corr = false;
   for (size_t p = 0; p < npat; ++p) {
     const size_t no = count_flags(opres + p * k, k), nr = count_flags(rpres + p * m, m);
     if (no + nr < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;  // nothing launched yet
@@ -514,6 +636,9 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     } else if (syn_chunk && build_syn_pattern(k, m, opres + p * k, rpres + p * m, G.data(), &syn[p])) {
       cls[p] = 4;
       any_syn = true;
+    } else if (corr_geo && corr_fits(k, no, nr)) {
+      cls[p] = 6;
+      any_corr = true;
     } else if (x_geo && (hr == 1 || count_flags(opres + p * k, k) + count_flags(rpres + p * m, xm_rec) >= k)) {
       cls[p] = 3;
       any_x = true;
@@ -632,6 +757,61 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
       p.ntiles = static_cast<uint64_t>(ids.size()) * p.tiles_per_block;
     }
     if (ag::launch_decode_syn(syn_chunk, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
+  if (any_corr) {
+    // patterns are built and uploaded only when (k, m, flags) changed
+    std::vector<uint8_t> key(16 + npat * (k + m));
+    const uint64_t km[2] = {k, m};
+    std::memcpy(key.data(), km, 16);
+    for (size_t p = 0; p < npat; ++p) {
+      if (cls[p] != 6) continue;
+      std::memcpy(&key[16 + p * (k + m)], opres + p * k, k);
+      std::memcpy(&key[16 + p * (k + m) + k], rpres + p * m, m);
+    }
+    if (key != c->corr_key) {
+      std::vector<ag::CorrPattern> corr(npat);
+      for (size_t p = 0; p < npat; ++p) {
+        if (cls[p] != 6) {
+          std::memset(&corr[p], 0, offsetof(ag::CorrPattern, kmat));
+          continue;
+        }
+        // corr_fits admitted the pattern; the MDS property makes N invertible
+        if (!build_corr_pattern(k, opres + p * k, rpres + p * m, &corr[p])) return AG_RS_ERR_DEVICE;
+      }
+      c->corr_key.clear();
+      AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read d_corr
+      if ((st = c->d_corr.ensure(npat * sizeof(ag::CorrPattern), c->stream))) return st;
+      AG_HIP(hipMemcpy(c->d_corr.ptr, corr.data(), npat * sizeof(ag::CorrPattern), hipMemcpyHostToDevice));
+      c->corr_key = key;
+    }
+    ag::DecodeCParams p{};
+    p.rec = rec;
+    p.rec_block_stride = rstride;
+    p.rec_shard_stride = S;
+    p.orig = orig;
+    p.orig_block_stride = ostride;
+    p.orig_shard_stride = S;
+    p.pat = c->d_corr.as<ag::CorrPattern>();
+    p.k = static_cast<uint32_t>(k);
+    p.chunks_per_shard = static_cast<uint32_t>(cps);
+    p.total_columns = static_cast<uint64_t>(nblocks) * cps;
+    if (npat == 1) {
+      p.ntiles = (p.total_columns + 63) / 64;
+    } else {
+      p.per_block = 1;
+      p.tiles_per_block = static_cast<uint32_t>(cps / 64);
+      std::vector<uint32_t> ids;
+      for (size_t b = 0; b < nblocks; ++b)
+        if (cls[b] == 6) ids.push_back(static_cast<uint32_t>(b));
+      if (ids.size() != nblocks) {
+        AG_HIP(hipStreamSynchronize(c->stream));  // a previous id upload may be pending
+        if ((st = c->d_corrblocks.ensure(ids.size() * 4, c->stream))) return st;
+        AG_HIP(hipMemcpy(c->d_corrblocks.ptr, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+        p.block_ids = c->d_corrblocks.as<uint32_t>();
+      }
+      p.ntiles = static_cast<uint64_t>(ids.size()) * p.tiles_per_block;
+    }
+    if (ag::launch_decode_c(p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   }
   if (any_x) {
     if ((st = c->ensure_tables())) return st;

@@ -19,6 +19,7 @@
 
 #include "rs_device.hpp"
 #include "rs_launch.hpp"
+#include "rs_xform.hpp"
 
 // Diagnostic builds only (wrong output): bit 0 skips decode_x's input multiply, bit 1 its
 // output multiply, bit 2 the formal derivative.
@@ -40,294 +41,6 @@ namespace {
 
 using dev::static_for;
 
-// =====================================================================================
-// xform<NW>: N = 8 * NW point transform (NW = 4 -> 32, NW = 8 -> 64); NW waves x 64
-// lanes; lane = one 64-byte column (32 symbols) of one block, each lane owns 8 of the N
-// shards in each of three passes:
-//   pass A  (wave w: shards 8w+t)       IFFT layers dist 1, 2, 4        (skew delta DIN)
-//   pass B  (wave w: shards w+NW*t)     IFFT dist 8 .. N/2; FFT N/2 .. 8 (DIN / DOUT)
-//   pass C  (wave w: shards 8w+t)       FFT layers dist 4, 2, 1         (skew delta DOUT)
-// Shards change owner between passes through LDS (2 rounds per exchange: 64 KiB per
-// round for N = 32, 128 KiB for N = 64).
-// Skew index of a layer of distance d on the group starting at g: g + d + delta - 1.
-// In pass B the group start depends only on shard bits >= 4, i.e. on the slot index, so
-// that code is wave-independent; passes A and C branch once per butterfly on the
-// (scalar) wave id.
-// =====================================================================================
-
-constexpr int kXfLanes = 64;
-
-using Regs8 = uint32_t[8][16];
-
-// butterfly whose skew index is BASE + 8 * wave (wave-uniform, runtime)
-template <int S, bool INV>
-__device__ __forceinline__ void bfly(uint32_t* x, uint32_t* y) {
-  if constexpr (INV) dev::ifft_bfly<S>(x, y); else dev::fft_bfly<S>(x, y);
-}
-template <int BASE, bool INV, int NW>
-__device__ __forceinline__ void bfly_w(int wave, uint32_t* x, uint32_t* y) {
-#ifdef AG_XF_DIAG_ONE_ROLE
-  wave = 0;  // diagnostic build only: every wave runs role 0's code (wrong output)
-#endif
-  if constexpr (NW == 4) {
-    switch (wave) {
-      case 0: bfly<BASE, INV>(x, y); break;
-      case 1: bfly<BASE + 8, INV>(x, y); break;
-      case 2: bfly<BASE + 16, INV>(x, y); break;
-      default: bfly<BASE + 24, INV>(x, y); break;
-    }
-  } else {
-    switch (wave) {
-      case 0: bfly<BASE, INV>(x, y); break;
-      case 1: bfly<BASE + 8, INV>(x, y); break;
-      case 2: bfly<BASE + 16, INV>(x, y); break;
-      case 3: bfly<BASE + 24, INV>(x, y); break;
-      case 4: bfly<BASE + 32, INV>(x, y); break;
-      case 5: bfly<BASE + 40, INV>(x, y); break;
-      case 6: bfly<BASE + 48, INV>(x, y); break;
-      default: bfly<BASE + 56, INV>(x, y); break;
-    }
-  }
-}
-template <int NW, int DIN>
-__device__ __forceinline__ void xf_pass_a(int wave, Regs8& r) {
-  static_for<4>([&](auto I) {  // dist 1
-    constexpr int t = 2 * decltype(I)::value;
-    bfly_w<t + 1 + DIN - 1, true, NW>(wave, r[t], r[t + 1]);
-  });
-  static_for<4>([&](auto I) {  // dist 2
-    constexpr int g = 4 * (decltype(I)::value >> 1);
-    constexpr int u = g + (decltype(I)::value & 1);
-    bfly_w<g + 2 + DIN - 1, true, NW>(wave, r[u], r[u + 2]);
-  });
-  static_for<4>([&](auto I) {  // dist 4
-    constexpr int u = decltype(I)::value;
-    bfly_w<4 + DIN - 1, true, NW>(wave, r[u], r[u + 4]);
-  });
-}
-
-// Pass B: slot t holds shard w + NW*t.  Layer on shard bit sb (dist 2^sb, sb >= 3) pairs
-// slots t, t + 2^tb with tb = sb - log2(NW); group start (NW*t) & ~(2d - 1).
-template <int NW>
-struct PassB {
-  static constexpr int kLogNw = NW == 4 ? 2 : 3;
-  static constexpr int kLayers = NW == 4 ? 2 : 3;  // shard bits 3 .. 3 + kLayers - 1
-  template <int L, int I>
-  struct Pair {
-    static constexpr int sb = 3 + L, tb = sb - kLogNw, d = 1 << sb;
-    static constexpr int t = ((I >> tb) << (tb + 1)) | (I & ((1 << tb) - 1));
-    static constexpr int u = t + (1 << tb);
-    static constexpr int g = (NW * t) & ~(2 * d - 1);
-  };
-};
-template <int NW, int DIN>
-__device__ __forceinline__ void xf_pass_b_ifft(Regs8& r) {
-  constexpr int NL = PassB<NW>::kLayers;
-  static_for<NL>([&](auto L) {  // ascending distance
-    static_for<4>([&](auto I) {
-      using P = typename PassB<NW>::template Pair<decltype(L)::value, decltype(I)::value>;
-      dev::ifft_bfly<P::g + P::d + DIN - 1>(r[P::t], r[P::u]);
-    });
-  });
-}
-template <int NW, int DOUT>
-__device__ __forceinline__ void xf_pass_b_fft(Regs8& r) {
-  constexpr int NL = PassB<NW>::kLayers;
-  static_for<NL>([&](auto L) {  // descending distance
-    static_for<4>([&](auto I) {
-      using P = typename PassB<NW>::template Pair<NL - 1 - decltype(L)::value, decltype(I)::value>;
-      dev::fft_bfly<P::g + P::d + DOUT - 1>(r[P::t], r[P::u]);
-    });
-  });
-}
-template <int NW, int DIN, int DOUT>
-__device__ __forceinline__ void xf_pass_b(Regs8& r) {
-  xf_pass_b_ifft<NW, DIN>(r);
-  xf_pass_b_fft<NW, DOUT>(r);
-}
-
-template <int NW, int DOUT>
-__device__ __forceinline__ void xf_pass_c(int wave, Regs8& r) {
-  static_for<4>([&](auto I) {  // dist 4
-    constexpr int u = decltype(I)::value;
-    bfly_w<4 + DOUT - 1, false, NW>(wave, r[u], r[u + 4]);
-  });
-  static_for<4>([&](auto I) {  // dist 2
-    constexpr int g = 4 * (decltype(I)::value >> 1);
-    constexpr int u = g + (decltype(I)::value & 1);
-    bfly_w<g + 2 + DOUT - 1, false, NW>(wave, r[u], r[u + 2]);
-  });
-  static_for<4>([&](auto I) {  // dist 1
-    constexpr int t = 2 * decltype(I)::value;
-    bfly_w<t + 1 + DOUT - 1, false, NW>(wave, r[t], r[t + 1]);
-  });
-}
-
-__device__ __forceinline__ void lds_put(uint4* lds, int slot, int lane, const uint32_t* v) {
-  static_for<4>([&](auto Q) {
-    constexpr int q = decltype(Q)::value;
-    lds[(slot * 4 + q) * kXfLanes + lane] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-  });
-}
-__device__ __forceinline__ void lds_get(const uint4* lds, int slot, int lane, uint32_t* v) {
-  static_for<4>([&](auto Q) {
-    constexpr int q = decltype(Q)::value;
-    const uint4 x = lds[(slot * 4 + q) * kXfLanes + lane];
-    v[4 * q] = x.x;
-    v[4 * q + 1] = x.y;
-    v[4 * q + 2] = x.z;
-    v[4 * q + 3] = x.w;
-  });
-}
-
-// ---- tile I/O -------------------------------------------------------------------
-// A tile is 64 consecutive 64-byte chunks (global chunk index g = 64 * tile + c; chunk g
-// is chunk g % C of block g / C, C = chunks per shard).  Each of a lane's four 16-byte
-// loads per shard is one slice of a lane-linear 1 KiB wave access: instruction q covers
-// chunks 16q .. 16q+15 of the tile; lane l < 32 takes low-byte quarter (l & 1) of chunk
-// 16q + (l >> 1), lane l + 32 the matching high-byte quarter.  One v_permlane32_swap per
-// register pair then gives every lane the low AND high bytes of 32 symbols (2 chunks x 16
-// symbols): lane l < 32 keeps chunks q = 0, 1, lane l + 32 chunks q = 2, 3.
-struct TileIO {
-  uint64_t off[4];  // byte offset of this lane's 16-byte piece of shard 0, per instruction q
-  uint64_t blk[4];  // block of chunk q (for the per-block store mask)
-  uint32_t valid;   // bit q: chunk q exists (idle pieces re-read the last chunk, never store)
-};
-__device__ __forceinline__ TileIO tile_io_g(uint64_t total_columns, uint32_t chunks_per_shard, uint64_t tile, int lane,
-                                           uint64_t block_stride) {
-  TileIO io;
-  io.valid = 0;
-  const uint32_t quarter = ((lane >> 5) << 1) | (lane & 1);
-  static_for<4>([&](auto Q) {
-    constexpr int q = decltype(Q)::value;
-    const uint64_t g = tile * kXfLanes + 16 * q + ((lane & 31) >> 1);
-    const bool ok = g < total_columns;
-    const uint64_t gc = ok ? g : total_columns - 1;
-    const uint64_t blk = gc / chunks_per_shard;
-    io.blk[q] = blk;
-    io.off[q] = blk * block_stride + (gc - blk * chunks_per_shard) * 64 + 16 * quarter;
-    io.valid |= ok ? (1u << q) : 0u;
-  });
-  return io;
-}
-__device__ __forceinline__ TileIO tile_io(const XformParams& p, uint64_t tile, int lane, uint64_t block_stride) {
-  return tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, block_stride);
-}
-
-// lanes l and l + 32 exchange register halves (see TileIO); an involution
-__device__ __forceinline__ void swap_halves(uint32_t* v) {
-  static_for<8>([&](auto K) {
-    constexpr int k = decltype(K)::value;
-    const auto r = __builtin_amdgcn_permlane32_swap(v[k], v[k + 8], false, false);
-    v[k] = r[0];
-    v[k + 8] = r[1];
-  });
-}
-
-// Raw 16-byte pieces of this wave's pass-A shards 8*wave + t (before swap / transpose).
-__device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& io, int wave, Regs8& raw) {
-  static_for<8>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    const uint32_t s = 8 * wave + t;  // wave-uniform condition
-    if (s < p.n_in) {
-      const uint8_t* base = p.in + s * p.in_shard_stride;
-      static_for<4>([&](auto Q) {
-        constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
-        raw[t][4 * q] = x.x;
-        raw[t][4 * q + 1] = x.y;
-        raw[t][4 * q + 2] = x.z;
-        raw[t][4 * q + 3] = x.w;
-      });
-    } else {
-      static_for<16>([&](auto P) { raw[t][decltype(P)::value] = 0; });
-    }
-  });
-}
-
-// Planes -> bytes -> lane-linear pieces, stored where the input pieces were read.
-__device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const TileIO& io, uint32_t qmask,
-                                            const uint32_t* planes) {
-  uint32_t v[16];
-  static_for<16>([&](auto P) {
-    constexpr int i = decltype(P)::value;
-    v[i] = planes[i];
-  });
-  dev::transpose8(v);
-  dev::transpose8(v + 8);
-  swap_halves(v);
-  static_for<4>([&](auto Q) {
-    constexpr int q = decltype(Q)::value;
-    if (qmask & (1u << q))
-      *reinterpret_cast<uint4*>(base + io.off[q]) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-  });
-}
-
-// LDS exchange between passes (2 rounds, 4 A-slots per wave per round).
-//   NW = 4: A-slot t of wave w (shard 8w+t) <-> B-slot 2w+(t>>2) of wave t&3
-//   NW = 8: A-slot t of wave w (shard 8w+t) <-> B-slot w of wave t
-template <int NW>
-__device__ __forceinline__ void xf_exchange_ab(int wave, int lane, uint4* lds, Regs8& ra, Regs8& rb) {
-  static_for<2>([&](auto Rho) {
-    constexpr int rho = decltype(Rho)::value;
-    static_for<4>([&](auto U) {
-      constexpr int u = decltype(U)::value;
-      lds_put(lds, 4 * wave + u, lane, ra[4 * rho + u]);
-    });
-    __syncthreads();
-    if constexpr (NW == 4) {
-      static_for<4>([&](auto W2) {
-        constexpr int w2 = decltype(W2)::value;
-        lds_get(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
-      });
-    } else {
-      if ((wave >> 2) == rho) {
-        static_for<8>([&](auto W2) {
-          constexpr int w2 = decltype(W2)::value;
-          lds_get(lds, 4 * w2 + (wave & 3), lane, rb[w2]);
-        });
-      }
-    }
-    __syncthreads();
-  });
-}
-
-template <int NW>
-__device__ __forceinline__ void xf_exchange_bc(int wave, int lane, uint4* lds, Regs8& rb, Regs8& ra) {
-  static_for<2>([&](auto Rho) {
-    constexpr int rho = decltype(Rho)::value;
-    if constexpr (NW == 4) {
-      static_for<4>([&](auto W2) {
-        constexpr int w2 = decltype(W2)::value;
-        lds_put(lds, 4 * w2 + wave, lane, rb[2 * w2 + rho]);
-      });
-    } else {
-      if ((wave >> 2) == rho) {
-        static_for<8>([&](auto W2) {
-          constexpr int w2 = decltype(W2)::value;
-          lds_put(lds, 4 * w2 + (wave & 3), lane, rb[w2]);
-        });
-      }
-    }
-    __syncthreads();
-    static_for<4>([&](auto U) {
-      constexpr int u = decltype(U)::value;
-      lds_get(lds, 4 * wave + u, lane, ra[4 * rho + u]);
-    });
-    __syncthreads();
-  });
-}
-
-// Store predicate of this wave's shard s for the four chunk slices of the tile: chunk
-// exists and, with a mask, bit s of its block's pattern word is set.
-__device__ __forceinline__ uint32_t store_qmask(const TileIO& io, const uint64_t* mask, uint32_t s) {
-  uint32_t qm = io.valid;
-  static_for<4>([&](auto Q) {
-    constexpr int q = decltype(Q)::value;
-    if (!((mask[q] >> s) & 1)) qm &= ~(1u << q);
-  });
-  return qm;
-}
 
 // One 64-chunk tile per workgroup of NW waves.  N = 32: 64 KiB LDS, two workgroups per
 // CU; N = 64: 128 KiB LDS, one workgroup (8 waves) per CU.
@@ -397,190 +110,6 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
   });
 }
 
-// =====================================================================================
-// xform8: the 32-point transform with 8 waves per workgroup and 4 shard slots per lane.
-// Half the per-lane state of xform<4> (16 loads per lane in flight instead of 32, ~half
-// the VGPRs), so two 8-wave workgroups share a CU and each wave has half the arithmetic
-// between its loads and its stores (tools/membench/membench4.hip: 64-column tile copies
-// 5.57 -> 5.74 TB/s at 8 waves; xform<4> runs at its own load/store skeleton's speed).
-// Every position bit is a slot bit (2) or a wave bit (3), so a layer's skew constant
-// depends only on slot bits (compile time) and wave bits (a scalar switch over the wave
-// bits above the layer).  A layer needs its bit in a slot; between layers one slot bit
-// trades places with one wave bit (x8_swap: partner waves swap half their slots through
-// 64 KiB of LDS; the other half stay in place):
-//   L0 slots p0 p1 | waves p2 p3 p4   IFFT b0 b1            (loads, FFT b0, stores)
-//   L1 slots p2 p1 | waves p0 p3 p4   IFFT b2               (FFT b1)
-//   L2 slots p2 p3 | waves p0 p1 p4   IFFT b3               (FFT b2)
-//   L3 slots p4 p3 | waves p0 p1 p2   IFFT b4, FFT b4 b3
-// =====================================================================================
-using Regs4 = uint32_t[4][16];
-
-// Position bits held by slot bits (S0, S1) and wave bits (W0, W1, W2).
-template <int S0, int S1, int W0, int W1, int W2>
-struct X8Lay {
-  static constexpr int sb[2] = {S0, S1};
-  static constexpr int wb[3] = {W0, W1, W2};
-  static constexpr int pos(int w, int t) {
-    return (((t >> 0) & 1) << sb[0]) | (((t >> 1) & 1) << sb[1]) | (((w >> 0) & 1) << wb[0]) |
-           (((w >> 1) & 1) << wb[1]) | (((w >> 2) & 1) << wb[2]);
-  }
-  static constexpr int slot_of(int b) { return sb[0] == b ? 0 : sb[1] == b ? 1 : -1; }
-  // wave bits whose position bit exceeds b (the ones a layer-b constant depends on)
-  static constexpr int rel(int b) { return (wb[0] > b ? 1 : 0) | (wb[1] > b ? 2 : 0) | (wb[2] > b ? 4 : 0); }
-};
-template <int L>
-struct X8LayoutSel;
-template <>
-struct X8LayoutSel<0> { using T = X8Lay<0, 1, 2, 3, 4>; };
-template <>
-struct X8LayoutSel<1> { using T = X8Lay<2, 1, 0, 3, 4>; };
-template <>
-struct X8LayoutSel<2> { using T = X8Lay<2, 3, 0, 1, 4>; };
-template <>
-struct X8LayoutSel<3> { using T = X8Lay<4, 3, 0, 1, 2>; };
-template <int L>
-using X8Layout = typename X8LayoutSel<L>::T;
-
-constexpr int x8_popc(int m) { return (m & 1) + ((m >> 1) & 1) + ((m >> 2) & 1); }
-// wave bits selected by REL packed into the low bits, and back
-template <int REL>
-__device__ __forceinline__ int x8_compress(int w) {
-  int v = 0, k = 0;
-  if constexpr (REL & 1) v |= (w & 1) << k++;
-  if constexpr (REL & 2) v |= ((w >> 1) & 1) << k++;
-  if constexpr (REL & 4) v |= ((w >> 2) & 1) << k++;
-  return v;
-}
-constexpr int x8_expand(int v, int rel) {
-  int w = 0, k = 0;
-  for (int j = 0; j < 3; ++j)
-    if ((rel >> j) & 1) w |= ((v >> k++) & 1) << j;
-  return w;
-}
-
-// The butterfly on slots (T, T | 2^i) of layer bit B in layout Lay for the wave bits V.
-// FFT butterflies with upd_y false skip y ^= x (y's new value is never used).
-template <typename Lay, int B, bool INV, int DELTA, int T, int V>
-__device__ __forceinline__ void x8_bfly(uint32_t* x, uint32_t* y, bool upd_y) {
-  constexpr int w = x8_expand(V, Lay::rel(B));
-  constexpr int S = (Lay::pos(w, T) & ~((2 << B) - 1)) + (1 << B) + DELTA - 1;
-  if constexpr (INV) {
-    dev::ifft_bfly<S>(x, y);
-  } else {
-    if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(x, y);
-    if (upd_y) dev::xor_planes(y, x);
-  }
-}
-template <typename Lay, int B, bool INV, int DELTA, int T>
-__device__ __forceinline__ void x8_bfly_w(int v, uint32_t* x, uint32_t* y, bool upd_y = true) {
-  constexpr int n = 1 << x8_popc(Lay::rel(B));
-  if constexpr (n == 1) {
-    x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y);
-  } else if constexpr (n == 2) {
-    if (v == 0) x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); else x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y);
-  } else if constexpr (n == 4) {
-    switch (v) {
-      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); break;
-      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y); break;
-      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2>(x, y, upd_y); break;
-      default: x8_bfly<Lay, B, INV, DELTA, T, 3>(x, y, upd_y); break;
-    }
-  } else {
-    switch (v) {
-      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); break;
-      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y); break;
-      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2>(x, y, upd_y); break;
-      case 3: x8_bfly<Lay, B, INV, DELTA, T, 3>(x, y, upd_y); break;
-      case 4: x8_bfly<Lay, B, INV, DELTA, T, 4>(x, y, upd_y); break;
-      case 5: x8_bfly<Lay, B, INV, DELTA, T, 5>(x, y, upd_y); break;
-      case 6: x8_bfly<Lay, B, INV, DELTA, T, 6>(x, y, upd_y); break;
-      default: x8_bfly<Lay, B, INV, DELTA, T, 7>(x, y, upd_y); break;
-    }
-  }
-}
-// One butterfly layer on position bit B in layout L (skew delta DELTA).  LIVE: the slots
-// that still carry needed values (half-pruned FFT); UPD_Y false: FFT x updates only.
-template <int L, int B, bool INV, int DELTA, int LIVE = 0xF, bool UPD_Y = true>
-__device__ __forceinline__ void x8_layer(int wave, Regs4& r) {
-  using Lay = X8Layout<L>;
-  constexpr int i = Lay::slot_of(B);
-  static_assert(i >= 0, "layer bit must be a slot bit");
-  const int v = x8_compress<Lay::rel(B)>(wave);
-  constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;  // the slots with bit i clear
-  if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)], UPD_Y);
-  if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)], UPD_Y);
-}
-template <typename Lay, int B, int DELTA, int LIVE>
-__device__ __forceinline__ void x8_layer_lay(int wave, Regs4& r) {
-  constexpr int i = Lay::slot_of(B);
-  static_assert(i >= 0, "layer bit must be a slot bit");
-  const int v = x8_compress<Lay::rel(B)>(wave);
-  constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;
-  if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, false, DELTA, t0>(v, r[t0], r[t0 | (1 << i)]);
-  if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, false, DELTA, t1>(v, r[t1], r[t1 | (1 << i)]);
-}
-
-// Slot bit I <-> wave bit J.  Slot t of wave w moves iff t_I != w_J: to slot t ^ 2^I of
-// wave w ^ 2^J, whose outgoing slots are exactly the incoming ones' registers.
-// The branches for t and t ^ 2^I have complementary conditions; the asm markers keep
-// LLVM from merging them into one access through a phi of register-array pointers
-// (which would send the whole slot array to scratch).
-// AG_X8_PAIRSYNC: partner waves synchronise through LDS epoch flags instead of workgroup
-// barriers (ready[w] = last swap whose data w has written, done[w] = last swap w has read).
-#ifndef AG_X8_PAIRSYNC
-#define AG_X8_PAIRSYNC 1
-#endif
-struct X8Flags {
-  uint32_t ready[8];
-  uint32_t done[8];
-};
-__device__ __forceinline__ void x8_wait_ge(const uint32_t* f, uint32_t e) {
-  while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < e) __builtin_amdgcn_s_sleep(1);
-}
-__device__ __forceinline__ void x8_signal(uint32_t* f, uint32_t e, int lane) {
-  if (lane == 0) __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-template <int I, int J, int EP, int LIVE = 0xF>
-__device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, X8Flags* fl, Regs4& r) {
-  const int wj = (wave >> J) & 1;
-  const int partner = wave ^ (1 << J);
-#if AG_X8_PAIRSYNC
-  // region `partner` was last read by the partner in swap EP - 1
-  if constexpr (EP > 1) x8_wait_ge(&fl->done[partner], EP - 1);
-#endif
-  static_for<4>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    constexpr int k = (t >> (1 - I)) & 1;  // the other slot bit: index within the pair
-    if (((LIVE >> t) & 1) && ((t >> I) & 1) != wj) {
-      lds_put(lds, 2 * partner + k, lane, r[t]);
-      __asm__ volatile("; x8_swap put %0" ::"n"(t));
-    }
-  });
-#if AG_X8_PAIRSYNC
-  x8_signal(&fl->ready[wave], EP, lane);
-  x8_wait_ge(&fl->ready[partner], EP);
-#else
-  __syncthreads();
-#endif
-  static_for<4>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    constexpr int k = (t >> (1 - I)) & 1;
-    if (((LIVE >> t) & 1) && ((t >> I) & 1) != wj) {
-      lds_get(lds, 2 * wave + k, lane, r[t]);
-      __asm__ volatile("; x8_swap get %0" ::"n"(t));
-    }
-  });
-#if AG_X8_PAIRSYNC
-  x8_signal(&fl->done[wave], EP, lane);
-#else
-  __syncthreads();
-#endif
-}
-
-#ifndef AG_X8_WAVES_PER_EU
-#define AG_X8_WAVES_PER_EU 4
-#endif
 // HALF: every stored output has position bit 4 clear (a decode whose erased originals all
 // lie in shards 0..15).  After FFT layer 4 only the x halves are needed (no y update),
 // and the remaining 16-point FFT runs on the two live slots per wave (slot bit 0 = p4 = 0)

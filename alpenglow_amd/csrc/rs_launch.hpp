@@ -71,6 +71,43 @@ struct DecodeSynParams {
 };
 hipError_t launch_decode_syn(unsigned chunk, const DecodeSynParams& p, hipStream_t stream);
 
+// Correction decoder (decode_c_kernel, rs_decode_c.hip) for the 32-point full-window
+// geometries (HighRate, m = 32, k <= 32) with lost recovery shards, any k survivors:
+//   d = X r is the full-recovery transform (X = FFT_32 o IFFT_0, the inverse of the 32:32
+//   encoder; original-coset points k..31 are virtual zeros).  With the lost recovery shards
+//   L read as zero, X r' differs from d by X[:, L] g, g = the lost values.  At |L| known
+//   original-coset points (present originals or virtual zeros) the syndromes
+//   s = d - X r' give g = N^-1 s (N = X[Dsel, L]), so the erased originals are
+//   d_E = (X r')_E + K s with K = X[E, L] N^-1 (|E| x |L| runtime multiplies).
+constexpr int kCorrMaxSyn = 16;    // |L| <= 16 (syndrome planes staged in 64 KiB of LDS)
+constexpr int kCorrMaxPairs = 256;  // |E| * |L| <= 256 (|E| + |L| <= 32)
+struct CorrPattern {
+  uint64_t rmask;  // recovery shards present (loaded); lost ones read as zero
+  uint64_t emask;  // originals restored (E)
+  uint64_t smask;  // original-coset points used as syndromes: present originals (< k) or virtual zeros
+  uint32_t ne, ns;  // |E|, |L| = number of syndromes
+  // K[a][b] (a < ne, b < ns) at dwords 8 * (a * ns + b): 16 rows of 16 bits, two rows per
+  // dword (row 2q in bits 0..15, row 2q+1 in bits 16..31); row o bit i = bit o of K * 2^i
+  uint32_t kmat[kCorrMaxPairs * 8];
+};
+struct DecodeCParams {
+  const uint8_t* rec;
+  uint64_t rec_block_stride;
+  uint64_t rec_shard_stride;
+  uint8_t* orig;  // present originals are read (syndromes), restored ones written here
+  uint64_t orig_block_stride;
+  uint64_t orig_shard_stride;
+  const CorrPattern* pat;     // [pattern]
+  const uint32_t* block_ids;  // per_block: blocks processed (null = 0..)
+  uint32_t per_block;         // 1: pattern = block; tiles_per_block 64-column tiles per block
+  uint32_t tiles_per_block;
+  uint32_t k;
+  uint32_t chunks_per_shard;
+  uint64_t total_columns;  // batch blocks * chunks_per_shard
+  uint64_t ntiles;         // 64-column tiles processed
+};
+hipError_t launch_decode_c(const DecodeCParams& p, hipStream_t stream);
+
 struct GfDeviceTables {
   const uint16_t* exp;
   const uint16_t* log;

@@ -264,6 +264,52 @@ def test_general_decode_per_block_patterns(ctx, dev, k, m, S, n):
         assert np.array_equal(got, blocks), mode
 
 
+@pytest.mark.parametrize("k,S,n,ne,nl", [(32, 4096, 5, 16, 4), (32, 1024, 7, 16, 16), (32, 64, 70, 31, 1),
+                                         (32, 8192, 3, 1, 16), (25, 2048, 4, 10, 7), (17, 64, 65, 5, 15),
+                                         (32, 32768, 2, 16, 8), (20, 4096, 3, 20, 12), (32, 4096, 3, 4, 20),
+                                         (32, 128, 33, 12, 13)])
+def test_correction_decode_one_pattern(ctx, dev, k, S, n, ne, nl):
+    """decode_c (32-point transform + K s correction) for k <= 32, m = 32 with ne erased
+    originals and nl lost recovery shards; nl > 16 falls back to decode_x.  ANY_K: the
+    restored originals must equal the encoded ones."""
+    m = 32
+    rng = random.Random(k * 7919 + S + ne * 31 + nl)
+    blocks = np.stack([np.frombuffer(o.block_bytes(900 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    lost, lost_r = rng.sample(range(k), ne), rng.sample(range(m), nl)
+    damaged = blocks.copy()
+    damaged[:, lost] = 0x5A
+    rec_d = rec.copy()
+    rec_d[:, lost_r] = 0xA5  # lost recovery shards must not be read
+    op = [0 if i in lost else 1 for i in range(k)]
+    rp = [0 if j in lost_r else 1 for j in range(m)]
+    got = gpu_decode(ctx, dev, damaged, rec_d, op, rp, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
+
+
+@pytest.mark.parametrize("S,n", [(4096, 24), (8192, 9)])
+def test_correction_decode_per_block_patterns(ctx, dev, S, n):
+    """A random pattern per block across the 32:32 decoders: full recovery set (transform),
+    1..16 lost recovery shards (decode_c), more (decode_x), nothing erased; then a second
+    pattern set through the same context (pattern cache)."""
+    k = m = 32
+    blocks = np.stack([np.frombuffer(o.block_bytes(1300 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    for seed in (1, 2):
+        rng = random.Random(S + n + seed)
+        op, rp, damaged, rec_d = [], [], blocks.copy(), rec.copy()
+        for b in range(n):
+            nl = rng.choice([0, 1, 2, 4, 8, 15, 16, 17, 24])
+            ne = rng.randrange(0, m - nl + 1)
+            lost, lost_r = rng.sample(range(k), min(ne, k)), rng.sample(range(m), nl)
+            damaged[b, lost] = 0x77
+            rec_d[b, lost_r] = 0x11
+            op += [0 if i in lost else 1 for i in range(k)]
+            rp += [0 if j in lost_r else 1 for j in range(m)]
+        got = gpu_decode(ctx, dev, damaged, rec_d, op, rp, rs.DECODE_ANY_K)
+        assert np.array_equal(got, blocks), seed
+
+
 @pytest.mark.parametrize("k,m,S,n", [(16, 4, 4096, 6), (16, 3, 640, 5), (13, 4, 128, 7), (64, 4, 1024, 3),
                                      (5, 2, 64, 9), (9, 1, 192, 4), (17, 2, 4096, 3), (16, 4, 64, 33)])
 def test_syndrome_decode_one_pattern(ctx, dev, k, m, S, n):
