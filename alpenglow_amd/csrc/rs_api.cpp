@@ -113,7 +113,7 @@ struct ag_rs_ctx {
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
-  DevBuf d_corr, d_corrblocks;              // correction decoder: patterns, block ids
+  DevBuf d_corr, d_corrk, d_corrblocks;     // correction decoder: patterns, K picks, block ids
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
   DevBuf d_merkle_nodes;                    // Merkle node scratch (callers without a nodes buffer)
   DevBuf d_aon_lens, d_aon_digests, d_aon_keys;  // all-or-nothing transforms
@@ -200,7 +200,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_corr, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
                       &one_out})
       b->release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
@@ -310,11 +310,12 @@ const uint16_t* full_window_x32() {
 // shards L (1 <= |L| <= kCorrMaxSyn).  Syndrome points: virtual zeros k..31 first (no
 // load), then present originals in index order.  False if the pattern does not fit (the
 // caller takes another decoder).
-bool build_corr_pattern(size_t k, const uint8_t* opres, const uint8_t* rpres, ag::CorrPattern* cp) {
+bool build_corr_pattern(size_t k, const uint8_t* opres, const uint8_t* rpres, ag::CorrPattern* cp,
+                        std::vector<uint32_t>& pool) {
   const uint16_t* X = full_window_x32();
   if (!X || k > 32) return false;
   const ag::Gf16Tables& t = ag::gf16_tables();
-  std::memset(cp, 0, offsetof(ag::CorrPattern, kmat));
+  std::memset(cp, 0, sizeof *cp);
   uint8_t E[32], L[32], D[32];
   size_t ne = 0, nl = 0, nd = 0;
   for (size_t j = 0; j < 32; ++j) {
@@ -347,18 +348,24 @@ bool build_corr_pattern(size_t k, const uint8_t* opres, const uint8_t* rpres, ag
       for (size_t c = 0; c < nl; ++c) acc ^= ag::gf_mul_elem(t, X[E[a] * 32 + L[c]], N[c * nl + b]);
       K[a * nl + b] = acc;
     }
-  // bitsliced rows, two per dword
-  std::memset(cp->kmat, 0, ne * nl * 8 * sizeof(uint32_t));
+  // table picks: per pair, group pair gp and output plane o, the two nibbles of row o
+  // (input planes 8gp..8gp+3, 8gp+4..8gp+7); row o bit i = bit o of K * 2^i
+  cp->kofs = pool.size();
+  pool.resize(pool.size() + ne * nl * ag::kCorrPairWords);
+  uint32_t* dst = pool.data() + cp->kofs;
   for (size_t a = 0; a < ne; ++a)
-    for (size_t b = 0; b < nl; ++b) {
+    for (size_t b = 0; b < nl; ++b, dst += ag::kCorrPairWords) {
       uint32_t rows[16] = {};
       const uint16_t v = K[a * nl + b];
       for (unsigned i = 0; i < 16; ++i) {
         const uint16_t prod = ag::gf_mul_elem(t, v, static_cast<uint16_t>(1u << i));
         for (unsigned o = 0; o < 16; ++o) rows[o] |= ((prod >> o) & 1u) << i;
       }
-      uint32_t* dst = cp->kmat + 8 * (a * nl + b);
-      for (unsigned q = 0; q < 8; ++q) dst[q] = rows[2 * q] | (rows[2 * q + 1] << 16);
+      for (unsigned gp = 0; gp < 2; ++gp)
+        for (unsigned o = 0; o < 16; ++o) {
+          dst[32 * gp + 2 * o] = (rows[o] >> (8 * gp)) & 15u;
+          dst[32 * gp + 2 * o + 1] = (rows[o] >> (8 * gp + 4)) & 15u;
+        }
     }
   return true;
 }
@@ -610,7 +617,8 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   // decode_c: the 32-point full-window geometries (HighRate, m = 32, k <= 32) with lost
   // recovery shards; any k survivors, same tiling rule
   const bool corr_geo = mode == AG_RS_DECODE_ANY_K && hr == 1 && m == 32 && k <= 32 && S % 64 == 0 && aligned &&
-                        (npat == 1 || cps % 64 == 0) && corr_enabled();
+                        (npat == 1 || cps % 64 == 0) && static_cast<uint64_t>(nblocks) * cps < (uint64_t{1} << 31) &&
+                        corr_enabled();
   bool any_fast = false, any_generic = false, any_x = false, any_syn = false, any_corr = false;
   for (size_t p = 0; p < npat; ++p) {
     const size_t no = count_flags(opres + p * k, k), nr = count_flags(rpres + p * m, m);
@@ -770,18 +778,21 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     }
     if (key != c->corr_key) {
       std::vector<ag::CorrPattern> corr(npat);
+      std::vector<uint32_t> pool;
       for (size_t p = 0; p < npat; ++p) {
         if (cls[p] != 6) {
-          std::memset(&corr[p], 0, offsetof(ag::CorrPattern, kmat));
+          std::memset(&corr[p], 0, sizeof corr[p]);
           continue;
         }
         // corr_fits admitted the pattern; the MDS property makes N invertible
-        if (!build_corr_pattern(k, opres + p * k, rpres + p * m, &corr[p])) return AG_RS_ERR_DEVICE;
+        if (!build_corr_pattern(k, opres + p * k, rpres + p * m, &corr[p], pool)) return AG_RS_ERR_DEVICE;
       }
       c->corr_key.clear();
       AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read d_corr
       if ((st = c->d_corr.ensure(npat * sizeof(ag::CorrPattern), c->stream))) return st;
+      if ((st = c->d_corrk.ensure(std::max<size_t>(pool.size(), 1) * 4, c->stream))) return st;
       AG_HIP(hipMemcpy(c->d_corr.ptr, corr.data(), npat * sizeof(ag::CorrPattern), hipMemcpyHostToDevice));
+      if (!pool.empty()) AG_HIP(hipMemcpy(c->d_corrk.ptr, pool.data(), pool.size() * 4, hipMemcpyHostToDevice));
       c->corr_key = key;
     }
     ag::DecodeCParams p{};
@@ -792,6 +803,7 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     p.orig_block_stride = ostride;
     p.orig_shard_stride = S;
     p.pat = c->d_corr.as<ag::CorrPattern>();
+    p.kpool = c->d_corrk.as<uint32_t>();
     p.k = static_cast<uint32_t>(k);
     p.chunks_per_shard = static_cast<uint32_t>(cps);
     p.total_columns = static_cast<uint64_t>(nblocks) * cps;

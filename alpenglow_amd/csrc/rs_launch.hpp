@@ -81,15 +81,18 @@ hipError_t launch_decode_syn(unsigned chunk, const DecodeSynParams& p, hipStream
 //   d_E = (X r')_E + K s with K = X[E, L] N^-1 (|E| x |L| runtime multiplies).
 constexpr int kCorrMaxSyn = 16;    // |L| <= 16 (syndrome planes staged in 64 KiB of LDS)
 constexpr int kCorrMaxPairs = 256;  // |E| * |L| <= 256 (|E| + |L| <= 32)
+constexpr int kCorrPairWords = 64;  // table picks per (a, b) pair
 struct CorrPattern {
   uint64_t rmask;  // recovery shards present (loaded); lost ones read as zero
   uint64_t emask;  // originals restored (E)
   uint64_t smask;  // original-coset points used as syndromes: present originals (< k) or virtual zeros
   uint32_t ne, ns;  // |E|, |L| = number of syndromes
-  // K[a][b] (a < ne, b < ns) at dwords 8 * (a * ns + b): 16 rows of 16 bits, two rows per
-  // dword (row 2q in bits 0..15, row 2q+1 in bits 16..31); row o bit i = bit o of K * 2^i
-  uint32_t kmat[kCorrMaxPairs * 8];
+  uint64_t kofs;    // K picks at kpool + kofs, pair (a, b) (a < ne, b < ns) at + 64 * (a * ns + b)
 };
+// K[a][b] as table picks: for group pair gp (input planes 8gp..8gp+7) and output plane o,
+// dwords [32 gp + 2 o] and [32 gp + 2 o + 1] are the 4-bit indices (row o of K[a][b]'s
+// 16x16 GF(2) matrix, input planes 8gp..8gp+3 and 8gp+4..8gp+7; row o bit i = bit o of
+// K * 2^i) into the two 16-entry XOR tables of the syndrome's planes.
 struct DecodeCParams {
   const uint8_t* rec;
   uint64_t rec_block_stride;
@@ -98,6 +101,7 @@ struct DecodeCParams {
   uint64_t orig_block_stride;
   uint64_t orig_shard_stride;
   const CorrPattern* pat;     // [pattern]
+  const uint32_t* kpool;      // table picks of every pattern
   const uint32_t* block_ids;  // per_block: blocks processed (null = 0..)
   uint32_t per_block;         // 1: pattern = block; tiles_per_block 64-column tiles per block
   uint32_t tiles_per_block;
