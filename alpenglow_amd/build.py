@@ -27,8 +27,8 @@ ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else "hipcc")
 CXX = os.environ.get("CXX_HOST", "g++")
 
-SOURCES = ["rs_kernels.hip", "rs_decode_c.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hip", "slice.hip", "rs_api.cpp", "gf16.cpp"]
-HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_xform.hpp", "rs_launch.hpp", "rs_consts.inc", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp", "slice.hpp"]
+SOURCES = ["rs_kernels.hip", "rs_decode_c.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hip", "slice.hip", "shredder.hip", "rs_api.cpp", "gf16.cpp"]
+HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_xform.hpp", "rs_launch.hpp", "rs_consts.inc", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp", "slice.hpp", "shredder.hpp"]
 # -fno-slp-vectorize: the SLP vectoriser packs the bitsliced XOR networks into <2 x i32>
 # ops, which lengthens live ranges (measured +40 VGPRs on the transform kernel).
 # -amdgpu-promote-alloca-to-vector-limit: keeps the four-Russians tables of decode_x and

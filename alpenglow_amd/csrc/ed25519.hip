@@ -84,9 +84,10 @@ __global__ __launch_bounds__(256) void shred_commit_kernel(const ShredCommitPara
   for (int i = 0; i < 32; ++i) c[17 + i] = p.roots[32 * t + i];
   uint8_t* out = p.commitments + kSliceCommitmentLen * t;
   for (uint32_t i = 0; i < kSliceCommitmentLen; ++i) out[i] = c[i];
-  const bool cached = p.cached && p.has_cached && p.has_cached[t];
+  const uint64_t ci = p.cached_group > 1 ? t / p.cached_group : t;
+  const bool cached = p.cached && p.has_cached && p.has_cached[ci];
   if (cached) {
-    const uint8_t* cc = p.cached + kSliceCommitmentLen * t;
+    const uint8_t* cc = p.cached + kSliceCommitmentLen * ci;
     uint32_t diff = 0;
     for (uint32_t i = 0; i < kSliceCommitmentLen; ++i) diff |= c[i] ^ cc[i];
     if (diff == 0) {  // validated_shred.rs:62-64: same commitment, no signature check

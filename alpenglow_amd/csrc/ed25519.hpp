@@ -75,6 +75,7 @@ struct ShredCommitParams {
   const uint8_t* roots;            // 32 B per shred
   const uint8_t* cached;           // 49 B per shred (nullable)
   const uint8_t* has_cached;       // per shred (nullable: no cache)
+  uint32_t cached_group;           // > 1: cached / has_cached entry t / cached_group (one per slice)
   uint64_t n;
   uint8_t* commitments;            // 49 B per shred (out)
   uint8_t* status;                 // out

@@ -27,6 +27,7 @@
 #include "wire.hpp"
 #include "merkle.hpp"
 #include "rs_launch.hpp"
+#include "shredder.hpp"
 
 using ag::next_pow2;
 
@@ -121,6 +122,8 @@ struct ag_rs_ctx {
   DevBuf stage_pad, stage_mask;                  // restrided shards (sizes not whole 64-byte chunks)
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
+  static constexpr int kPipeBufs = 24;
+  DevBuf pipe[kPipeBufs];                   // composed shredder scratch (ag_shredder_*_batch)
   DevBuf d_sh_roots, d_sh_commit, d_sh_onvalid, d_sh_list;  // shred validation scratch
   DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
   // host-memory calls: two staging slots, H2D / D2H streams next to the compute stream
@@ -203,6 +206,7 @@ struct ag_rs_ctx {
                       &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
                       &one_out})
       b->release();
+    for (DevBuf& b : pipe) b.release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -1815,6 +1819,12 @@ int ensure_ed_base(ag_rs_ctx* c) {
   return ag::launch_ed25519_init(c->d_ed_base.as<int32_t>(), c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
 }
 constexpr size_t kMaxSigBatch = size_t{1} << 31;
+int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data_stride, size_t data_bytes,
+                        const uint32_t* shred_index, const uint8_t* proofs, size_t proofs_stride, size_t height,
+                        const uint64_t* slots, const uint64_t* slice_indices, const uint8_t* is_last,
+                        const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
+                        const uint8_t* has_cached, uint32_t cached_group, uint8_t* status, uint8_t* roots_out,
+                        uint8_t* commitments_out);
 }  // namespace
 
 int ag_ed25519_public_key_batch(ag_rs_ctx* c, size_t n, const uint8_t* seeds, uint8_t* pks) {
@@ -1881,6 +1891,23 @@ int ag_shred_validate_batch(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t 
                             const uint64_t* slots, const uint64_t* slice_indices, const uint8_t* is_last,
                             const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
                             const uint8_t* has_cached, uint8_t* status, uint8_t* roots_out, uint8_t* commitments_out) {
+  return shred_validate_impl(c, n, data, data_stride, data_bytes, shred_index, proofs, proofs_stride, height, slots,
+                             slice_indices, is_last, sigs, sig_stride, pk, cached, has_cached, 1, status, roots_out,
+                             commitments_out);
+}
+
+}  // extern "C"
+
+namespace {
+
+// ag_shred_validate_batch with the cache entries shared by cached_group consecutive shreds
+// (the composed deshred: one cached commitment per slice).
+int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data_stride, size_t data_bytes,
+                        const uint32_t* shred_index, const uint8_t* proofs, size_t proofs_stride, size_t height,
+                        const uint64_t* slots, const uint64_t* slice_indices, const uint8_t* is_last,
+                        const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
+                        const uint8_t* has_cached, uint32_t cached_group, uint8_t* status, uint8_t* roots_out,
+                        uint8_t* commitments_out) {
   if (!c || n >= kMaxSigBatch || data_bytes >= (size_t{1} << 28) ||
       height > static_cast<size_t>(ag::kMerkleMaxHeight) ||
       (n && (!shred_index || !slots || !slice_indices || !is_last || !sigs || !pk || !status ||
@@ -1926,6 +1953,7 @@ int ag_shred_validate_batch(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t 
   cp.roots = roots;
   cp.cached = cached;
   cp.has_cached = has_cached;
+  cp.cached_group = cached_group;
   cp.n = n;
   cp.commitments = commits;
   cp.status = status;
@@ -1950,6 +1978,10 @@ int ag_shred_validate_batch(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t 
   vp.base_table = c->d_ed_base.as<int32_t>();
   return ag::launch_ed25519_verify(vp, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
 }
+
+}  // namespace
+
+extern "C" {
 
 int ag_slice_sign_batch(ag_rs_ctx* c, size_t nslices, const uint8_t* seed, const uint8_t* pk, const uint64_t* slots,
                         const uint64_t* slice_indices, const uint8_t* is_last, const uint8_t* roots, uint8_t* sigs,
@@ -2132,6 +2164,271 @@ int ag_slice_parse_batch(ag_rs_ctx* c, size_t nslices, const uint8_t* codewords,
   std::memcpy(parent_ids, out.data() + (o_id - o_st), AG_SLICE_BLOCK_ID_BYTES * nslices);
   std::memcpy(data_offsets, out.data() + (o_off - o_st), 4 * nslices);
   std::memcpy(data_lens, out.data() + (o_len - o_st), 4 * nslices);
+  return AG_RS_OK;
+}
+
+}  // extern "C"
+
+// =====================================================================================
+// Composed Shredder (RegularShredder): ag_shredder_shred_batch / ag_shredder_deshred_batch
+// =====================================================================================
+namespace {
+
+constexpr size_t kPipeProofBytes = 32 * ag::kPipeHeight;  // one Merkle path of a slice tree
+
+int pipe_buf(ag_rs_ctx* c, int i, size_t bytes, uint8_t** out) {
+  const int st = c->pipe[i].ensure(std::max<size_t>(bytes, 64), c->stream);
+  if (st) return st;
+  *out = c->pipe[i].as<uint8_t>();
+  return AG_RS_OK;
+}
+
+bool pipe_args_ok(size_t nslices, size_t S, const uint8_t* codewords, const uint8_t* packets,
+                  const uint32_t* packet_lens) {
+  return S != 0 && S % 2 == 0 && S <= 1024 && nslices < (size_t{1} << 24) &&
+         (nslices == 0 || (codewords && packets && packet_lens)) && reinterpret_cast<uintptr_t>(codewords) % 16 == 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ag_shredder_shred_batch(ag_rs_ctx* c, size_t nslices, size_t S, const uint8_t* parent_flags,
+                            const uint8_t* parent_ids, const uint8_t* data, size_t data_stride,
+                            const uint32_t* data_lens, const uint64_t* slots, const uint64_t* slice_indices,
+                            const uint8_t* is_last, const uint8_t* seed, const uint8_t* pk, uint8_t* codewords,
+                            uint8_t* roots_out, uint8_t* sigs_out, uint8_t* packets, size_t packet_stride,
+                            uint32_t* packet_lens) {
+  if (!c || !pipe_args_ok(nslices, S, codewords, packets, packet_lens) ||
+      (nslices && (!parent_flags || !parent_ids || !data_lens || !slots || !slice_indices || !is_last || !seed ||
+                   !pk)))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (nslices == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  const size_t n = nslices, N = n * ag::kPipeShreds, cw_stride = ag::kPipeShreds * S;
+  // 1. Slice::payload_bytes into the data regions, 2. ReedSolomonCoder::shred in place
+  std::vector<uint32_t> lens(n);
+  int st = ag_slice_frame_batch(c, n, S, parent_flags, parent_ids, data, data_stride, data_lens, codewords, cw_stride,
+                                lens.data());
+  if (st) return st;
+  if ((st = ag_rs_coder_shred_batch(c, ag::kPipeShreds - ag::kPipeData, n, S, nullptr, 0, lens.data(), codewords,
+                                    cw_stride)))
+    return st;
+  // 3. slice Merkle trees: roots and every shred's path
+  uint8_t *roots = roots_out, *sigs = sigs_out, *proofs, *kind, *sidx, *dlen, *height;
+  if (!roots && (st = pipe_buf(c, 0, 32 * n, &roots))) return st;
+  if (!sigs && (st = pipe_buf(c, 1, 64 * n, &sigs))) return st;
+  if ((st = pipe_buf(c, 2, kPipeProofBytes * N, &proofs)) || (st = pipe_buf(c, 3, N, &kind)) ||
+      (st = pipe_buf(c, 4, 4 * N, &sidx)) || (st = pipe_buf(c, 5, 4 * N, &dlen)) ||
+      (st = pipe_buf(c, 6, 4 * N, &height)))
+    return st;
+  if ((st = ag_merkle_build_batch(c, ag::kPipeShreds, S, n, codewords, S, cw_stride, roots, nullptr, 0, proofs,
+                                  ag::kPipeShreds * kPipeProofBytes)))
+    return st;
+  // 4. slice_sig = sign(SliceCommitment(header, root))
+  if ((st = ag_slice_sign_batch(c, n, seed, pk, slots, slice_indices, is_last, roots, sigs, nullptr))) return st;
+  // 5. the 64 datagrams per slice (header and signature shared by the slice's rows)
+  ag::PipeExpandParams ep{};
+  ep.nslices = n;
+  ep.shred_bytes = static_cast<uint32_t>(S);
+  ep.kind = kind;
+  ep.shred_index = reinterpret_cast<uint32_t*>(sidx);
+  ep.data_len = reinterpret_cast<uint32_t*>(dlen);
+  ep.height = reinterpret_cast<uint32_t*>(height);
+  if (ag::launch_pipe_expand(ep, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  ag::ShredColumns cols{};
+  cols.kind = kind;
+  cols.slot = const_cast<uint64_t*>(slots);
+  cols.slice_index = const_cast<uint64_t*>(slice_indices);
+  cols.is_last = const_cast<uint8_t*>(is_last);
+  cols.shred_index = ep.shred_index;
+  cols.data = codewords;
+  cols.data_stride = S;
+  cols.data_len = ep.data_len;
+  cols.sig = sigs;
+  cols.proof = proofs;
+  cols.proof_stride = kPipeProofBytes;
+  cols.height = ep.height;
+  cols.hdr_group = ag::kPipeShreds;
+  if (ag::launch_shred_serialize(cols, N, packets, packet_stride, packet_lens, c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  return AG_RS_OK;
+}
+
+int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* packets, size_t packet_stride,
+                              uint32_t* packet_lens, const uint8_t* pk, uint8_t* codewords, int32_t* status,
+                              uint64_t* slots_out, uint64_t* slice_indices_out, uint8_t* is_last_out,
+                              uint8_t* parent_flags_out, uint8_t* parent_ids_out, uint32_t* data_offsets_out,
+                              uint32_t* data_lens_out) {
+  if (!c || !pipe_args_ok(nslices, S, codewords, packets, packet_lens) ||
+      (nslices && (!pk || !status || !slots_out || !slice_indices_out || !is_last_out || !parent_flags_out ||
+                   !parent_ids_out || !data_offsets_out || !data_lens_out)))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (nslices == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  const size_t n = nslices, N = n * ag::kPipeShreds, cw_stride = ag::kPipeShreds * S;
+  int st;
+  // per-shred columns (payload rows straight into the codewords: row 64 s + j is shard j of slice s)
+  uint8_t *kind, *slot, *sidx, *last, *shidx, *dlen, *sig, *proof, *height, *wire, *vstat, *roots;
+  if ((st = pipe_buf(c, 0, N, &kind)) || (st = pipe_buf(c, 1, 8 * N, &slot)) || (st = pipe_buf(c, 2, 8 * N, &sidx)) ||
+      (st = pipe_buf(c, 3, N, &last)) || (st = pipe_buf(c, 4, 4 * N, &shidx)) || (st = pipe_buf(c, 5, 4 * N, &dlen)) ||
+      (st = pipe_buf(c, 6, 64 * N, &sig)) || (st = pipe_buf(c, 7, kPipeProofBytes * N, &proof)) ||
+      (st = pipe_buf(c, 8, 4 * N, &height)) || (st = pipe_buf(c, 9, N, &wire)) || (st = pipe_buf(c, 10, N, &vstat)) ||
+      (st = pipe_buf(c, 11, 32 * N, &roots)))
+    return st;
+  ag::ShredColumns cols{};
+  cols.kind = kind;
+  cols.slot = reinterpret_cast<uint64_t*>(slot);
+  cols.slice_index = reinterpret_cast<uint64_t*>(sidx);
+  cols.is_last = last;
+  cols.shred_index = reinterpret_cast<uint32_t*>(shidx);
+  cols.data = codewords;
+  cols.data_stride = S;
+  cols.data_len = reinterpret_cast<uint32_t*>(dlen);
+  cols.sig = sig;
+  cols.proof = proof;
+  cols.proof_stride = kPipeProofBytes;
+  cols.height = reinterpret_cast<uint32_t*>(height);
+  // 1. network::deserialize (absent slots have length 0: malformed, never written)
+  if (ag::launch_shred_deserialize(packets, packet_stride, packet_lens, N, cols, wire, c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  // 2. ValidatedShred::try_new: one signature per slice (its first plausible shred) ...
+  uint8_t *pick, *gdata, *gproof, *gslot, *gsidx, *glast, *gidx, *gsig, *pstat, *commits, *hasc;
+  if ((st = pipe_buf(c, 12, n, &pick)) || (st = pipe_buf(c, 13, n * S, &gdata)) ||
+      (st = pipe_buf(c, 14, kPipeProofBytes * n, &gproof)) || (st = pipe_buf(c, 15, 8 * n, &gslot)) ||
+      (st = pipe_buf(c, 16, 8 * n, &gsidx)) || (st = pipe_buf(c, 17, n, &glast)) || (st = pipe_buf(c, 18, 4 * n, &gidx)) ||
+      (st = pipe_buf(c, 19, 64 * n, &gsig)) || (st = pipe_buf(c, 20, n, &pstat)) ||
+      (st = pipe_buf(c, 21, ag::kSliceCommitmentLen * n, &commits)) || (st = pipe_buf(c, 22, n, &hasc)))
+    return st;
+  ag::PipePickParams pp{};
+  pp.nslices = n;
+  pp.shred_bytes = static_cast<uint32_t>(S);
+  pp.wire_status = wire;
+  pp.cols = cols;
+  pp.pick = pick;
+  pp.g_data = gdata;
+  pp.g_proof = gproof;
+  pp.g_slot = reinterpret_cast<uint64_t*>(gslot);
+  pp.g_slice_index = reinterpret_cast<uint64_t*>(gsidx);
+  pp.g_is_last = glast;
+  pp.g_shred_index = reinterpret_cast<uint32_t*>(gidx);
+  pp.g_sig = gsig;
+  AG_HIP(hipMemsetAsync(gdata, 0, n * S, c->stream));  // slices without a pick: defined bytes
+  AG_HIP(hipMemsetAsync(gidx, 0, 4 * n, c->stream));
+  if (ag::launch_pipe_pick(pp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  if ((st = shred_validate_impl(c, n, gdata, S, S, pp.g_shred_index, gproof, kPipeProofBytes, ag::kPipeHeight,
+                                pp.g_slot, pp.g_slice_index, glast, gsig, 64, pk, nullptr, nullptr, 1, pstat, nullptr,
+                                commits)))
+    return st;
+  if (ag::launch_pipe_cache_flags(pick, pstat, n, hasc, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  // ... then every shred against its slice's commitment (signature only without a cache)
+  if ((st = shred_validate_impl(c, N, codewords, S, S, cols.shred_index, proof, kPipeProofBytes, ag::kPipeHeight,
+                                cols.slot, cols.slice_index, last, sig, 64, pk, commits, hasc, ag::kPipeShreds, vstat,
+                                roots, nullptr)))
+    return st;
+  // 3. per slice: the shreds kept, the root, header and signature
+  uint8_t* per_slice;
+  if ((st = pipe_buf(c, 23, (8 + 8 + 8 + 32 + 32 + 64 + 8) * n, &per_slice))) return st;
+  // 32-byte rows first: the Merkle build wants 16-byte aligned roots
+  uint8_t* sroot = per_slice;
+  uint8_t* roots2 = sroot + 32 * n;
+  uint8_t* ssig = roots2 + 32 * n;
+  uint64_t* d_present = reinterpret_cast<uint64_t*>(ssig + 64 * n);
+  uint64_t* d_slot = d_present + n;
+  uint8_t* ssidx = reinterpret_cast<uint8_t*>(d_slot + n);
+  uint8_t* slast = ssidx + 8 * n;
+  std::vector<uint64_t> h_present(n), h_slot(n), h_sidx(n);
+  ag::PipeCheckParams kp{};
+  kp.nslices = n;
+  kp.shred_bytes = static_cast<uint32_t>(S);
+  kp.wire_status = wire;
+  kp.val_status = vstat;
+  kp.roots = roots;
+  kp.cols = cols;
+  kp.present = d_present;
+  kp.root = sroot;
+  kp.slot = d_slot;
+  kp.slice_index = reinterpret_cast<uint64_t*>(ssidx);
+  kp.is_last = slast;
+  kp.sig = ssig;
+  if (ag::launch_pipe_check(kp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  std::vector<uint8_t> h_last(n);
+  AG_HIP(hipMemcpyAsync(h_present.data(), d_present, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipMemcpyAsync(h_slot.data(), d_slot, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipMemcpyAsync(h_sidx.data(), ssidx, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipMemcpyAsync(h_last.data(), slast, n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipStreamSynchronize(c->stream));
+  // 4. ReedSolomonCoder::deshred over the kept shreds (restores the data shreds, re-encodes
+  //    all coding shreds, strips the padding)
+  std::vector<uint8_t> dp(n * ag::kPipeData), cp(n * (ag::kPipeShreds - ag::kPipeData));
+  for (size_t s = 0; s < n; ++s)
+    for (uint32_t j = 0; j < ag::kPipeShreds; ++j) {
+      const uint8_t bit = static_cast<uint8_t>((h_present[s] >> j) & 1);
+      if (j < ag::kPipeData) dp[s * ag::kPipeData + j] = bit;
+      else cp[s * (ag::kPipeShreds - ag::kPipeData) + j - ag::kPipeData] = bit;
+    }
+  std::vector<int64_t> plen(n);
+  if ((st = ag_rs_coder_deshred_batch(c, ag::kPipeShreds - ag::kPipeData, n, S, codewords, cw_stride, dp.data(),
+                                      cp.data(), AG_RS_DECODE_ANY_K, plen.data())))
+    return st;
+  // 5. check_merkle_tree: the rebuilt tree's root must be the signed one; its paths serve
+  //    the reconstructed datagrams
+  if ((st = ag_merkle_build_batch(c, ag::kPipeShreds, S, n, codewords, S, cw_stride, roots2, nullptr, 0, proof,
+                                  ag::kPipeShreds * kPipeProofBytes)))
+    return st;
+  uint8_t* same = pstat;  // first validation's statuses are dead
+  if (ag::launch_pipe_root_cmp(roots2, sroot, n, same, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  std::vector<uint8_t> h_same(n);
+  AG_HIP(hipMemcpyAsync(h_same.data(), same, n, hipMemcpyDeviceToHost, c->stream));
+  // 6. SlicePayload::try_from
+  std::vector<uint8_t> sstat(n);
+  if ((st = ag_slice_parse_batch(c, n, codewords, cw_stride, plen.data(), sstat.data(), parent_flags_out,
+                                 parent_ids_out, data_offsets_out, data_lens_out)))
+    return st;  // synchronous: h_same has landed
+  std::vector<uint8_t> ok(n);
+  for (size_t s = 0; s < n; ++s) {
+    int32_t r = AG_RS_OK;
+    if (plen[s] < 0) {
+      r = -plen[s] == AG_RS_ERR_INVALID_PADDING ? AG_RS_ERR_BAD_ENCODING : static_cast<int32_t>(-plen[s]);
+    } else if (!h_same[s]) {
+      r = AG_RS_ERR_INVALID_MERKLE_TREE;
+    } else if (sstat[s] == AG_SLICE_TOO_LARGE) {
+      r = AG_RS_ERR_TOO_MUCH_DATA;
+    } else if (sstat[s] != AG_SLICE_OK) {
+      r = AG_RS_ERR_BAD_ENCODING;
+    }
+    status[s] = r;
+    ok[s] = r == AG_RS_OK;
+    slots_out[s] = ok[s] ? h_slot[s] : 0;
+    slice_indices_out[s] = ok[s] ? h_sidx[s] : 0;
+    is_last_out[s] = ok[s] ? h_last[s] : 0;
+  }
+  // 7. fill_missing_shreds: datagrams for the absent slots of the slices that succeeded
+  uint8_t *d_ok, *fresh;
+  if ((st = pipe_buf(c, 20, n, &d_ok)) || (st = pipe_buf(c, 10, 4 * N, &fresh))) return st;
+  AG_HIP(hipMemcpyAsync(d_ok, ok.data(), n, hipMemcpyHostToDevice, c->stream));
+  ag::PipeExpandParams ep{};
+  ep.nslices = n;
+  ep.shred_bytes = static_cast<uint32_t>(S);
+  ep.skip = d_present;
+  ep.slice_ok = d_ok;
+  ep.kind = kind;
+  ep.shred_index = cols.shred_index;
+  ep.data_len = cols.data_len;
+  ep.height = cols.height;
+  if (ag::launch_pipe_expand(ep, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  ag::ShredColumns fc = cols;
+  fc.slot = d_slot;
+  fc.slice_index = reinterpret_cast<uint64_t*>(ssidx);
+  fc.is_last = slast;
+  fc.sig = ssig;
+  fc.hdr_group = ag::kPipeShreds;
+  if (ag::launch_shred_serialize(fc, N, packets, packet_stride, reinterpret_cast<uint32_t*>(fresh), c->stream) !=
+          hipSuccess ||
+      ag::launch_pipe_merge_lens(reinterpret_cast<uint32_t*>(fresh), d_present, d_ok, n, packet_lens, c->stream) !=
+          hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  AG_HIP(hipStreamSynchronize(c->stream));  // host vectors read by async copies
   return AG_RS_OK;
 }
 

@@ -1,0 +1,170 @@
+// Glue kernels of the composed Shredder pipeline (gfx950).
+//
+// What they replace: the per-slice bookkeeping around the batched stages in the
+// reference's RegularShredder::shred (shredder.rs:337-345 -> data_and_coding_to_output_shreds
+// :533-560) and Shredder::deshred (:282-311 -> check_merkle_tree :616-625,
+// fill_missing_shreds :576-611), plus the receiver's per-shred checks
+// (ValidatedShred::try_new with the blockstore's cached commitment,
+// validated_shred.rs:52-81).  The stages themselves (framing, RS, Merkle, Ed25519, wire) are
+// the library's other kernels; ag_shredder_*_batch in rs_api.cpp chains them.
+#include <hip/hip_runtime.h>
+
+#include "shredder.hpp"
+
+namespace ag {
+namespace {
+
+__global__ __launch_bounds__(256) void pipe_expand_kernel(const PipeExpandParams p) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= p.nslices * kPipeShreds) return;
+  const uint64_t s = t / kPipeShreds;
+  const uint32_t j = static_cast<uint32_t>(t % kPipeShreds);
+  const bool skip = (p.skip && ((p.skip[s] >> j) & 1)) || (p.slice_ok && !p.slice_ok[s]);
+  p.kind[t] = j >= kPipeData ? 1 : 0;
+  p.shred_index[t] = j;
+  p.data_len[t] = skip ? 0xFFFFFFFFu : p.shred_bytes;
+  p.height[t] = kPipeHeight;
+}
+
+// shred t fits slot j of its slice: parsed, index j, Data for j < 32, S bytes, 6 digests
+__device__ __forceinline__ bool plausible(const ShredColumns& c, const uint8_t* wire_status, uint64_t t, uint32_t j,
+                                          uint32_t S) {
+  return wire_status[t] == kWireOk && c.shred_index[t] == j && c.kind[t] == (j >= kPipeData ? 1 : 0) &&
+         c.data_len[t] == S && c.height[t] == kPipeHeight;
+}
+
+// one 64-lane wave per slice; lane j looks at shred j
+__global__ __launch_bounds__(64) void pipe_pick_kernel(const PipePickParams p) {
+  const uint64_t s = blockIdx.x;
+  const uint32_t j = threadIdx.x;
+  const uint64_t t = s * kPipeShreds + j;
+  const uint64_t ok = __builtin_amdgcn_ballot_w64(plausible(p.cols, p.wire_status, t, j, p.shred_bytes));
+  const uint32_t pick = ok ? static_cast<uint32_t>(__builtin_ctzll(ok)) : kPipeNone;
+  if (j == 0) p.pick[s] = static_cast<uint8_t>(pick);
+  if (pick == kPipeNone) return;
+  const uint64_t r = s * kPipeShreds + pick;
+  // payload row (2-byte aligned: S is only even), proof, signature, header
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(p.cols.data + r * p.cols.data_stride);
+  uint16_t* dst = reinterpret_cast<uint16_t*>(p.g_data + s * p.shred_bytes);
+  for (uint32_t i = j; i < p.shred_bytes / 2; i += kPipeShreds) dst[i] = src[i];
+  const uint8_t* pp = p.cols.proof + r * p.cols.proof_stride;
+  for (uint32_t i = j; i < 32 * kPipeHeight; i += kPipeShreds) p.g_proof[s * 32 * kPipeHeight + i] = pp[i];
+  p.g_sig[64 * s + j] = p.cols.sig[64 * r + j];
+  if (j == 0) {
+    p.g_slot[s] = p.cols.slot[r];
+    p.g_slice_index[s] = p.cols.slice_index[r];
+    p.g_is_last[s] = p.cols.is_last[r];
+    p.g_shred_index[s] = pick;
+  }
+}
+
+__global__ __launch_bounds__(256) void pipe_cache_kernel(const uint8_t* pick, const uint8_t* pick_status,
+                                                         uint64_t nslices, uint8_t* has_cached) {
+  const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= nslices) return;
+  has_cached[s] = pick[s] != kPipeNone && pick_status[s] == 0 ? 1 : 0;  // kShredOk
+}
+
+__global__ __launch_bounds__(64) void pipe_check_kernel(const PipeCheckParams p) {
+  const uint64_t s = blockIdx.x;
+  const uint32_t j = threadIdx.x;
+  const uint64_t t = s * kPipeShreds + j;
+  const bool valid = plausible(p.cols, p.wire_status, t, j, p.shred_bytes) && p.val_status[t] == 0;
+  const uint64_t v = __builtin_amdgcn_ballot_w64(valid);
+  if (v == 0) {
+    if (j == 0) p.present[s] = 0;
+    return;
+  }
+  const uint32_t r0 = static_cast<uint32_t>(__builtin_ctzll(v));
+  const uint64_t r = s * kPipeShreds + r0;
+  // keep the shreds whose commitment (header + root) equals the first kept one's
+  bool same = valid && p.cols.slot[t] == p.cols.slot[r] && p.cols.slice_index[t] == p.cols.slice_index[r] &&
+              p.cols.is_last[t] == p.cols.is_last[r];
+  if (same) {
+    const uint32_t* a = reinterpret_cast<const uint32_t*>(p.roots + 32 * t);
+    const uint32_t* b = reinterpret_cast<const uint32_t*>(p.roots + 32 * r);
+    for (int i = 0; i < 8; ++i) same = same && a[i] == b[i];
+  }
+  const uint64_t keep = __builtin_amdgcn_ballot_w64(same);
+  if (j == 0) {
+    p.present[s] = keep;
+    p.slot[s] = p.cols.slot[r];
+    p.slice_index[s] = p.cols.slice_index[r];
+    p.is_last[s] = p.cols.is_last[r];
+  }
+  if (j < 32) p.root[32 * s + j] = p.roots[32 * r + j];
+  p.sig[64 * s + j] = p.cols.sig[64 * r + j];
+}
+
+__global__ __launch_bounds__(256) void pipe_root_cmp_kernel(const uint8_t* a, const uint8_t* b, uint64_t nslices,
+                                                            uint8_t* same) {
+  const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= nslices) return;
+  const uint32_t* x = reinterpret_cast<const uint32_t*>(a + 32 * s);
+  const uint32_t* y = reinterpret_cast<const uint32_t*>(b + 32 * s);
+  uint32_t d = 0;
+  for (int i = 0; i < 8; ++i) d |= x[i] ^ y[i];
+  same[s] = d == 0 ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void pipe_merge_kernel(const uint32_t* fresh, const uint64_t* present,
+                                                         const uint8_t* slice_ok, uint64_t nslices,
+                                                         uint32_t* packet_lens) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= nslices * kPipeShreds) return;
+  const uint64_t s = t / kPipeShreds;
+  const uint32_t j = static_cast<uint32_t>(t % kPipeShreds);
+  if (slice_ok[s] && !((present[s] >> j) & 1)) packet_lens[t] = fresh[t];
+}
+
+dim3 grid256(uint64_t n) { return dim3(static_cast<unsigned>((n + 255) / 256)); }
+
+}  // namespace
+
+hipError_t launch_pipe_expand(const PipeExpandParams& p, hipStream_t stream) {
+  const uint64_t n = p.nslices * kPipeShreds;
+  if (n == 0) return hipSuccess;
+  if (n > 0x7FFFFFFFull * 256) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pipe_expand_kernel, grid256(n), dim3(256), 0, stream, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_pipe_pick(const PipePickParams& p, hipStream_t stream) {
+  if (p.nslices == 0) return hipSuccess;
+  if (p.nslices > 0x7FFFFFFFull || p.cols.proof_stride < 32 * kPipeHeight) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pipe_pick_kernel, dim3(static_cast<unsigned>(p.nslices)), dim3(64), 0, stream, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_pipe_cache_flags(const uint8_t* pick, const uint8_t* pick_status, uint64_t nslices,
+                                   uint8_t* has_cached, hipStream_t stream) {
+  if (nslices == 0) return hipSuccess;
+  hipLaunchKernelGGL(pipe_cache_kernel, grid256(nslices), dim3(256), 0, stream, pick, pick_status, nslices,
+                     has_cached);
+  return hipGetLastError();
+}
+
+hipError_t launch_pipe_check(const PipeCheckParams& p, hipStream_t stream) {
+  if (p.nslices == 0) return hipSuccess;
+  if (p.nslices > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(pipe_check_kernel, dim3(static_cast<unsigned>(p.nslices)), dim3(64), 0, stream, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_pipe_root_cmp(const uint8_t* a, const uint8_t* b, uint64_t nslices, uint8_t* same,
+                                hipStream_t stream) {
+  if (nslices == 0) return hipSuccess;
+  hipLaunchKernelGGL(pipe_root_cmp_kernel, grid256(nslices), dim3(256), 0, stream, a, b, nslices, same);
+  return hipGetLastError();
+}
+
+hipError_t launch_pipe_merge_lens(const uint32_t* fresh, const uint64_t* present, const uint8_t* slice_ok,
+                                  uint64_t nslices, uint32_t* packet_lens, hipStream_t stream) {
+  const uint64_t n = nslices * kPipeShreds;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(pipe_merge_kernel, grid256(n), dim3(256), 0, stream, fresh, present, slice_ok, nslices,
+                     packet_lens);
+  return hipGetLastError();
+}
+
+}  // namespace ag

@@ -103,13 +103,14 @@ __global__ __launch_bounds__(256) void shred_serialize_kernel(const ShredColumns
     if (lane == 0) packet_lens[t] = 0;  // does not fit the caller's rows: nothing written
     return;
   }
+  const uint64_t h = c.hdr_group > 1 ? t / c.hdr_group : t;  // header row
   if (lane == 0) {
     const uint32_t kind = c.kind[t];
     pk[0] = static_cast<uint8_t>(kind);
     pk[1] = pk[2] = pk[3] = 0;
-    st_u64(pk + 4, c.slot[t]);
-    st_u64(pk + 12, c.slice_index[t]);
-    pk[20] = c.is_last[t] ? 1 : 0;
+    st_u64(pk + 4, c.slot[h]);
+    st_u64(pk + 12, c.slice_index[h]);
+    pk[20] = c.is_last[h] ? 1 : 0;
     st_u64(pk + 21, c.shred_index[t]);
     st_u64(pk + 29, dlen);
     st_u64(pk + o_sig + 64, plen);
@@ -117,7 +118,7 @@ __global__ __launch_bounds__(256) void shred_serialize_kernel(const ShredColumns
   }
   const uint8_t* dd = c.data + t * c.data_stride;
   for (uint32_t i = lane; i < dlen; i += 64) pk[kShredHeadBytes + i] = dd[i];
-  pk[o_sig + lane] = c.sig[64 * t + lane];
+  pk[o_sig + lane] = c.sig[64 * h + lane];
   const uint8_t* pp = c.proof + t * c.proof_stride;
   for (uint32_t i = lane; i < 32 * plen; i += 64) pk[o_sig + 72 + i] = pp[i];
 }

@@ -26,6 +26,8 @@ struct ShredColumns {
   uint8_t* proof;        // proof + t*proof_stride, height digests
   uint64_t proof_stride;
   uint32_t* height;
+  uint32_t hdr_group;    // serialize only: > 1 reads slot / slice_index / is_last / sig of row
+                         // t / hdr_group (one header per slice); 0 or 1: per shred
 };
 
 // network::deserialize::<Shred> for n packets (packet t at packets + t*packet_stride,

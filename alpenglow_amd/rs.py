@@ -51,6 +51,8 @@ STATUS_KIND = {
     20: "TooMuchData",
     21: "InvalidPadding",
     22: "InvalidLayout",
+    23: "BadEncoding",
+    24: "InvalidMerkleTree",
     100: "InvalidArgument",
     101: "NoDevice",
     102: "DeviceError",
@@ -79,6 +81,7 @@ EXPORTS = (
     "ag_ed25519_public_key_batch", "ag_ed25519_sign_batch", "ag_ed25519_verify_batch", "ag_shred_validate_batch",
     "ag_slice_sign_batch", "ag_shred_deserialize_batch", "ag_shred_serialize_batch",
     "ag_slice_frame_batch", "ag_slice_parse_batch",
+    "ag_shredder_shred_batch", "ag_shredder_deshred_batch",
 )
 
 
@@ -157,6 +160,8 @@ def load():
         "ag_shred_serialize_batch": ([p, sz, p, p, sz, p], i),
         "ag_slice_frame_batch": ([p, sz, sz, p, p, p, sz, p, p, sz, p], i),
         "ag_slice_parse_batch": ([p, sz, p, sz, p, p, p, p, p, p], i),
+        "ag_shredder_shred_batch": ([p, sz, sz, p, p, p, sz, p, p, p, p, p, p, p, p, p, p, sz, p], i),
+        "ag_shredder_deshred_batch": ([p, sz, sz, p, sz, p, p, p, p, p, p, p, p, p, p, p], i),
     }
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
@@ -649,6 +654,22 @@ SLICE_OK, SLICE_TOO_LARGE, SLICE_BAD_ENCODING, SLICE_NO_PAYLOAD = 0, 1, 2, 3
 BLOCK_ID_BYTES = 40
 
 
+def _parent_arrays(parents, nslices: int):
+    import numpy as np
+
+    if len(parents) != nslices:
+        raise ValueError("parents do not match the batch")
+    flags = np.zeros(nslices, np.uint8)
+    ids = np.zeros((nslices, BLOCK_ID_BYTES), np.uint8)
+    for b, par in enumerate(parents):
+        if par is not None:
+            slot, h = par
+            flags[b] = 1
+            ids[b, :8] = np.frombuffer(int(slot).to_bytes(8, "little"), np.uint8)
+            ids[b, 8:] = np.frombuffer(bytes(h), np.uint8)
+    return flags, ids
+
+
 def slice_frame_batch(ctx: Context, nslices: int, shred_bytes: int, parents, data, data_stride: int, data_lens,
                       codewords, codeword_stride: int):
     """Slice::payload_bytes for a batch, written into the codewords' data regions.
@@ -658,17 +679,10 @@ def slice_frame_batch(ctx: Context, nslices: int, shred_bytes: int, parents, dat
     pass to ``coder_shred_batch(..., payloads=None, payload_lens=...)``."""
     import numpy as np
 
-    flags = np.zeros(nslices, np.uint8)
-    ids = np.zeros((nslices, BLOCK_ID_BYTES), np.uint8)
-    for b, par in enumerate(parents):
-        if par is not None:
-            slot, h = par
-            flags[b] = 1
-            ids[b, :8] = np.frombuffer(int(slot).to_bytes(8, "little"), np.uint8)
-            ids[b, 8:] = np.frombuffer(bytes(h), np.uint8)
+    flags, ids = _parent_arrays(parents, nslices)
     lens = np.ascontiguousarray(np.asarray(data_lens, dtype=np.uint32))
     out = np.zeros(nslices, np.uint32)
-    if len(parents) != nslices or lens.size != nslices:
+    if lens.size != nslices:
         raise ValueError("parents / data_lens do not match the batch")
     _check(load().ag_slice_frame_batch(ctx.handle, nslices, shred_bytes, flags.ctypes.data, ids.ctypes.data,
                                        _ptr(data) if data is not None else None, data_stride, lens.ctypes.data,
@@ -693,3 +707,66 @@ def slice_parse_batch(ctx: Context, nslices: int, codewords, codeword_stride: in
     parents = [(int.from_bytes(ids[b, :8].tobytes(), "little"), ids[b, 8:].tobytes()) if flags[b] else None
                for b in range(nslices)]
     return st, parents, offs, dl
+
+
+# ---- composed Shredder (RegularShredder: shredder.rs:282-345, :533-625) ------------------
+
+def shredder_shred_batch(ctx: Context, nslices: int, shred_bytes: int, parents, data, data_stride: int, data_lens,
+                         slots, slice_indices, is_last, seed, pk, codewords, packets, packet_stride: int,
+                         packet_lens, roots_out=None, sigs_out=None):
+    """RegularShredder::shred for a batch of slices of one shred size: Slice::payload_bytes,
+    ReedSolomonCoder::shred, the slice Merkle tree, the slice signature and the 64 Shred
+    datagrams per slice (slice s, shred j at packets + (64 s + j) * packet_stride).
+
+    parents / data_lens: host (as slice_frame_batch); data, slots, slice_indices, is_last,
+    seed, pk, codewords (64 * shred_bytes per slice), packets, packet_lens: device."""
+    import numpy as np
+
+    flags, ids = _parent_arrays(parents, nslices)
+    lens = np.ascontiguousarray(np.asarray(data_lens, dtype=np.uint32))
+    if lens.size != nslices:
+        raise ValueError("data_lens do not match the batch")
+    _check(load().ag_shredder_shred_batch(ctx.handle, nslices, shred_bytes, flags.ctypes.data, ids.ctypes.data,
+                                          _optr(data), data_stride, lens.ctypes.data, _ptr(slots),
+                                          _ptr(slice_indices), _ptr(is_last), _ptr(seed), _ptr(pk),
+                                          _ptr(codewords), _optr(roots_out), _optr(sigs_out), _ptr(packets),
+                                          packet_stride, _ptr(packet_lens)), "ag_shredder_shred_batch")
+
+
+@dataclass
+class DeshredBatch:
+    """Per-slice results of shredder_deshred_batch (numpy arrays; parents as in
+    slice_parse_batch).  status[s] is 0 or an AG_RS_ERR_* code (STATUS_KIND names it)."""
+    status: object
+    slots: object
+    slice_indices: object
+    is_last: object
+    parents: list
+    data_offsets: object
+    data_lens: object
+
+
+def shredder_deshred_batch(ctx: Context, nslices: int, shred_bytes: int, packets, packet_stride: int, packet_lens,
+                           pk, codewords) -> DeshredBatch:
+    """Shredder::deshred for a batch: the received datagrams (slot s * 64 + j, length 0 =
+    absent) are parsed, validated (ValidatedShred::try_new under pk), deshredded, checked
+    against the slice's Merkle root and parsed as SlicePayload; the absent datagrams of
+    every successful slice are filled in (packets / packet_lens updated in place)."""
+    import numpy as np
+
+    st = np.zeros(nslices, np.int32)
+    slots = np.zeros(nslices, np.uint64)
+    sidx = np.zeros(nslices, np.uint64)
+    last = np.zeros(nslices, np.uint8)
+    flags = np.zeros(nslices, np.uint8)
+    ids = np.zeros((nslices, BLOCK_ID_BYTES), np.uint8)
+    offs = np.zeros(nslices, np.uint32)
+    dl = np.zeros(nslices, np.uint32)
+    _check(load().ag_shredder_deshred_batch(ctx.handle, nslices, shred_bytes, _ptr(packets), packet_stride,
+                                            _ptr(packet_lens), _ptr(pk), _ptr(codewords), st.ctypes.data,
+                                            slots.ctypes.data, sidx.ctypes.data, last.ctypes.data, flags.ctypes.data,
+                                            ids.ctypes.data, offs.ctypes.data, dl.ctypes.data),
+           "ag_shredder_deshred_batch")
+    parents = [(int.from_bytes(ids[b, :8].tobytes(), "little"), ids[b, 8:].tobytes()) if flags[b] else None
+               for b in range(nslices)]
+    return DeshredBatch(st, slots, sidx, last, parents, offs, dl)

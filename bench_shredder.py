@@ -1,0 +1,140 @@
+#!/usr/bin/env python3
+"""bench_shredder.py -- the composed RegularShredder on the device (SURVEY.md §8 a10 end to
+end; VERDICT r01 "composed Shredder pipeline"): ag_shredder_shred_batch (Slice framing ->
+ReedSolomonCoder::shred -> slice Merkle tree -> slice signature -> 64 Shred datagrams per
+slice; shredder.rs:337-345, :533-560) and ag_shredder_deshred_batch (datagrams -> parse ->
+ValidatedShred::try_new with the cached commitment -> ReedSolomonCoder::deshred ->
+check_merkle_tree -> SlicePayload::try_from -> fill_missing_shreds; shredder.rs:282-311,
+validated_shred.rs:52-81).
+
+Workload: n maximum slices (32 758 data bytes + 9-byte header = 32 767-byte payload, 1 KiB
+shreds).  Shred builds all 64 datagrams per slice; deshred receives, per slice, the first
+32..64 datagrams of a seeded random arrival order (the follower deshreds once 32 arrived,
+slot_block_data.rs:331-370) and fills in the rest.  Device-resident buffers; wall clock
+around each (synchronous) call.  Prints one JSON line; the verify block checks the round
+trip (every payload and datagram restored) and a spot check against the CPU composition of
+the reference (oracle/shredder_oracle.py, checker only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+GIB = float(1 << 30)
+PKT = 1344  # datagram slot (1325 bytes for a 1 KiB shred, rounded to 64)
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    ap.add_argument("--slices", type=int, default=65536)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--arrived", type=int, default=32, help="datagrams received per slice before deshred (32..64)")
+    args = ap.parse_args()
+    import numpy as np
+    import torch
+
+    from alpenglow_amd import rs
+
+    dev = torch.device("cuda:0")
+    torch.zeros(1, device=dev)
+    ctx = rs.Context(0)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    ctx.set_stream(stream.cuda_stream)
+    n, S = args.slices, 1024
+    D = 32 * S - 1 - 9  # data bytes: framed payload = MAX_DATA_PER_SLICE
+    data = torch.empty((n, 32 * S), dtype=torch.uint8, device=dev)
+    rs.fill_splitmix(ctx, data, n, 32 * S, 32 * S, 0x5EED0000)
+    g = torch.Generator(device="cpu").manual_seed(0xA221)
+    slots = torch.randint(0, 1 << 40, (n,), generator=g, dtype=torch.int64).to(dev)
+    sidx = torch.randint(0, 1024, (n,), generator=g, dtype=torch.int64).to(dev)
+    last = (torch.arange(n) % 1024 == 1023).to(torch.uint8).to(dev)
+    seed = torch.arange(32, dtype=torch.uint8).to(dev)
+    pk = torch.empty(32, dtype=torch.uint8, device=dev)
+    rs.ed25519_public_key_batch(ctx, 1, seed, pk)
+    cw = torch.empty((n, 64 * S), dtype=torch.uint8, device=dev)
+    pkts = torch.zeros((n * 64, PKT), dtype=torch.uint8, device=dev)
+    lens = torch.zeros(n * 64, dtype=torch.int32, device=dev)
+    parents, dlens = [None] * n, np.full(n, D, np.uint32)
+    # arrival: per slice the first `arrived` of a random order
+    order = torch.argsort(torch.rand((n, 64), generator=g), dim=1)
+    keep = torch.zeros((n, 64), dtype=torch.bool)
+    keep.scatter_(1, order[:, :args.arrived], True)
+    keep = keep.reshape(-1).to(dev)
+
+    def shred():
+        rs.shredder_shred_batch(ctx, n, S, parents, data, 32 * S, dlens, slots, sidx, last, seed, pk, cw, pkts, PKT,
+                                lens)
+
+    def deshred():
+        return rs.shredder_deshred_batch(ctx, n, S, pkts, PKT, lens, pk, cw)
+
+    shred()
+    torch.cuda.synchronize()
+    full_lens = lens.clone()
+    full_pkts = pkts[: 64 * 8].clone()
+    for _ in range(args.warmup):
+        lens.mul_(keep)
+        deshred()
+        shred()
+    torch.cuda.synchronize()
+    t_sh = t_de = 0.0
+    for _ in range(args.steps):
+        a = time.perf_counter()
+        shred()
+        torch.cuda.synchronize()
+        b = time.perf_counter()
+        lens.mul_(keep)  # the datagrams that did not arrive
+        torch.cuda.synchronize()
+        c = time.perf_counter()
+        res = deshred()  # synchronous
+        d = time.perf_counter()
+        t_sh += b - a
+        t_de += d - c
+    ok = bool((res.status == 0).all()) and bool(torch.equal(lens, full_lens)) and \
+        bool(torch.equal(pkts[: 64 * 8], full_pkts)) and bool((res.data_lens == D).all())
+    ok = ok and bool(torch.equal(cw[:, 9:9 + D][:64], data[:64, :D]))
+    # spot check: two slices against the CPU composition of the reference (checker only)
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import shredder_oracle as so
+    hp, hl = pkts[:128].cpu().numpy(), lens[:128].cpu().numpy()
+    sl, si, ls = slots[:2].cpu().tolist(), sidx[:2].cpu().tolist(), last[:2].cpu().tolist()
+    spot = True
+    for b in range(2):
+        want, *_ = so.shred(None, data[b, :D].cpu().numpy().tobytes(), sl[b], si[b], bool(ls[b]),
+                            bytes(range(32)))
+        spot &= all(hp[b * 64 + j, :hl[b * 64 + j]].tobytes() == want[j] for j in range(64))
+    steps = args.steps
+    line = {
+        "metric": "slices/s composed RegularShredder shred + deshred (datagrams in, datagrams out), max slices",
+        "value": n * steps / (t_sh + t_de),
+        "unit": "slices/s",
+        "n_gpus": 1,
+        "steps": steps,
+        "warmup": args.warmup,
+        "ms_per_step": (t_sh + t_de) * 1e3 / steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic (splitmix64 payloads, device-generated; one leader key)",
+        "config": {"workload": f"{n} slices x {D + 9} B payload, 64 datagrams of 1325 B per slice; deshred from a "
+                               f"random {args.arrived} of 64 datagrams per slice"},
+        "payload_GiBps": n * (D + 9) * steps / (t_sh + t_de) / GIB,
+        "calls_ms": {"shred_batch": t_sh * 1e3 / steps, "deshred_batch": t_de * 1e3 / steps},
+        "shred_slices_per_s": n * steps / t_sh,
+        "deshred_slices_per_s": n * steps / t_de,
+        "verify": {"roundtrip_restores_everything": ok, "datagrams_match_oracle": bool(spot)},
+    }
+    print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()

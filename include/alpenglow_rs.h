@@ -66,6 +66,7 @@ enum {
   AG_RS_ERR_INVALID_PADDING = 21,             /* InvalidPadding (reed_solomon.rs:31) */
   AG_RS_ERR_INVALID_LAYOUT = 22,              /* DeshredError::InvalidLayout (shredder.rs:75) */
   AG_RS_ERR_BAD_ENCODING = 23,                /* DeshredError::BadEncoding (decrypt_payload, shredder.rs:518) */
+  AG_RS_ERR_INVALID_MERKLE_TREE = 24,         /* DeshredError::InvalidMerkleTree (shredder.rs:616-625) */
   AG_RS_ERR_INVALID_ARGUMENT = 100,
   AG_RS_ERR_NO_DEVICE = 101,                  /* no usable GPU: never a CPU fallback */
   AG_RS_ERR_DEVICE = 102,                     /* HIP runtime / kernel launch failure */
@@ -390,6 +391,49 @@ int ag_shred_deserialize_batch(ag_rs_ctx* ctx, size_t n, const uint8_t* packets,
  * shred does not fit packet_stride or its own rows. */
 int ag_shred_serialize_batch(ag_rs_ctx* ctx, size_t n, const ag_shred_columns* cols, uint8_t* packets,
                              size_t packet_stride, uint32_t* packet_lens);
+
+/* ---- 9. composed Shredder (RegularShredder, 32 data + 32 coding shreds) ----------------
+ * One call per direction for nslices slices of one shred size S (even, <= 1024), every
+ * stage on the device, one leader key.  Slice s owns 64 datagram slots (packets +
+ * (64 s + j) * packet_stride, j = shred index; packet_stride >= 1325 for S = 1024) and one
+ * codeword of 64 raw shreds (codewords + s * 64 * S: 32 data shreds, then 32 coding
+ * shreds, 16-byte aligned).  Slice headers (slots, slice_indices, is_last: one entry per
+ * slice) and the key (seed, pk: 32 B) are device arrays; the rest is stated per argument.
+ *
+ * shred_batch -- RegularShredder::shred (shredder.rs:337-345): Slice::payload_bytes (the
+ * framing of section 4b; parent_flags / parent_ids / data_lens HOST, data device) ->
+ * ReedSolomonCoder::shred -> slice Merkle tree (roots_out, 32 B per slice, nullable) ->
+ * sign(SliceCommitment) (sigs_out, 64 B per slice, nullable) -> the 64 Shred datagrams of
+ * every slice, data shreds first (data_and_coding_to_output_shreds, :533-560);
+ * packet_lens (device) gets each datagram's length.  Errors (nothing launched):
+ * TOO_MUCH_DATA (a framed slice does not fit 32 * S or 32767 bytes), INVALID_ARGUMENT.
+ *
+ * deshred_batch -- Shredder::deshred (shredder.rs:282-311) behind the receiver's checks:
+ * the datagrams present (packet_lens > 0) are parsed (network::deserialize), their fields
+ * checked against their slot (shred index j, kind, S bytes, 6-digest path) and validated
+ * (ValidatedShred::try_new, validated_shred.rs:52-81: Merkle path -> root -> commitment ->
+ * Ed25519 under pk; the first such shred of a slice is verified by signature and the
+ * others compared with its commitment, as the blockstore's cache does); datagrams failing
+ * any check count as absent.  Then ReedSolomonCoder::deshred (any 32 survivors, ANY_K),
+ * check_merkle_tree, SlicePayload::try_from, and fill_missing_shreds: every absent slot of
+ * a slice that succeeded receives its datagram (packet and packet_lens written; the
+ * present ones are left as they were).  Per slice (HOST outputs): status[s] = AG_RS_OK or
+ * AG_RS_ERR_NOT_ENOUGH_SHARDS / _TOO_MUCH_DATA / _BAD_ENCODING (invalid padding or
+ * SlicePayload encoding) / _INVALID_MERKLE_TREE; for AG_RS_OK the header (slots_out,
+ * slice_indices_out, is_last_out), the parent (parent_flags_out, parent_ids_out 40 B) and
+ * the data at codewords + s * 64 * S + data_offsets_out[s], data_lens_out[s] bytes.  The
+ * codewords hold the 64 raw shreds of every successful slice.  Synchronous. */
+int ag_shredder_shred_batch(ag_rs_ctx* ctx, size_t nslices, size_t shred_bytes, const uint8_t* parent_flags,
+                            const uint8_t* parent_ids, const uint8_t* data, size_t data_stride,
+                            const uint32_t* data_lens, const uint64_t* slots, const uint64_t* slice_indices,
+                            const uint8_t* is_last, const uint8_t* seed, const uint8_t* pk, uint8_t* codewords,
+                            uint8_t* roots_out, uint8_t* sigs_out, uint8_t* packets, size_t packet_stride,
+                            uint32_t* packet_lens);
+int ag_shredder_deshred_batch(ag_rs_ctx* ctx, size_t nslices, size_t shred_bytes, uint8_t* packets,
+                              size_t packet_stride, uint32_t* packet_lens, const uint8_t* pk, uint8_t* codewords,
+                              int32_t* status, uint64_t* slots_out, uint64_t* slice_indices_out,
+                              uint8_t* is_last_out, uint8_t* parent_flags_out, uint8_t* parent_ids_out,
+                              uint32_t* data_offsets_out, uint32_t* data_lens_out);
 
 #ifdef __cplusplus
 }
