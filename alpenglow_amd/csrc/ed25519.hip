@@ -74,6 +74,10 @@ __global__ __launch_bounds__(64) void ed_sign_kernel(const EdSignParams p) {
 __global__ __launch_bounds__(256) void shred_commit_kernel(const ShredCommitParams p) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (t >= p.n) return;
+  if (p.active && !p.active[t]) {
+    p.status[t] = kShredInvalidSignature;
+    return;
+  }
   uint8_t c[kSliceCommitmentLen];
   const uint64_t slot = p.slots[t], si = p.slice_indices[t];
   for (int i = 0; i < 8; ++i) {

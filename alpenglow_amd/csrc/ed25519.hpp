@@ -76,6 +76,8 @@ struct ShredCommitParams {
   const uint8_t* cached;           // 49 B per shred (nullable)
   const uint8_t* has_cached;       // per shred (nullable: no cache)
   uint32_t cached_group;           // > 1: cached / has_cached entry t / cached_group (one per slice)
+  const uint8_t* active;           // nullable: shreds with active[t] == 0 get kShredInvalidSignature
+                                   // without a signature check (absent / malformed datagrams)
   uint64_t n;
   uint8_t* commitments;            // 49 B per shred (out)
   uint8_t* status;                 // out

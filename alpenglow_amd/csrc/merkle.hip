@@ -166,7 +166,7 @@ __global__ __launch_bounds__(256) void merkle_proof_kernel(const MerkleBuildPara
 template <bool A4>
 __global__ __launch_bounds__(256) void merkle_verify_kernel(const MerkleVerifyParams p) {
   const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= p.n) return;
+  if (t >= p.n || (p.active && !p.active[t])) return;
   uint32_t node[8];
   leaf_hash<A4>(p.leaves + t * p.leaf_stride, p.leaf_bytes, node);
   uint32_t idx = p.index[t];

@@ -47,6 +47,7 @@ struct MerkleVerifyParams {
   uint64_t n;
   uint8_t* ok;
   uint8_t* roots_out;  // derive_root mode (merkle.rs:411-428): root digests out, 32 B each; ok unused
+  const uint8_t* active;  // nullable: leaves with active[t] == 0 are skipped (nothing written)
 };
 hipError_t launch_merkle_verify(const MerkleVerifyParams& p, hipStream_t stream);
 

@@ -122,7 +122,7 @@ struct ag_rs_ctx {
   DevBuf stage_pad, stage_mask;                  // restrided shards (sizes not whole 64-byte chunks)
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
-  static constexpr int kPipeBufs = 24;
+  static constexpr int kPipeBufs = 25;
   DevBuf pipe[kPipeBufs];                   // composed shredder scratch (ag_shredder_*_batch)
   DevBuf d_sh_roots, d_sh_commit, d_sh_onvalid, d_sh_list;  // shred validation scratch
   DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
@@ -1823,8 +1823,8 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
                         const uint32_t* shred_index, const uint8_t* proofs, size_t proofs_stride, size_t height,
                         const uint64_t* slots, const uint64_t* slice_indices, const uint8_t* is_last,
                         const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
-                        const uint8_t* has_cached, uint32_t cached_group, uint8_t* status, uint8_t* roots_out,
-                        uint8_t* commitments_out);
+                        const uint8_t* has_cached, uint32_t cached_group, const uint8_t* active, uint8_t* status,
+                        uint8_t* roots_out, uint8_t* commitments_out);
 }  // namespace
 
 int ag_ed25519_public_key_batch(ag_rs_ctx* c, size_t n, const uint8_t* seeds, uint8_t* pks) {
@@ -1892,8 +1892,8 @@ int ag_shred_validate_batch(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t 
                             const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
                             const uint8_t* has_cached, uint8_t* status, uint8_t* roots_out, uint8_t* commitments_out) {
   return shred_validate_impl(c, n, data, data_stride, data_bytes, shred_index, proofs, proofs_stride, height, slots,
-                             slice_indices, is_last, sigs, sig_stride, pk, cached, has_cached, 1, status, roots_out,
-                             commitments_out);
+                             slice_indices, is_last, sigs, sig_stride, pk, cached, has_cached, 1, nullptr, status,
+                             roots_out, commitments_out);
 }
 
 }  // extern "C"
@@ -1906,8 +1906,8 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
                         const uint32_t* shred_index, const uint8_t* proofs, size_t proofs_stride, size_t height,
                         const uint64_t* slots, const uint64_t* slice_indices, const uint8_t* is_last,
                         const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
-                        const uint8_t* has_cached, uint32_t cached_group, uint8_t* status, uint8_t* roots_out,
-                        uint8_t* commitments_out) {
+                        const uint8_t* has_cached, uint32_t cached_group, const uint8_t* active, uint8_t* status,
+                        uint8_t* roots_out, uint8_t* commitments_out) {
   if (!c || n >= kMaxSigBatch || data_bytes >= (size_t{1} << 28) ||
       height > static_cast<size_t>(ag::kMerkleMaxHeight) ||
       (n && (!shred_index || !slots || !slice_indices || !is_last || !sigs || !pk || !status ||
@@ -1943,6 +1943,7 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
   mp.proofs_stride = proofs_stride;
   mp.n = n;
   mp.roots_out = roots;
+  mp.active = active;
   if (ag::launch_merkle_verify(mp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   // 2. SliceCommitment + cached-commitment rule (validated_shred.rs:57-64)
   AG_HIP(hipMemsetAsync(count, 0, 4, c->stream));
@@ -1954,6 +1955,7 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
   cp.cached = cached;
   cp.has_cached = has_cached;
   cp.cached_group = cached_group;
+  cp.active = active;
   cp.n = n;
   cp.commitments = commits;
   cp.status = status;
@@ -2300,6 +2302,8 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
       (st = pipe_buf(c, 19, 64 * n, &gsig)) || (st = pipe_buf(c, 20, n, &pstat)) ||
       (st = pipe_buf(c, 21, ag::kSliceCommitmentLen * n, &commits)) || (st = pipe_buf(c, 22, n, &hasc)))
     return st;
+  uint8_t* plaus;  // per shred: the datagram parsed and fits its slot
+  if ((st = pipe_buf(c, 24, N, &plaus))) return st;
   ag::PipePickParams pp{};
   pp.nslices = n;
   pp.shred_bytes = static_cast<uint32_t>(S);
@@ -2313,18 +2317,19 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   pp.g_is_last = glast;
   pp.g_shred_index = reinterpret_cast<uint32_t*>(gidx);
   pp.g_sig = gsig;
+  pp.plausible = plaus;
   AG_HIP(hipMemsetAsync(gdata, 0, n * S, c->stream));  // slices without a pick: defined bytes
   AG_HIP(hipMemsetAsync(gidx, 0, 4 * n, c->stream));
   if (ag::launch_pipe_pick(pp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   if ((st = shred_validate_impl(c, n, gdata, S, S, pp.g_shred_index, gproof, kPipeProofBytes, ag::kPipeHeight,
-                                pp.g_slot, pp.g_slice_index, glast, gsig, 64, pk, nullptr, nullptr, 1, pstat, nullptr,
-                                commits)))
+                                pp.g_slot, pp.g_slice_index, glast, gsig, 64, pk, nullptr, nullptr, 1, nullptr, pstat,
+                                nullptr, commits)))
     return st;
   if (ag::launch_pipe_cache_flags(pick, pstat, n, hasc, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   // ... then every shred against its slice's commitment (signature only without a cache)
   if ((st = shred_validate_impl(c, N, codewords, S, S, cols.shred_index, proof, kPipeProofBytes, ag::kPipeHeight,
-                                cols.slot, cols.slice_index, last, sig, 64, pk, commits, hasc, ag::kPipeShreds, vstat,
-                                roots, nullptr)))
+                                cols.slot, cols.slice_index, last, sig, 64, pk, commits, hasc, ag::kPipeShreds, plaus,
+                                vstat, roots, nullptr)))
     return st;
   // 3. per slice: the shreds kept, the root, header and signature
   uint8_t* per_slice;

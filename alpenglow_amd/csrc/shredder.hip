@@ -38,7 +38,9 @@ __global__ __launch_bounds__(64) void pipe_pick_kernel(const PipePickParams p) {
   const uint64_t s = blockIdx.x;
   const uint32_t j = threadIdx.x;
   const uint64_t t = s * kPipeShreds + j;
-  const uint64_t ok = __builtin_amdgcn_ballot_w64(plausible(p.cols, p.wire_status, t, j, p.shred_bytes));
+  const bool fits = plausible(p.cols, p.wire_status, t, j, p.shred_bytes);
+  p.plausible[t] = fits ? 1 : 0;
+  const uint64_t ok = __builtin_amdgcn_ballot_w64(fits);
   const uint32_t pick = ok ? static_cast<uint32_t>(__builtin_ctzll(ok)) : kPipeNone;
   if (j == 0) p.pick[s] = static_cast<uint8_t>(pick);
   if (pick == kPipeNone) return;

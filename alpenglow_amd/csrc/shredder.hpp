@@ -49,6 +49,7 @@ struct PipePickParams {
   uint32_t* g_shred_index;
   uint8_t* g_sig;               // [nslices][64]
   uint8_t* has_cached;          // [nslices]: filled by launch_pipe_cache_flags
+  uint8_t* plausible;           // [nslices * 64] out: shred t parsed and fits its slot
 };
 hipError_t launch_pipe_pick(const PipePickParams& p, hipStream_t stream);
 // has_cached[s] = the picked shred of slice s passed its signature check.
