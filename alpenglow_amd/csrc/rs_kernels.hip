@@ -1465,7 +1465,7 @@ bool xform_supported(unsigned n) { return n == 32 || n == 64; }
 
 hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hipStream_t stream) {
   if (p.total_columns == 0) return hipSuccess;
-  const uint64_t tiles = (p.total_columns + (n == 32 ? 63 : 31)) / (n == 32 ? 64 : 32);
+  const uint64_t tiles = (p.total_columns + 63) / 64;
   if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const dim3 grid(static_cast<unsigned>(tiles));
   if (n == 32) {
@@ -1478,9 +1478,9 @@ hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hi
     }
   } else if (n == 64) {
     switch (j) {
-      case 0: hipLaunchKernelGGL((xform64h_kernel<0, 64>), grid, dim3(256), 0, stream, p); break;
-      case 1: hipLaunchKernelGGL((xform64h_kernel<0, 128>), grid, dim3(256), 0, stream, p); break;
-      case 2: hipLaunchKernelGGL((xform64h_kernel<0, 192>), grid, dim3(256), 0, stream, p); break;
+      case 0: return launch_xform16(0, 64, p, stream);
+      case 1: return launch_xform16(0, 128, p, stream);
+      case 2: return launch_xform16(0, 192, p, stream);
       default: return hipErrorInvalidValue;
     }
   } else {
@@ -1587,19 +1587,25 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
       else
         hipLaunchKernelGGL((xform8_kernel<0, 32>), grid, dim3(512), 0, stream, p);
       break;
+    // 64-point: xform16 (A/B against xform64h, profiles/r02_ab_xform16.json: encode 3.87 ->
+    // 4.46 TB/s, reconstruct 3.24 -> 4.14); variant 7 = xform64h, variant 1 = xform<8>.
     case XformKind::kEncode64:
       if (xform_variant() == 1)
         hipLaunchKernelGGL((xform_kernel<8, 64, 0>), grid, dim3(512), 0, stream, p);
-      else
+      else if (xform_variant() == 7)
         hipLaunchKernelGGL((xform64h_kernel<64, 0>), dim3(static_cast<unsigned>((p.total_columns + 31) / 32)),
                            dim3(256), 0, stream, p);
+      else
+        return launch_xform16(64, 0, p, stream);
       break;
     case XformKind::kDecode64:
       if (xform_variant() == 1)
         hipLaunchKernelGGL((xform_kernel<8, 0, 64>), grid, dim3(512), 0, stream, p);
-      else
+      else if (xform_variant() == 7)
         hipLaunchKernelGGL((xform64h_kernel<0, 64>), dim3(static_cast<unsigned>((p.total_columns + 31) / 32)),
                            dim3(256), 0, stream, p);
+      else
+        return launch_xform16(0, 64, p, stream);
       break;
     default:
       return hipErrorInvalidValue;

@@ -322,18 +322,21 @@ __device__ __forceinline__ uint32_t store_qmask(const TileIO& io, const uint64_t
 // =====================================================================================
 using Regs4 = uint32_t[4][16];
 
-// Position bits held by slot bits (S0, S1) and wave bits (W0, W1, W2).
-template <int S0, int S1, int W0, int W1, int W2>
+// Position bits held by slot bits (S0, S1) and wave bits (W0, W1, W2[, W3]).  W3 < 0: three
+// wave bits (xform8, 32 points); W3 >= 0: sixteen waves (xform16, 64 points).
+template <int S0, int S1, int W0, int W1, int W2, int W3 = -1>
 struct X8Lay {
   static constexpr int sb[2] = {S0, S1};
-  static constexpr int wb[3] = {W0, W1, W2};
+  static constexpr int wb[4] = {W0, W1, W2, W3};
   static constexpr int pos(int w, int t) {
     return (((t >> 0) & 1) << sb[0]) | (((t >> 1) & 1) << sb[1]) | (((w >> 0) & 1) << wb[0]) |
-           (((w >> 1) & 1) << wb[1]) | (((w >> 2) & 1) << wb[2]);
+           (((w >> 1) & 1) << wb[1]) | (((w >> 2) & 1) << wb[2]) | (W3 >= 0 ? ((w >> 3) & 1) << (W3 & 31) : 0);
   }
   static constexpr int slot_of(int b) { return sb[0] == b ? 0 : sb[1] == b ? 1 : -1; }
   // wave bits whose position bit exceeds b (the ones a layer-b constant depends on)
-  static constexpr int rel(int b) { return (wb[0] > b ? 1 : 0) | (wb[1] > b ? 2 : 0) | (wb[2] > b ? 4 : 0); }
+  static constexpr int rel(int b) {
+    return (wb[0] > b ? 1 : 0) | (wb[1] > b ? 2 : 0) | (wb[2] > b ? 4 : 0) | (W3 >= 0 && wb[3] > b ? 8 : 0);
+  }
 };
 template <int L>
 struct X8LayoutSel;
@@ -348,19 +351,22 @@ struct X8LayoutSel<3> { using T = X8Lay<4, 3, 0, 1, 2>; };
 template <int L>
 using X8Layout = typename X8LayoutSel<L>::T;
 
-constexpr int x8_popc(int m) { return (m & 1) + ((m >> 1) & 1) + ((m >> 2) & 1); }
+constexpr int x8_popc(int m) { return (m & 1) + ((m >> 1) & 1) + ((m >> 2) & 1) + ((m >> 3) & 1); }
 // wave bits selected by REL packed into the low bits, and back
 template <int REL>
 __device__ __forceinline__ int x8_compress(int w) {
+  if constexpr (REL == 0) return 0;
+  if constexpr (REL == 15) return w;
   int v = 0, k = 0;
   if constexpr (REL & 1) v |= (w & 1) << k++;
   if constexpr (REL & 2) v |= ((w >> 1) & 1) << k++;
   if constexpr (REL & 4) v |= ((w >> 2) & 1) << k++;
+  if constexpr (REL & 8) v |= ((w >> 3) & 1) << k++;
   return v;
 }
 constexpr int x8_expand(int v, int rel) {
   int w = 0, k = 0;
-  for (int j = 0; j < 3; ++j)
+  for (int j = 0; j < 4; ++j)
     if ((rel >> j) & 1) w |= ((v >> k++) & 1) << j;
   return w;
 }
@@ -392,7 +398,7 @@ __device__ __forceinline__ void x8_bfly_w(int v, uint32_t* x, uint32_t* y, bool 
       case 2: x8_bfly<Lay, B, INV, DELTA, T, 2>(x, y, upd_y); break;
       default: x8_bfly<Lay, B, INV, DELTA, T, 3>(x, y, upd_y); break;
     }
-  } else {
+  } else if constexpr (n == 8) {
     switch (v) {
       case 0: x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); break;
       case 1: x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y); break;
@@ -402,6 +408,25 @@ __device__ __forceinline__ void x8_bfly_w(int v, uint32_t* x, uint32_t* y, bool 
       case 5: x8_bfly<Lay, B, INV, DELTA, T, 5>(x, y, upd_y); break;
       case 6: x8_bfly<Lay, B, INV, DELTA, T, 6>(x, y, upd_y); break;
       default: x8_bfly<Lay, B, INV, DELTA, T, 7>(x, y, upd_y); break;
+    }
+  } else {
+    switch (v) {
+      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); break;
+      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y); break;
+      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2>(x, y, upd_y); break;
+      case 3: x8_bfly<Lay, B, INV, DELTA, T, 3>(x, y, upd_y); break;
+      case 4: x8_bfly<Lay, B, INV, DELTA, T, 4>(x, y, upd_y); break;
+      case 5: x8_bfly<Lay, B, INV, DELTA, T, 5>(x, y, upd_y); break;
+      case 6: x8_bfly<Lay, B, INV, DELTA, T, 6>(x, y, upd_y); break;
+      case 7: x8_bfly<Lay, B, INV, DELTA, T, 7>(x, y, upd_y); break;
+      case 8: x8_bfly<Lay, B, INV, DELTA, T, 8>(x, y, upd_y); break;
+      case 9: x8_bfly<Lay, B, INV, DELTA, T, 9>(x, y, upd_y); break;
+      case 10: x8_bfly<Lay, B, INV, DELTA, T, 10>(x, y, upd_y); break;
+      case 11: x8_bfly<Lay, B, INV, DELTA, T, 11>(x, y, upd_y); break;
+      case 12: x8_bfly<Lay, B, INV, DELTA, T, 12>(x, y, upd_y); break;
+      case 13: x8_bfly<Lay, B, INV, DELTA, T, 13>(x, y, upd_y); break;
+      case 14: x8_bfly<Lay, B, INV, DELTA, T, 14>(x, y, upd_y); break;
+      default: x8_bfly<Lay, B, INV, DELTA, T, 15>(x, y, upd_y); break;
     }
   }
 }
@@ -416,6 +441,16 @@ __device__ __forceinline__ void x8_layer(int wave, Regs4& r) {
   constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;  // the slots with bit i clear
   if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)], UPD_Y);
   if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)], UPD_Y);
+}
+// the same on an explicit layout type (xform8's pruned FFT layouts, xform16's layouts)
+template <typename Lay, int B, bool INV, int DELTA>
+__device__ __forceinline__ void x8_layer_t(int wave, Regs4& r) {
+  constexpr int i = Lay::slot_of(B);
+  static_assert(i >= 0, "layer bit must be a slot bit");
+  const int v = x8_compress<Lay::rel(B)>(wave);
+  constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;
+  x8_bfly_w<Lay, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)]);
+  x8_bfly_w<Lay, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)]);
 }
 template <typename Lay, int B, int DELTA, int LIVE>
 __device__ __forceinline__ void x8_layer_lay(int wave, Regs4& r) {
@@ -437,10 +472,12 @@ __device__ __forceinline__ void x8_layer_lay(int wave, Regs4& r) {
 #ifndef AG_X8_PAIRSYNC
 #define AG_X8_PAIRSYNC 1
 #endif
-struct X8Flags {
-  uint32_t ready[8];
-  uint32_t done[8];
+template <int NWAVES>
+struct XFlags {
+  uint32_t ready[NWAVES];
+  uint32_t done[NWAVES];
 };
+using X8Flags = XFlags<8>;
 __device__ __forceinline__ void x8_wait_ge(const uint32_t* f, uint32_t e) {
   while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) < e) __builtin_amdgcn_s_sleep(1);
 }
@@ -448,8 +485,8 @@ __device__ __forceinline__ void x8_signal(uint32_t* f, uint32_t e, int lane) {
   if (lane == 0) __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int I, int J, int EP, int LIVE = 0xF>
-__device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, X8Flags* fl, Regs4& r) {
+template <int I, int J, int EP, int LIVE = 0xF, typename Flags>
+__device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, Flags* fl, Regs4& r) {
   const int wj = (wave >> J) & 1;
   const int partner = wave ^ (1 << J);
 #if AG_X8_PAIRSYNC

@@ -17,7 +17,7 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t g) {
   return x * q + (x < r ? x : r) + (b >> 3);
 }
 
-template <int NC, int NWV, int WPE, int D>
+template <int NC, int NWV, int WPE, int D, int QM = 0>
 __global__ __launch_bounds__(64 * NWV, WPE) void tile_copy(const uint8_t* __restrict__ in, uint8_t* __restrict__ out,
                                                            uint32_t S) {
   extern __shared__ int pad[];
@@ -30,10 +30,17 @@ __global__ __launch_bounds__(64 * NWV, WPE) void tile_copy(const uint8_t* __rest
   const uint8_t* src = in + blk * bstride + (size_t)tt * NC * 64 + lane * 16;
   uint8_t* dst = out + blk * bstride + (size_t)K * S + (size_t)tt * NC * 64 + lane * 16;
   u32x4 v[SH][Q];
+  if constexpr (QM) {  // q-major: every shard's q-th KiB before the next KiB
 #pragma unroll
-  for (int s = 0; s < SH; ++s)
+    for (int q = 0; q < Q; ++q)
 #pragma unroll
-    for (int q = 0; q < Q; ++q) v[s][q] = *reinterpret_cast<const u32x4*>(src + (size_t)(wave * SH + s) * S + q * 1024);
+      for (int s = 0; s < SH; ++s) v[s][q] = *reinterpret_cast<const u32x4*>(src + (size_t)(wave * SH + s) * S + q * 1024);
+  } else {
+#pragma unroll
+    for (int s = 0; s < SH; ++s)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) v[s][q] = *reinterpret_cast<const u32x4*>(src + (size_t)(wave * SH + s) * S + q * 1024);
+  }
 #pragma unroll 1
   for (int d = 0; d < D; ++d) {
 #pragma unroll
@@ -47,10 +54,17 @@ __global__ __launch_bounds__(64 * NWV, WPE) void tile_copy(const uint8_t* __rest
       }
   }
   if (v[0][0].x == 0xdeadbeef && threadIdx.x == 100000) pad[0] = 1;
+  if constexpr (QM & 2) {
 #pragma unroll
-  for (int s = 0; s < SH; ++s)
+    for (int q = 0; q < Q; ++q)
 #pragma unroll
-    for (int q = 0; q < Q; ++q) *reinterpret_cast<u32x4*>(dst + (size_t)(wave * SH + s) * S + q * 1024) = v[s][q];
+      for (int s = 0; s < SH; ++s) *reinterpret_cast<u32x4*>(dst + (size_t)(wave * SH + s) * S + q * 1024) = v[s][q];
+  } else {
+#pragma unroll
+    for (int s = 0; s < SH; ++s)
+#pragma unroll
+      for (int q = 0; q < Q; ++q) *reinterpret_cast<u32x4*>(dst + (size_t)(wave * SH + s) * S + q * 1024) = v[s][q];
+  }
 }
 
 #define CK(x)                                                                        \
@@ -98,15 +112,25 @@ int main(int argc, char** argv) {
   char nm[128];
   // LDS per workgroup that caps the workgroups per CU at W (160 KiB LDS per CU)
   auto lds_cap = [](int w) { return w <= 0 ? 0 : (160 << 10) / w - 1024; };
-#define T(NC, NWV, WPE, D, WGCU)                                                                      \
-  snprintf(nm, sizeof nm, "NC%d waves%d wpe%d D%d wg/cu<=%d", NC, NWV, WPE, D, WGCU);                  \
+#define TQ(NC, NWV, WPE, D, WGCU, QM)                                                                 \
+  snprintf(nm, sizeof nm, "NC%d waves%d wpe%d D%d wg/cu<=%d qm%d", NC, NWV, WPE, D, WGCU, QM);         \
   timeit(nm, moved, [&] {                                                                              \
-    hipLaunchKernelGGL((tile_copy<NC, NWV, WPE, D>), dim3(nblk * (S / (64 * NC))), dim3(64 * NWV),     \
+    hipLaunchKernelGGL((tile_copy<NC, NWV, WPE, D, QM>), dim3(nblk * (S / (64 * NC))), dim3(64 * NWV), \
                        lds_cap(WGCU), 0, (const uint8_t*)a, a, S);                                     \
   });
+#define T(NC, NWV, WPE, D, WGCU) TQ(NC, NWV, WPE, D, WGCU, 0)
   // current transform shape: NC64, 4 waves x 8 shards, 2 WG/CU
   T(64, 4, 2, 0, 2)
+  TQ(64, 4, 2, 0, 2, 1)
+  TQ(64, 4, 2, 0, 2, 3)
+  TQ(64, 4, 2, 43, 2, 1)
+  TQ(64, 4, 2, 43, 2, 3)
   T(64, 8, 2, 0, 1)
+  TQ(64, 8, 4, 0, 2, 0)
+  TQ(64, 8, 4, 0, 2, 3)
+  TQ(64, 8, 4, 43, 2, 3)
+  TQ(32, 4, 2, 43, 4, 3)
+  TQ(32, 8, 2, 43, 2, 3)
   // NC16 shapes
   T(16, 4, 2, 0, 2)
   T(16, 4, 2, 0, 0)
