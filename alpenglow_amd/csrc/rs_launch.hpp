@@ -111,6 +111,7 @@ struct DecodeCParams {
   uint32_t chunks_per_shard;
   uint64_t total_columns;  // batch blocks * chunks_per_shard
   uint64_t ntiles;         // 64-column tiles processed
+  uint32_t balance;        // set by the launcher: spread the restored originals over the waves
 };
 hipError_t launch_decode_c(const DecodeCParams& p, hipStream_t stream);
 
