@@ -65,6 +65,41 @@ struct DevBuf {
   }
 };
 
+// Grow-only pinned host buffer: the crate-API single-call paths stage through it, so their
+// copies are DMA transfers instead of the runtime's pageable staging (one copy per direction).
+struct PinBuf {
+  void* ptr = nullptr;
+  size_t size = 0;
+  int ensure(size_t n) {
+    if (n <= size) return AG_RS_OK;
+    release();
+    if (hipHostMalloc(&ptr, n, hipHostMallocMapped) != hipSuccess) {
+      ptr = nullptr;
+      return AG_RS_ERR_OUT_OF_MEMORY;
+    }
+    if (hipHostGetDevicePointer(&dptr, ptr, 0) != hipSuccess) {
+      release();
+      return AG_RS_ERR_DEVICE;
+    }
+    size = n;
+    return AG_RS_OK;
+  }
+  template <typename T>
+  T* as() const {
+    return static_cast<T*>(ptr);
+  }
+  template <typename T>
+  T* dev() const {  // the same bytes as the device addresses them (zero-copy over PCIe)
+    return static_cast<T*>(dptr);
+  }
+  void* dptr = nullptr;
+  void release() {
+    if (ptr) (void)hipHostFree(ptr);
+    ptr = dptr = nullptr;
+    size = 0;
+  }
+};
+
 int check_geometry(size_t k, size_t m, size_t S) {
   if (ag::use_high_rate(k, m) < 0) return AG_RS_ERR_UNSUPPORTED_SHARD_COUNT;
   if (S == 0 || S % 2) return AG_RS_ERR_INVALID_SHARD_SIZE;
@@ -133,6 +168,7 @@ struct ag_rs_ctx {
   } slot[2];
   hipStream_t h2d = nullptr, d2h = nullptr;
   DevBuf one_in, one_out;                 // crate-API single codeword
+  PinBuf one_pin;                         // its pinned host staging
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
   std::vector<uint64_t> xmask_host;       // last general-decode masks (d_xmask), W = xmask_w
   size_t xmask_w = 0;
@@ -207,6 +243,7 @@ struct ag_rs_ctx {
                       &one_out})
       b->release();
     for (DevBuf& b : pipe) b.release();
+    one_pin.release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -1431,15 +1468,49 @@ struct ag_rs_decoder {
 };
 
 namespace {
+// One codeword through the device, zero-copy: the kernels read the originals from and
+// write the recovery shards to mapped pinned host memory (a 32-shard slice is 32 KiB each
+// way; two DMA copies and their scheduling cost more than the kernel's PCIe accesses).
 int run_one_encode(ag_rs_ctx* c, size_t k, size_t m, size_t S, const uint8_t* orig, uint8_t* rec) {
   int st;
   if ((st = c->enter())) return st;
-  if ((st = c->one_in.ensure(k * S, c->stream)) || (st = c->one_out.ensure(m * S, c->stream))) return st;
-  AG_HIP(hipMemcpyAsync(c->one_in.ptr, orig, k * S, hipMemcpyHostToDevice, c->stream));
-  if ((st = encode_device(c, k, m, S, 1, c->one_in.as<uint8_t>(), k * S, c->one_out.as<uint8_t>(), m * S)))
-    return st;
-  AG_HIP(hipMemcpyAsync(rec, c->one_out.ptr, m * S, hipMemcpyDeviceToHost, c->stream));
+  const size_t ob = k * S, rb = m * S;
+  if ((st = c->one_pin.ensure(ob + rb))) return st;
+  uint8_t* pin = c->one_pin.as<uint8_t>();
+  uint8_t* pd = c->one_pin.dev<uint8_t>();
+  std::memcpy(pin, orig, ob);
+  if ((st = encode_device(c, k, m, S, 1, pd, ob, pd + ob, rb))) return st;
   AG_HIP(hipStreamSynchronize(c->stream));
+  std::memcpy(rec, pin + ob, rb);
+  return AG_RS_OK;
+}
+
+// One codeword decoded on the device, zero-copy like run_one_encode: originals and recovery
+// shards in mapped pinned memory, decode in place (restored originals land in the original
+// region), and with `coding` the re-encode of every recovery shard from the completed
+// originals (ReedSolomonCoder::deshred's encode_coding_from_data, reed_solomon.rs:206).
+// EXACT runs as ANY_K when exactly k shards are present: k shards fix the codeword, so both
+// decoders return its originals for any input bytes.
+int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, uint8_t* orig, const uint8_t* rec,
+                   const uint8_t* opres, const uint8_t* rpres, int mode, uint8_t* coding) {
+  int st;
+  if ((st = c->enter())) return st;
+  const size_t ob = k * S, rb = m * S;
+  size_t present = 0;
+  for (size_t i = 0; i < k; ++i) present += opres[i] != 0;
+  for (size_t i = 0; i < m; ++i) present += rpres[i] != 0;
+  if (present < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
+  if (present == k) mode = AG_RS_DECODE_ANY_K;
+  if ((st = c->one_pin.ensure(ob + 2 * rb))) return st;
+  uint8_t* pin = c->one_pin.as<uint8_t>();
+  uint8_t* pd = c->one_pin.dev<uint8_t>();
+  std::memcpy(pin, orig, ob);
+  std::memcpy(pin + ob, rec, rb);
+  if ((st = decode_device(c, k, m, S, 1, pd, ob, pd + ob, rb, opres, rpres, 1, mode))) return st;
+  if (coding && (st = encode_device(c, k, m, S, 1, pd, ob, pd + ob + rb, rb))) return st;
+  AG_HIP(hipStreamSynchronize(c->stream));
+  std::memcpy(orig, pin, ob);
+  if (coding) std::memcpy(coding, pin + ob + rb, rb);
   return AG_RS_OK;
 }
 }  // namespace
@@ -1578,9 +1649,8 @@ int ag_rs_decoder_decode(ag_rs_decoder* d) {
   std::fill(d->restored.begin(), d->restored.end(), 0);
   if (d->no < d->k) {
     // exact crate semantics: decode from every present shard
-    const int st = ag_rs_decode_batch(d->ctx, d->k, d->m, d->S, 1, d->orig.data(), d->k * d->S, d->rec.data(),
-                                      d->m * d->S, d->opres.data(), d->rpres.data(), 1, AG_RS_DECODE_EXACT,
-                                      AG_RS_MEM_HOST);
+    const int st = run_one_decode(d->ctx, d->k, d->m, d->S, d->orig.data(), d->rec.data(), d->opres.data(),
+                                  d->rpres.data(), AG_RS_DECODE_EXACT, nullptr);
     if (st) return st;
     for (size_t i = 0; i < d->k; ++i) d->restored[i] = d->opres[i] ? 0 : 1;
   }
@@ -1702,26 +1772,29 @@ int ag_rs_coder_deshred(ag_rs_coder* c, size_t data_shreds, const uint8_t* const
     if (shreds[i] && (st = ag_rs_decoder_add_original_shard(c->dec, i, shreds[i], S))) return st;
   for (size_t j = data_shreds; j < kTotalShreds; ++j)
     if (shreds[j] && (st = ag_rs_decoder_add_recovery_shard(c->dec, j - data_shreds, shreds[j], S))) return st;
-  if ((st = ag_rs_decoder_decode(c->dec))) return st;
-  std::vector<uint8_t> data(kDataShreds * S);
-  size_t total = 0;
-  for (size_t i = 0; i < kDataShreds; ++i) {
-    const uint8_t* d = (i < data_shreds && shreds[i]) ? shreds[i] : c->dec->orig.data() + i * S;
-    if (total + S > kMaxAfterPadding) return AG_RS_ERR_TOO_MUCH_DATA;
-    std::memcpy(data.data() + i * S, d, S);
-    total += S;
-  }
+  ag_rs_decoder* dec = c->dec;
+  if (dec->no + dec->nr < kDataShreds) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
+  // decode and the re-encode of every coding shard (:206) in one device round trip; the
+  // completed originals (present ones as added, restored ones written back) are dec->orig
+  std::vector<uint8_t> coding(c->num_coding * S);
+  const bool coded = dec->no < kDataShreds;
+  if (coded && (st = run_one_decode(c->ctx, kDataShreds, c->num_coding, S, dec->orig.data(), dec->rec.data(),
+                                    dec->opres.data(), dec->rpres.data(), AG_RS_DECODE_EXACT, coding.data())))
+    return st;
+  // concatenation with the TooMuchData bound of :169-188 (exceeded iff 32 S > 32 768)
+  if (kDataShreds * S > kMaxAfterPadding) return AG_RS_ERR_TOO_MUCH_DATA;
+  const uint8_t* data = dec->orig.data();
+  const size_t total = kDataShreds * S;
   // strip padding: trailing zeros then the 0x80 marker
   size_t zeros = 0;
   while (zeros < total && data[total - 1 - zeros] == 0) ++zeros;
   const size_t padding = zeros + 1;
   if (padding > total || data[total - padding] != 0x80) return AG_RS_ERR_INVALID_PADDING;
   const size_t plen = total - padding;
-  std::vector<uint8_t> coding(c->num_coding * S);
-  if ((st = coder_encode(c, data.data(), S, coding.data()))) return st;
-  std::memcpy(payload_out, data.data(), plen);
+  if (!coded && (st = coder_encode(c, data, S, coding.data()))) return st;
+  std::memcpy(payload_out, data, plen);
   *payload_len = plen;
-  std::memcpy(data_out, data.data(), data.size());
+  std::memcpy(data_out, data, total);
   std::memcpy(coding_out, coding.data(), coding.size());
   *shred_bytes = S;
   return AG_RS_OK;
