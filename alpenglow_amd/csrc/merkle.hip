@@ -163,10 +163,16 @@ __global__ __launch_bounds__(256) void merkle_proof_kernel(const MerkleBuildPara
 
 // check_proof (merkle.rs:374-387, 417-428) for one leaf per thread; derive_root (:411-428)
 // when roots_out is set.
-template <bool A4>
+// LIST: thread i verifies leaf list[i] for i < list[n] (the compacted active leaves).
+template <bool A4, bool LIST>
 __global__ __launch_bounds__(256) void merkle_verify_kernel(const MerkleVerifyParams p) {
-  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= p.n || (p.active && !p.active[t])) return;
+  uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if constexpr (LIST) {
+    if (t >= p.list[p.n]) return;
+    t = p.list[t];
+  } else {
+    if (t >= p.n || (p.active && !p.active[t])) return;
+  }
   uint32_t node[8];
   leaf_hash<A4>(p.leaves + t * p.leaf_stride, p.leaf_bytes, node);
   uint32_t idx = p.index[t];
@@ -191,6 +197,21 @@ __global__ __launch_bounds__(256) void merkle_verify_kernel(const MerkleVerifyPa
 #pragma unroll
   for (int i = 0; i < 8; ++i) ok = ok && node[i] == root[i];
   p.ok[t] = ok ? 1 : 0;
+}
+
+// list[0 .. *count) = the t < n with active[t] != 0 (in no particular order): one atomic
+// per wave for its active lanes.
+__global__ __launch_bounds__(256) void compact_active_kernel(const uint8_t* __restrict__ active, uint64_t n,
+                                                             uint32_t* count, uint32_t* __restrict__ list) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool a = t < n && active[t] != 0;
+  const uint64_t m = __builtin_amdgcn_ballot_w64(a);
+  if (m == 0) return;
+  uint32_t base = 0;
+  if (lane == __builtin_ctzll(m)) base = atomicAdd(count, static_cast<uint32_t>(__builtin_popcountll(m)));
+  base = __shfl(base, __builtin_ctzll(m), 64);
+  if (a) list[base + __builtin_popcountll(m & ((uint64_t{1} << lane) - 1))] = static_cast<uint32_t>(t);
 }
 
 }  // namespace
@@ -225,8 +246,16 @@ hipError_t launch_merkle_verify(const MerkleVerifyParams& p, hipStream_t stream)
   if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const bool a16 = (reinterpret_cast<uintptr_t>(p.leaves) | p.leaf_stride) % 16 == 0;
   const dim3 grid(static_cast<unsigned>(groups));
-  if (a16) hipLaunchKernelGGL((merkle_verify_kernel<true>), grid, dim3(256), 0, stream, p);
-  else hipLaunchKernelGGL((merkle_verify_kernel<false>), grid, dim3(256), 0, stream, p);
+  if (p.active && p.list && p.n < 0xFFFFFFFFull) {
+    if (hipMemsetAsync(p.list + p.n, 0, 4, stream) != hipSuccess) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(compact_active_kernel, grid, dim3(256), 0, stream, p.active, p.n, p.list + p.n, p.list);
+    if (a16) hipLaunchKernelGGL((merkle_verify_kernel<true, true>), grid, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((merkle_verify_kernel<false, true>), grid, dim3(256), 0, stream, p);
+  } else if (a16) {
+    hipLaunchKernelGGL((merkle_verify_kernel<true, false>), grid, dim3(256), 0, stream, p);
+  } else {
+    hipLaunchKernelGGL((merkle_verify_kernel<false, false>), grid, dim3(256), 0, stream, p);
+  }
   return hipGetLastError();
 }
 

@@ -48,6 +48,8 @@ struct MerkleVerifyParams {
   uint8_t* ok;
   uint8_t* roots_out;  // derive_root mode (merkle.rs:411-428): root digests out, 32 B each; ok unused
   const uint8_t* active;  // nullable: leaves with active[t] == 0 are skipped (nothing written)
+  uint32_t* list;         // nullable, n + 1 words of device scratch: with `active`, the active
+                          // leaves are compacted first so that no lane idles on a skipped one
 };
 hipError_t launch_merkle_verify(const MerkleVerifyParams& p, hipStream_t stream);
 

@@ -2017,6 +2017,7 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
   mp.n = n;
   mp.roots_out = roots;
   mp.active = active;
+  mp.list = list;  // scratch until the signature list below reuses it (stream order)
   if (ag::launch_merkle_verify(mp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   // 2. SliceCommitment + cached-commitment rule (validated_shred.rs:57-64)
   AG_HIP(hipMemsetAsync(count, 0, 4, c->stream));

@@ -10,8 +10,9 @@
 //
 // Kernels: one wave per packet.  Lane 0 reads the fixed fields and the two lengths (the
 // offsets depend on data_len), the wave then copies the data, signature and proof bytes
-// lane-parallel (byte-granular: the data starts at offset 37, unaligned).  The packet bytes
-// are read once and the columns written once: HBM-bound, ~1.3 KB per shred each way.
+// lane-parallel: deserialize moves the data (at packet offset 37, unaligned) as 16-byte groups
+// of words funnel-shifted with v_alignbyte, the signature and proof bytes singly.  The packet bytes are
+// read once and the columns written once: ~1.3 KB per shred each way.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -34,6 +35,43 @@ __device__ __forceinline__ uint32_t ld_u32(const uint8_t* p) {
 __device__ __forceinline__ void st_u64(uint8_t* p, uint64_t v) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) p[i] = static_cast<uint8_t>(v >> (8 * i));
+}
+
+// Destination words [0, nw) from a source whose word w is (sw[w], sw[w + 1]) shifted right by
+// sh bytes (sh = 0: sw[w] itself; sw[nw] is read only when sh != 0).  Four words per lane
+// per step (dwordx4 accesses need only 4-byte alignment), the last partial group word by word.
+__device__ __forceinline__ void shift_words(uint32_t* __restrict__ dw, const uint32_t* __restrict__ sw, uint32_t nw,
+                                            uint32_t sh, int lane) {
+  for (uint32_t w = 4 * lane; w < nw; w += 256) {
+    if (w + 4 <= nw) {
+      const uint4 x = *reinterpret_cast<const uint4*>(sw + w);
+      uint4 o = x;
+      if (sh) {
+        const uint32_t e = sw[w + 4];
+        o.x = __builtin_amdgcn_alignbyte(x.y, x.x, sh);
+        o.y = __builtin_amdgcn_alignbyte(x.z, x.y, sh);
+        o.z = __builtin_amdgcn_alignbyte(x.w, x.z, sh);
+        o.w = __builtin_amdgcn_alignbyte(e, x.w, sh);
+      }
+      *reinterpret_cast<uint4*>(dw + w) = o;
+    } else {
+      for (uint32_t v = w; v < nw; ++v) dw[v] = sh ? __builtin_amdgcn_alignbyte(sw[v + 1], sw[v], sh) : sw[v];
+    }
+  }
+}
+// dst[0, len) = src[0, len) for a 4-byte-aligned dst and any src whose aligned base is
+// readable through src + len + 3 (the packet row continues past the data): whole words
+// funnel-shifted, the tail bytes singly.  Lane-parallel.
+__device__ __forceinline__ void copy_to_aligned(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src,
+                                                uint32_t len, int lane) {
+  const uint32_t mis = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(src) & 3);
+  const uint32_t nw = len >> 2;
+  shift_words(reinterpret_cast<uint32_t*>(dst), reinterpret_cast<const uint32_t*>(src - mis), nw, mis, lane);
+  for (uint32_t i = 4 * nw + lane; i < len; i += 64) dst[i] = src[i];
+}
+// the data rows are 4-byte aligned (every row, so word copies never leave a row)
+__device__ __forceinline__ bool word_rows(const ShredColumns& c) {
+  return ((reinterpret_cast<uintptr_t>(c.data) | c.data_stride) & 3) == 0;
 }
 
 __global__ __launch_bounds__(256) void shred_deserialize_kernel(const uint8_t* __restrict__ packets,
@@ -84,7 +122,8 @@ __global__ __launch_bounds__(256) void shred_deserialize_kernel(const uint8_t* _
   }
   if (st != kWireOk) return;
   uint8_t* dd = c.data + t * c.data_stride;
-  for (uint32_t i = lane; i < dlen; i += 64) dd[i] = pk[kShredHeadBytes + i];
+  if (word_rows(c)) copy_to_aligned(dd, pk + kShredHeadBytes, static_cast<uint32_t>(dlen), lane);
+  else for (uint32_t i = lane; i < dlen; i += 64) dd[i] = pk[kShredHeadBytes + i];
   c.sig[64 * t + lane] = pk[o_sig + lane];
   uint8_t* pp = c.proof + t * c.proof_stride;
   for (uint32_t i = lane; i < 32 * plen; i += 64) pp[i] = pk[o_sig + 72 + i];
@@ -117,6 +156,8 @@ __global__ __launch_bounds__(256) void shred_serialize_kernel(const ShredColumns
     packet_lens[t] = o_sig + 72 + 32 * plen;
   }
   const uint8_t* dd = c.data + t * c.data_stride;
+  // byte stores: the word-wide copy (copy_from_aligned) measured slower here, 4.1 vs 3.2 ms
+  // per 4 M datagrams on 1325-byte rows (profiles/r02_wire_copy_ab.json)
   for (uint32_t i = lane; i < dlen; i += 64) pk[kShredHeadBytes + i] = dd[i];
   pk[o_sig + lane] = c.sig[64 * h + lane];
   const uint8_t* pp = c.proof + t * c.proof_stride;

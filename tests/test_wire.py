@@ -93,7 +93,8 @@ def _cols(torch, rs, n, S_cap, H_cap, dev):
 
 
 @pytest.mark.gpu
-def test_gpu_serialize_matches_oracle(ctx):
+@pytest.mark.parametrize("stride", [1500, 1501])  # odd rows: every packet alignment for the word copies
+def test_gpu_serialize_matches_oracle(ctx, stride):
     import torch
     from alpenglow_amd import rs
     rng = random.Random(3)
@@ -117,7 +118,6 @@ def test_gpu_serialize_matches_oracle(ctx):
     t["data"].copy_(torch.from_numpy(data))
     t["proof"].copy_(torch.from_numpy(proof))
     t["sig"].copy_(torch.from_numpy(np.frombuffer(b"".join(s[6] for s in shreds), np.uint8).reshape(n, 64).copy()))
-    stride = 1500
     packets = torch.full((n, stride), 0xAB, dtype=torch.uint8, device=dev)
     lens = torch.zeros(n, dtype=torch.int32, device=dev)
     rs.shred_serialize_batch(ctx, n, c, packets, stride, lens)
@@ -138,7 +138,8 @@ def test_gpu_serialize_matches_oracle(ctx):
 
 
 @pytest.mark.gpu
-def test_gpu_deserialize_matches_oracle(ctx):
+@pytest.mark.parametrize("stride", [1600, 1603])
+def test_gpu_deserialize_matches_oracle(ctx, stride):
     import torch
     from alpenglow_amd import rs
     rng = random.Random(4)
@@ -151,7 +152,7 @@ def test_gpu_deserialize_matches_oracle(ctx):
         pkts.extend(huge_proof_len_variants(b))  # u64 wrap of 32 * proof_len (always included)
     big = wo.serialize(*_shred(rng, S=1024, height=10))   # valid, but wider than the proof rows
     pkts.append(big)
-    n, stride = len(pkts), 1600
+    n = len(pkts)
     buf = np.zeros((n, stride), np.uint8)
     for i, b in enumerate(pkts):
         buf[i, :len(b)] = np.frombuffer(b, np.uint8)
