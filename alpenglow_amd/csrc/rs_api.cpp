@@ -156,6 +156,7 @@ struct ag_rs_ctx {
   DevBuf d_slice_meta;                           // slice framing / parsing metadata
   DevBuf stage_pad, stage_mask;                  // restrided shards (sizes not whole 64-byte chunks)
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
+  DevBuf d_pipe_few, d_pipe_mask;           // composed deshred: too-few flags, re-encode store masks
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
   static constexpr int kPipeBufs = 25;
   DevBuf pipe[kPipeBufs];                   // composed shredder scratch (ag_shredder_*_batch)
@@ -240,7 +241,7 @@ struct ag_rs_ctx {
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
                       &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
-                      &one_out})
+                      &one_out, &d_pipe_few, &d_pipe_mask})
       b->release();
     for (DevBuf& b : pipe) b.release();
     one_pin.release();
@@ -2267,6 +2268,87 @@ bool pipe_args_ok(size_t nslices, size_t S, const uint8_t* codewords, const uint
 
 }  // namespace
 
+namespace {
+// A/B aid: AG_PIPE_HOST_CODER=1 keeps the host-pattern coder path (ag_rs_coder_deshred_batch).
+bool pipe_device_coder() {
+  static const bool dev = [] {
+    const char* e = std::getenv("AG_PIPE_HOST_CODER");
+    return !(e && e[0] == '1');
+  }();
+  return dev;
+}
+// ReedSolomonCoder::deshred (reed_solomon.rs:140-208, ANY_K) over the kept shreds of every
+// slice without a host round trip, for whole-chunk shreds (S % 64 == 0): the per-slice
+// patterns come from the kept-shred masks on the device (launch_pipe_patterns), the per-lane
+// window decoder restores the data shreds, coder_strip finds each payload's padding, and the
+// 32-point encode rewrites the coding shreds of the slices that decoded and stripped (store
+// masks per slice; the others keep theirs).  plen[s] as ag_rs_coder_deshred_batch: the
+// payload length, or -NotEnoughShreds / -InvalidPadding.
+int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
+                       int64_t* plen) {
+  constexpr size_t k = kDataShreds, W = 64;
+  const size_t cps = S / 64;
+  int st;
+  if ((st = c->ensure_tables()) || (st = c->d_xmask.ensure(3 * n * 8, c->stream)) ||
+      (st = c->d_rows.ensure(n * W * 16 * 4, c->stream)) || (st = c->d_pipe_few.ensure(n, c->stream)) ||
+      (st = c->d_pipe_mask.ensure(8 * n, c->stream)) || (st = c->d_strip.ensure(8 * n, c->stream)))
+    return st;
+  c->xmask_host.clear();  // d_xmask / d_rows no longer hold decode_device's cached patterns
+  c->xmask_w = 0;
+  uint64_t* xm = c->d_xmask.as<uint64_t>();
+  uint8_t* few = c->d_pipe_few.as<uint8_t>();
+  if (ag::launch_pipe_patterns(d_present, n, xm, few, c->stream) != hipSuccess ||
+      ag::launch_decode_rows(xm, xm + n, static_cast<uint32_t>(n), static_cast<uint32_t>(W), c->dtables(),
+                             c->d_rows.as<uint32_t>(), c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  ag::DecodeXParams p{};
+  p.rec = cw + k * S;
+  p.rec_block_stride = cw_stride;
+  p.rec_shard_stride = S;
+  p.orig = cw;
+  p.orig_block_stride = cw_stride;
+  p.orig_shard_stride = S;
+  p.pmask = xm + n;
+  p.rows = c->d_rows.as<uint32_t>();
+  p.k = static_cast<uint32_t>(k);
+  p.m = 32;
+  p.chunk = 32;
+  p.low_rate = 0;
+  p.chunks_per_shard = static_cast<uint32_t>(cps);
+  p.total_columns = static_cast<uint64_t>(n) * cps;
+  p.per_lane = 1;
+  if (ag::launch_decode_x(static_cast<unsigned>(W), p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  int64_t* strip = c->d_strip.as<int64_t>();
+  if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(k * S), n, strip, c->stream) != hipSuccess ||
+      ag::launch_pipe_store_masks(few, strip, n, c->d_pipe_mask.as<uint64_t>(), c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  ag::XformParams xp{};
+  xp.in = cw;
+  xp.in_block_stride = cw_stride;
+  xp.in_shard_stride = S;
+  xp.out = cw + k * S;
+  xp.out_block_stride = cw_stride;
+  xp.out_shard_stride = S;
+  xp.out_mask = c->d_pipe_mask.as<uint64_t>();
+  xp.pattern_per_block = 1;
+  xp.n_in = static_cast<uint32_t>(k);
+  xp.n_out = 32;
+  xp.chunks_per_shard = static_cast<uint32_t>(cps);
+  xp.total_columns = static_cast<uint64_t>(n) * cps;
+  if (ag::launch_xform(ag::XformKind::kEncode32, xp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  std::vector<uint8_t> hfew(n);
+  AG_HIP(hipMemcpyAsync(plen, strip, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipMemcpyAsync(hfew.data(), few, n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipStreamSynchronize(c->stream));
+  for (size_t s = 0; s < n; ++s) {
+    if (hfew[s]) plen[s] = -AG_RS_ERR_NOT_ENOUGH_SHARDS;
+    else if (plen[s] < 0) plen[s] = -AG_RS_ERR_INVALID_PADDING;
+  }
+  return AG_RS_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int ag_shredder_shred_batch(ag_rs_ctx* c, size_t nslices, size_t S, const uint8_t* parent_flags,
@@ -2438,18 +2520,22 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   AG_HIP(hipMemcpyAsync(h_last.data(), slast, n, hipMemcpyDeviceToHost, c->stream));
   AG_HIP(hipStreamSynchronize(c->stream));
   // 4. ReedSolomonCoder::deshred over the kept shreds (restores the data shreds, re-encodes
-  //    all coding shreds, strips the padding)
-  std::vector<uint8_t> dp(n * ag::kPipeData), cp(n * (ag::kPipeShreds - ag::kPipeData));
-  for (size_t s = 0; s < n; ++s)
-    for (uint32_t j = 0; j < ag::kPipeShreds; ++j) {
-      const uint8_t bit = static_cast<uint8_t>((h_present[s] >> j) & 1);
-      if (j < ag::kPipeData) dp[s * ag::kPipeData + j] = bit;
-      else cp[s * (ag::kPipeShreds - ag::kPipeData) + j - ag::kPipeData] = bit;
-    }
+  //    all coding shreds, strips the padding); on the device for whole-chunk shreds
   std::vector<int64_t> plen(n);
-  if ((st = ag_rs_coder_deshred_batch(c, ag::kPipeShreds - ag::kPipeData, n, S, codewords, cw_stride, dp.data(),
-                                      cp.data(), AG_RS_DECODE_ANY_K, plen.data())))
-    return st;
+  if (S % 64 == 0 && pipe_device_coder()) {
+    if ((st = pipe_coder_deshred(c, n, S, codewords, cw_stride, d_present, plen.data()))) return st;
+  } else {
+    std::vector<uint8_t> dp(n * ag::kPipeData), cp(n * (ag::kPipeShreds - ag::kPipeData));
+    for (size_t s = 0; s < n; ++s)
+      for (uint32_t j = 0; j < ag::kPipeShreds; ++j) {
+        const uint8_t bit = static_cast<uint8_t>((h_present[s] >> j) & 1);
+        if (j < ag::kPipeData) dp[s * ag::kPipeData + j] = bit;
+        else cp[s * (ag::kPipeShreds - ag::kPipeData) + j - ag::kPipeData] = bit;
+      }
+    if ((st = ag_rs_coder_deshred_batch(c, ag::kPipeShreds - ag::kPipeData, n, S, codewords, cw_stride, dp.data(),
+                                        cp.data(), AG_RS_DECODE_ANY_K, plen.data())))
+      return st;
+  }
   // 5. check_merkle_tree: the rebuilt tree's root must be the signed one; its paths serve
   //    the reconstructed datagrams
   if ((st = ag_merkle_build_batch(c, ag::kPipeShreds, S, n, codewords, S, cw_stride, roots2, nullptr, 0, proof,

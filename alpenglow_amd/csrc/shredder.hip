@@ -121,6 +121,37 @@ __global__ __launch_bounds__(256) void pipe_merge_kernel(const uint32_t* fresh, 
 
 dim3 grid256(uint64_t n) { return dim3(static_cast<unsigned>((n + 255) / 256)); }
 
+// ANY_K survivors of one slice's kept shreds in the W = 64 window (decode_device's rule).
+__global__ __launch_bounds__(256) void pipe_patterns_kernel(const uint64_t* __restrict__ present, uint64_t n,
+                                                            uint64_t* __restrict__ xm, uint8_t* __restrict__ few) {
+  const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint64_t pr = present[s];
+  const uint64_t ob = pr & 0xFFFFFFFFull;
+  uint64_t rb = pr >> 32;
+  const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(pr));
+  uint64_t in = 0, out = 0, e = 0;
+  if (cnt >= kPipeData && ob != 0xFFFFFFFFull) {
+    const uint32_t budget = kPipeData - static_cast<uint32_t>(__builtin_popcountll(ob));
+    while (static_cast<uint32_t>(__builtin_popcountll(rb)) > budget) rb &= ~(uint64_t{1} << (63 - __builtin_clzll(rb)));
+    in = rb | (ob << 32);
+    out = (~ob & 0xFFFFFFFFull) << 32;
+    e = (~rb & 0xFFFFFFFFull) | out;
+  }
+  xm[s] = e;
+  xm[n + 2 * s] = in;
+  xm[n + 2 * s + 1] = out;
+  few[s] = cnt < kPipeData ? 1 : 0;
+}
+
+__global__ __launch_bounds__(256) void pipe_store_mask_kernel(const uint8_t* __restrict__ few,
+                                                              const int64_t* __restrict__ strip, uint64_t n,
+                                                              uint64_t* __restrict__ mask) {
+  const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  mask[s] = (!few[s] && strip[s] >= 0) ? ~uint64_t{0} : uint64_t{0};
+}
+
 }  // namespace
 
 hipError_t launch_pipe_expand(const PipeExpandParams& p, hipStream_t stream) {
@@ -166,6 +197,20 @@ hipError_t launch_pipe_merge_lens(const uint32_t* fresh, const uint64_t* present
   if (n == 0) return hipSuccess;
   hipLaunchKernelGGL(pipe_merge_kernel, grid256(n), dim3(256), 0, stream, fresh, present, slice_ok, nslices,
                      packet_lens);
+  return hipGetLastError();
+}
+
+hipError_t launch_pipe_patterns(const uint64_t* present, uint64_t nslices, uint64_t* xm, uint8_t* few,
+                                hipStream_t stream) {
+  if (nslices == 0) return hipSuccess;
+  hipLaunchKernelGGL(pipe_patterns_kernel, grid256(nslices), dim3(256), 0, stream, present, nslices, xm, few);
+  return hipGetLastError();
+}
+
+hipError_t launch_pipe_store_masks(const uint8_t* few, const int64_t* strip, uint64_t nslices, uint64_t* mask,
+                                   hipStream_t stream) {
+  if (nslices == 0) return hipSuccess;
+  hipLaunchKernelGGL(pipe_store_mask_kernel, grid256(nslices), dim3(256), 0, stream, few, strip, nslices, mask);
   return hipGetLastError();
 }
 

@@ -84,4 +84,19 @@ hipError_t launch_pipe_root_cmp(const uint8_t* a, const uint8_t* b, uint64_t nsl
 hipError_t launch_pipe_merge_lens(const uint32_t* fresh, const uint64_t* present, const uint8_t* slice_ok,
                                   uint64_t nslices, uint32_t* packet_lens, hipStream_t stream);
 
+// The ReedSolomonCoder::deshred patterns of the kept shreds on the device (32:32 HighRate,
+// window W = 64: recovery j at position j, original i at 32 + i), for the per-lane decode_x
+// kernel (the patterns rs_api.cpp's decode_device builds on the host for ANY_K):
+//   xm[s] = erased positions (locator), xm[n + 2 s] = survivors loaded (the present originals,
+//   then recovery shards in index order up to 32), xm[n + 2 s + 1] = originals restored.
+// Slices with fewer than 32 kept shreds, or nothing to restore, get empty masks (no loads, no
+// stores); few[s] = 1 for the former (NotEnoughShreds, reed_solomon.rs:144).
+hipError_t launch_pipe_patterns(const uint64_t* present, uint64_t nslices, uint64_t* xm, uint8_t* few,
+                                hipStream_t stream);
+// mask[s] = ~0 (store every coding shard of the re-encode) when the slice decoded and its
+// padding stripped (few[s] == 0 and strip[s] >= 0), else 0 (the coding shreds stay as they
+// are, like the reference's early returns).
+hipError_t launch_pipe_store_masks(const uint8_t* few, const int64_t* strip, uint64_t nslices, uint64_t* mask,
+                                   hipStream_t stream);
+
 }  // namespace ag
