@@ -15,7 +15,8 @@ namespace ag {
 namespace {
 
 // One 256-thread workgroup per slice; each thread writes whole dwords of the framed
-// payload (header bytes, data bytes, and zeros past the end up to the next dword).
+// payload (header bytes, data bytes, and zeros past the end up to the next dword), four at
+// a time where they are all data.
 __global__ __launch_bounds__(256) void slice_frame_kernel(const SliceFrameParams p) {
   const uint64_t b = blockIdx.x;
   if (b >= p.n) return;
@@ -33,9 +34,33 @@ __global__ __launch_bounds__(256) void slice_frame_kernel(const SliceFrameParams
     const uint32_t k = i - (hdr - 8);  // byte k of the u64 LE length
     return k < 4 ? (len >> (8 * k)) & 0xFFu : 0u;
   };
-  for (uint32_t w = threadIdx.x; 4 * w < total; w += blockDim.x) {
+  auto word_at = [&](uint32_t w) {
     const uint32_t i = 4 * w;
-    dst[w] = byte_at(i) | (byte_at(i + 1) << 8) | (byte_at(i + 2) << 16) | (byte_at(i + 3) << 24);
+    return byte_at(i) | (byte_at(i + 1) << 8) | (byte_at(i + 2) << 16) | (byte_at(i + 3) << 24);
+  };
+  // Groups of four destination words.  A group wholly inside the data, with its source words
+  // inside the data row, is five aligned source words funnel-shifted by the header length
+  // (v_alignbyte); the rest (header, the last words) go byte by byte.
+  const bool wsrc = ((reinterpret_cast<uintptr_t>(p.data) | p.data_stride) & 3) == 0;
+  const uint32_t nwords = (total + 3) / 4;
+  const uint32_t* sw = reinterpret_cast<const uint32_t*>(src);
+  for (uint32_t g = threadIdx.x; 4 * g < nwords; g += blockDim.x) {
+    const uint32_t w0 = 4 * g, i0 = 4 * w0;
+    if (wsrc && i0 >= hdr && i0 + 16 <= total && (i0 - hdr) + 20 <= p.data_stride) {
+      const uint32_t j = i0 - hdr, sh = j & 3, q = j >> 2;
+      const uint4 x = *reinterpret_cast<const uint4*>(sw + q);  // 4-byte aligned: fine for dwordx4
+      const uint32_t e = sw[q + 4];
+      uint4 o = x;
+      if (sh) {
+        o.x = __builtin_amdgcn_alignbyte(x.y, x.x, sh);
+        o.y = __builtin_amdgcn_alignbyte(x.z, x.y, sh);
+        o.z = __builtin_amdgcn_alignbyte(x.w, x.z, sh);
+        o.w = __builtin_amdgcn_alignbyte(e, x.w, sh);
+      }
+      *reinterpret_cast<uint4*>(dst + w0) = o;
+    } else {
+      for (uint32_t w = w0; w < w0 + 4 && w < nwords; ++w) dst[w] = word_at(w);
+    }
   }
 }
 
