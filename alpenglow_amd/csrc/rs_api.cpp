@@ -352,6 +352,63 @@ const uint16_t* full_window_x32() {
 // shards L (1 <= |L| <= kCorrMaxSyn).  Syndrome points: virtual zeros k..31 first (no
 // load), then present originals in index order.  False if the pattern does not fit (the
 // caller takes another decoder).
+// decode_c's balanced correction (rs_decode_c.hip), decided per pattern: layout H0 gives wave
+// w the positions 2w, 16 + 2w, 2w + 1, 17 + 2w (slots 0..3).  Every wave keeps at most
+// quota = ceil(|E| / 8) of its own restored originals (lowest slots first); the surplus, in
+// ascending position order, is dealt to the waves below quota (ascending wave order), which
+// accumulate it in their free slots (ascending slot order) and return the sums through LDS
+// slot = the output's donation rank.
+void corr_assign(ag::CorrPattern* cp) {
+  auto pos = [](uint32_t w, uint32_t t) { return (t & 1 ? 16u : 0u) + 2 * w + (t >> 1); };
+  const uint64_t em = cp->emask;
+  const uint32_t ne = static_cast<uint32_t>(__builtin_popcountll(em & 0xFFFFFFFFull));
+  const uint32_t quota = (ne + 7) >> 3;
+  auto rank = [&](uint64_t m, uint32_t a) {
+    return static_cast<uint32_t>(__builtin_popcountll(m & ((uint64_t{1} << a) - 1)));
+  };
+  uint32_t own[8], donated[8], cap[8];
+  uint64_t dmask = 0;
+  for (uint32_t w = 0; w < 8; ++w) {
+    own[w] = 0;
+    for (uint32_t t = 0; t < 4; ++t)
+      if ((em >> pos(w, t)) & 1) own[w] |= 1u << t;
+    uint32_t m = own[w];
+    for (uint32_t q = 0; q < quota && m; ++q) m &= m - 1;
+    donated[w] = m;
+    for (uint32_t t = 0; t < 4; ++t)
+      if ((m >> t) & 1) dmask |= uint64_t{1} << pos(w, t);
+    const uint32_t c = static_cast<uint32_t>(__builtin_popcount(own[w]));
+    cap[w] = c < quota ? quota - c : 0;
+  }
+  const uint32_t nd = static_cast<uint32_t>(__builtin_popcountll(dmask));
+  uint64_t rem = dmask;
+  uint32_t d = 0;
+  for (uint32_t w = 0; w < 8; ++w) {
+    uint32_t act = 0, foreign = 0;
+    for (uint32_t t = 0; t < 4; ++t) {
+      uint32_t a = 64, lds = 0;
+      if (((own[w] & ~donated[w]) >> t) & 1) {
+        a = pos(w, t);
+      } else if ((donated[w] >> t) & 1) {
+        lds = rank(dmask, pos(w, t));
+      } else if (!((own[w] >> t) & 1) && cap[w] && d < nd) {
+        a = static_cast<uint32_t>(__builtin_ctzll(rem));
+        rem &= rem - 1;
+        lds = d++;
+        --cap[w];
+        foreign |= 1u << t;
+      }
+      uint32_t kofs = 0;
+      if (a < 64) {
+        act |= 1u << t;
+        kofs = ag::kCorrPairWords * rank(em, a) * cp->ns;
+      }
+      cp->wslot[w][t] = kofs | (lds << 20);
+    }
+    cp->wsum[w] = act | (own[w] << 4) | (donated[w] << 8) | (foreign << 12) | ((nd ? 1u : 0u) << 16);
+  }
+}
+
 bool build_corr_pattern(size_t k, const uint8_t* opres, const uint8_t* rpres, ag::CorrPattern* cp,
                         std::vector<uint32_t>& pool) {
   const uint16_t* X = full_window_x32();
@@ -379,6 +436,7 @@ bool build_corr_pattern(size_t k, const uint8_t* opres, const uint8_t* rpres, ag
   std::sort(D, D + nd);
   cp->ne = static_cast<uint32_t>(ne);
   cp->ns = static_cast<uint32_t>(nl);
+  corr_assign(cp);
   // N = X[D, L], K = X[E, L] N^-1
   std::vector<uint16_t> N(nl * nl), K(ne * nl, 0);
   for (size_t b = 0; b < nl; ++b)

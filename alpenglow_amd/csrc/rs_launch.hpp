@@ -90,6 +90,14 @@ struct CorrPattern {
   uint64_t smask;  // original-coset points used as syndromes: present originals (< k) or virtual zeros
   uint32_t ne, ns;  // |E|, |L| = number of syndromes
   uint64_t kofs;    // K picks at kpool + kofs, pair (a, b) (a < ne, b < ns) at + 64 * (a * ns + b)
+  // The balanced correction's assignment (decode_c, layout H0), per wave w:
+  //   wsum[w]: bits 0-3 slots that accumulate K s (own kept or foreign), 4-7 slots holding own
+  //            restored originals (stored at the end), 8-11 own outputs donated to other
+  //            waves, 12-15 slots accumulating a foreign output; bit 16: the pattern donates
+  //   wslot[w][t]: bits 0-19 the slot's K row offset (kCorrPairWords * rank * ns), bits
+  //            20-24 its LDS exchange slot (foreign: written; donated: read)
+  uint32_t wsum[8];
+  uint32_t wslot[8][4];
 };
 // K[a][b] as table picks: for group pair gp (input planes 8gp..8gp+7) and output plane o,
 // dwords [32 gp + 2 o] and [32 gp + 2 o + 1] are the 4-bit indices (row o of K[a][b]'s
@@ -111,7 +119,6 @@ struct DecodeCParams {
   uint32_t chunks_per_shard;
   uint64_t total_columns;  // batch blocks * chunks_per_shard
   uint64_t ntiles;         // 64-column tiles processed
-  uint32_t balance;        // set by the launcher: spread the restored originals over the waves
 };
 hipError_t launch_decode_c(const DecodeCParams& p, hipStream_t stream);
 
