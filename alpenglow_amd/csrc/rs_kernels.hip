@@ -595,7 +595,8 @@ __device__ __forceinline__ void xf_derivative(int wave, int lane, uint4* lds, Re
 
 // x <- M x for a runtime matrix that differs per lane (per-lane erasure patterns): rows
 // are this lane's 16 row words; every term is one v_bitop3 with a v_bfe_i32 mask.
-__device__ __forceinline__ void mul_rt_lane(uint32_t* x, const uint32_t* __restrict__ rows) {
+template <typename RowPtr>
+__device__ __forceinline__ void mul_rt_lane(uint32_t* x, RowPtr rows) {
   uint32_t r[16];
   static_for<4>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
@@ -726,6 +727,191 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
         mul_rt_dx(ra[t], rows + j * 16);
 #endif
         store_shard(dst, io_o, io_o.valid, ra[t]);
+      }
+    }
+  });
+}
+
+// =====================================================================================
+// decode_x16<PL>: the W = 64 window decoder (decode_x's algorithm) on xform16's layout:
+// 16 waves x 4 slots, one 1024-thread workgroup per CU at 4 waves/SIMD (decode_x<8> keeps 8
+// slots per lane at 216 VGPRs: 2 waves/SIMD and one 8-wave workgroup per CU, latency-bound).
+// Positions by layout (X8Lay: slot bits | wave bits):
+//   G0 slots p0 p1 | waves p2 p3 p4 p5   loads + locator multiplies, IFFT b0 b1; FFT b0, stores
+//   G1 slots p2 p1 | waves p0 p3 p4 p5   IFFT b2 / FFT b1
+//   G2 slots p2 p3 | waves p0 p1 p4 p5   IFFT b3 / FFT b2
+//   G3 slots p4 p3 | waves p0 p1 p2 p5   IFFT b4 / FFT b3
+//   G4 slots p4 p5 | waves p0 p1 p2 p3   IFFT b5, formal derivative, FFT b5 b4
+// The derivative w'[j] = w[j] ^ XOR_{b : bit b of j clear} w[j | 2^b] (pre-derivative terms)
+// in G4: slot bits in-lane, wave bits from the partner waves' pre-derivative copies in LDS,
+// two slots per round (2 x 128 KiB would not fit).
+// =====================================================================================
+template <bool PL>
+__global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams p) {
+  using G0 = X8Lay<0, 1, 2, 3, 4, 5>;
+  using G1 = X8Lay<2, 1, 0, 3, 4, 5>;
+  using G2 = X8Lay<2, 3, 0, 1, 4, 5>;
+  using G3 = X8Lay<4, 3, 0, 1, 2, 5>;
+  using G4 = X8Lay<4, 5, 0, 1, 2, 3>;
+  constexpr int W = 64;
+  __shared__ uint4 lds[32 * 4 * kXfLanes];  // 16 waves x 2 slots x 4 KiB
+  __shared__ XFlags<16> flags;
+  // PL with 16 or 32 chunks per shard: the tile's 4 (2) blocks' multiply rows, staged once
+  // by the workgroup (one 16-byte load per thread) instead of 48 dependent 64-byte loads
+  // per lane, each exposing its latency to the product that waits on it
+  __shared__ uint4 lrows[4 * W * 4];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
+  const bool staged = PL && (p.chunks_per_shard == 16 || p.chunks_per_shard == 32);
+  if (staged) {
+    const uint32_t nbt = kXfLanes / p.chunks_per_shard;
+    const uint64_t b0 = static_cast<uint64_t>(tile) * kXfLanes / p.chunks_per_shard;
+    const uint64_t nblocks = p.total_columns / p.chunks_per_shard;
+    const uint32_t lb = threadIdx.x / (W * 4);
+    if (lb < nbt && b0 + lb < nblocks)
+      lrows[threadIdx.x] = reinterpret_cast<const uint4*>(p.rows + (b0 + lb) * (W * 16))[threadIdx.x % (W * 4)];
+  }
+  if (threadIdx.x < 32) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
+  __syncthreads();
+  uint64_t in_mask, out_mask;
+  const uint32_t* rows;
+  const uint4* rows_l = lrows;
+  TileIO io_r, io_o;
+  uint64_t off_r = 0, off_o = 0;
+  if constexpr (PL) {
+    const uint64_t gc = static_cast<uint64_t>(tile) * kXfLanes + lane;
+    const bool ok = gc < p.total_columns;
+    const uint64_t blk = ok ? gc / p.chunks_per_shard : 0;
+    const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
+    in_mask = ok ? p.pmask[2 * blk] : 0;
+    out_mask = ok ? p.pmask[2 * blk + 1] : 0;
+    rows = p.rows + blk * (W * 16);
+    rows_l = lrows + (lane / p.chunks_per_shard) * (W * 4);  // staged: the lane's block in the tile
+    off_r = blk * p.rec_block_stride + col * 64;
+    off_o = blk * p.orig_block_stride + col * 64;
+  } else {
+    uint64_t vtile = tile, pat = 0;
+    if (p.per_block) {
+      const uint64_t bi = tile / p.tiles_per_block;
+      const uint64_t blk = p.block_ids ? p.block_ids[bi] : bi;
+      vtile = blk * p.tiles_per_block + (tile - bi * p.tiles_per_block);
+      pat = blk;
+    }
+    in_mask = p.pmask[2 * pat];
+    out_mask = p.pmask[2 * pat + 1];
+    rows = p.rows + pat * (W * 16);
+    io_r = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.rec_block_stride);
+    io_o = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.orig_block_stride);
+  }
+  const uint32_t opos = p.low_rate ? 0 : p.chunk, rpos = p.low_rate ? p.chunk : 0;
+  Regs4 r;
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = 4 * wave + t;  // G0 position (wave-uniform)
+    if ((in_mask >> j) & 1) {          // PL: per lane
+      const bool is_rec = p.low_rate ? j >= p.chunk : j < p.chunk;
+      const uint8_t* base = is_rec ? p.rec + (j - rpos) * p.rec_shard_stride : p.orig + (j - opos) * p.orig_shard_stride;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint8_t* src;
+        if constexpr (PL) src = base + (is_rec ? off_r : off_o) + 16 * q;
+        else src = base + (is_rec ? io_r.off[q] : io_o.off[q]);
+        const uint4 x = *reinterpret_cast<const uint4*>(src);
+        r[t][4 * q] = x.x;
+        r[t][4 * q + 1] = x.y;
+        r[t][4 * q + 2] = x.z;
+        r[t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { r[t][decltype(P)::value] = 0; });
+    }
+  });
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = 4 * wave + t;
+    if ((in_mask >> j) & 1) {
+      if constexpr (!PL) swap_halves(r[t]);
+      dev::planes_from_raw(r[t]);
+      if constexpr (PL) {
+        if (staged) mul_rt_lane(r[t], rows_l + 4 * j); else mul_rt_lane(r[t], rows + j * 16);
+      } else {
+        mul_rt_dx(r[t], rows + j * 16);
+      }
+    }
+  });
+  // IFFT_64 (skew delta 0)
+  x8_layer_t<G0, 0, true, 0>(wave, r);
+  x8_layer_t<G0, 1, true, 0>(wave, r);
+  x8_swap<0, 0, 1>(wave, lane, lds, &flags, r);
+  x8_layer_t<G1, 2, true, 0>(wave, r);
+  x8_swap<1, 1, 2>(wave, lane, lds, &flags, r);
+  x8_layer_t<G2, 3, true, 0>(wave, r);
+  x8_swap<0, 2, 3>(wave, lane, lds, &flags, r);
+  x8_layer_t<G3, 4, true, 0>(wave, r);
+  x8_swap<1, 3, 4>(wave, lane, lds, &flags, r);
+  x8_layer_t<G4, 5, true, 0>(wave, r);
+  // formal derivative in G4 (slot t: position bits p4 = t & 1, p5 = t >> 1; wave bits p0..p3)
+  __syncthreads();  // every wave's swap reads are done: the exchange buffer is free
+  static_for<2>([&](auto Rho) {
+    constexpr int rho = decltype(Rho)::value;
+    // slot = 2 * wave + u holds this wave's pre-derivative slot 2 rho + u
+    static_for<2>([&](auto U) { lds_put(lds, 2 * wave + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+    // slot-bit terms of slots 2 rho, 2 rho + 1 from pre-derivative partners (ascending t: a
+    // partner t | 2^i > t is unmodified; slots 2, 3 are untouched until round 1)
+    static_for<2>([&](auto U) {
+      constexpr int t = 2 * rho + decltype(U)::value;
+      if constexpr (!(t & 1)) dev::xor_planes(r[t], r[t | 1]);
+      if constexpr (!(t & 2)) dev::xor_planes(r[t], r[t | 2]);
+    });
+    __syncthreads();
+    static_for<4>([&](auto B) {
+      constexpr int b = decltype(B)::value;
+      if (!((wave >> b) & 1)) {
+        const int pw = wave | (1 << b);
+        static_for<2>([&](auto U) {
+          constexpr int u = decltype(U)::value;
+          static_for<4>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            const uint4 x = lds[((2 * pw + u) * 4 + q) * kXfLanes + lane];
+            r[2 * rho + u][4 * q] ^= x.x;
+            r[2 * rho + u][4 * q + 1] ^= x.y;
+            r[2 * rho + u][4 * q + 2] ^= x.z;
+            r[2 * rho + u][4 * q + 3] ^= x.w;
+          });
+        });
+      }
+    });
+    __syncthreads();
+  });
+  // FFT_64 (skew delta 0), ending in G0
+  x8_layer_t<G4, 5, false, 0>(wave, r);
+  x8_layer_t<G4, 4, false, 0>(wave, r);
+  x8_swap<1, 3, 5>(wave, lane, lds, &flags, r);
+  x8_layer_t<G3, 3, false, 0>(wave, r);
+  x8_swap<0, 2, 6>(wave, lane, lds, &flags, r);
+  x8_layer_t<G2, 2, false, 0>(wave, r);
+  x8_swap<1, 1, 7>(wave, lane, lds, &flags, r);
+  x8_layer_t<G1, 1, false, 0>(wave, r);
+  x8_swap<0, 0, 8>(wave, lane, lds, &flags, r);
+  const uint32_t mine = static_cast<uint32_t>(out_mask >> (4 * wave)) & 0xF;
+  if constexpr (PL) {
+    if (__builtin_amdgcn_ballot_w64(mine != 0) == 0) return;  // nothing to restore in this wave
+  } else {
+    if (mine == 0) return;
+  }
+  x8_layer_t<G0, 0, false, 0>(wave, r);
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = 4 * wave + t;
+    if ((out_mask >> j) & 1) {
+      uint8_t* dst = p.orig + (j - opos) * p.orig_shard_stride;
+      if constexpr (PL) {
+        if (staged) mul_rt_lane(r[t], rows_l + 4 * j); else mul_rt_lane(r[t], rows + j * 16);
+        dev::store_chunk(dst + off_o, r[t]);
+      } else {
+        mul_rt_dx(r[t], rows + j * 16);
+        store_shard(dst, io_o, io_o.valid, r[t]);
       }
     }
   });
@@ -1517,8 +1703,14 @@ hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, 
       else hipLaunchKernelGGL((decode_x_kernel<4>), grid, dim3(256), 0, stream, p);
       break;
     case 64:
-      if (pl) hipLaunchKernelGGL((decode_x_kernel<8, true>), grid, dim3(512), 0, stream, p);
-      else hipLaunchKernelGGL((decode_x_kernel<8>), grid, dim3(512), 0, stream, p);
+      // the 16-wave layout (decode_x16); A/B variant 15 = decode_x<8>
+      if (xform_variant() == 15) {
+        if (pl) hipLaunchKernelGGL((decode_x_kernel<8, true>), grid, dim3(512), 0, stream, p);
+        else hipLaunchKernelGGL((decode_x_kernel<8>), grid, dim3(512), 0, stream, p);
+      } else {
+        if (pl) hipLaunchKernelGGL((decode_x16_kernel<true>), grid, dim3(1024), 0, stream, p);
+        else hipLaunchKernelGGL((decode_x16_kernel<false>), grid, dim3(1024), 0, stream, p);
+      }
       break;
     default: return hipErrorInvalidValue;
   }
