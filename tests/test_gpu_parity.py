@@ -877,4 +877,36 @@ def test_lowrate_window_decode(ctx, dev, k, m, S):
             if j not in keep_r:
                 d_r[b, j] = 0x22
     got = gpu_decode(ctx, dev, d_o, d_r, op, rp, rs.DECODE_ANY_K)
-    assert np.array_equal(got, blocks)
+    assert np.array_equal(got, blocks)@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [0, 7])
+def test_decoder_crate_api_exact_semantics(ctx, extra):
+    """The per-call decoder (zero-copy path) keeps the crate's EXACT results on arbitrary
+    bytes: with exactly k shards present (extra = 0) any bytes fix one codeword, so the ANY_K
+    kernels it then uses must agree with the crate's decoder; with surplus shards (extra = 7)
+    and one tampered recovery shard the crate's every-shard algorithm must be reproduced."""
+    k, m, S = 32, 32, 1024
+    rng = np.random.default_rng(90 + extra)
+    orig = rng.integers(0, 256, (k, S), dtype=np.uint8)
+    rec = ro_c.encode(orig, m)
+    if extra:
+        rec[3, 17] ^= 0x5A  # inconsistent input
+    else:
+        rec = rng.integers(0, 256, (m, S), dtype=np.uint8)  # not a codeword with orig at all
+    op = np.zeros(k, np.uint8)
+    op[rng.choice(k, 12, replace=False)] = 1
+    rp = np.zeros(m, np.uint8)
+    rp[rng.choice(m, k - 12 + extra, replace=False)] = 1
+    damaged = (orig * op[:, None]).astype(np.uint8)
+    want = ro_c.decode(damaged, op, rec, rp)
+    dec = rs.ReedSolomonDecoder(ctx, k, m, S)
+    for i in np.flatnonzero(op):
+        dec.add_original_shard(int(i), orig[i].tobytes())
+    for j in np.flatnonzero(rp):
+        dec.add_recovery_shard(int(j), rec[j].tobytes())
+    res = dec.decode()
+    assert sorted(res) == sorted(int(i) for i in np.flatnonzero(op == 0))
+    for i, b in res.items():
+        assert b == want[i].tobytes(), i
+
+
+
