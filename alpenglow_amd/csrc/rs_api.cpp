@@ -1565,11 +1565,16 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, uint8_t* orig, co
   uint8_t* pd = c->one_pin.dev<uint8_t>();
   std::memcpy(pin, orig, ob);
   std::memcpy(pin + ob, rec, rb);
+  // exactly k shards, all of them recovery shards: the completed codeword passes through
+  // them, so its re-encoded recovery shards are the received ones (bit for bit)
+  size_t nr = 0;
+  for (size_t i = 0; i < m; ++i) nr += rpres[i] != 0;
+  const bool reuse = coding && present == k && nr == m;
   if ((st = decode_device(c, k, m, S, 1, pd, ob, pd + ob, rb, opres, rpres, 1, mode))) return st;
-  if (coding && (st = encode_device(c, k, m, S, 1, pd, ob, pd + ob + rb, rb))) return st;
+  if (coding && !reuse && (st = encode_device(c, k, m, S, 1, pd, ob, pd + ob + rb, rb))) return st;
   AG_HIP(hipStreamSynchronize(c->stream));
   std::memcpy(orig, pin, ob);
-  if (coding) std::memcpy(coding, pin + ob + rb, rb);
+  if (coding) std::memcpy(coding, reuse ? rec : pin + ob + rb, rb);
   return AG_RS_OK;
 }
 }  // namespace
