@@ -1929,7 +1929,14 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
       out[b] = lens[b];
     }
   }
-  // re-encode all coding shards (encode_coding_from_data) of each run of good slices
+  // re-encode all coding shards (encode_coding_from_data) of each run of good slices.  A
+  // slice whose present shards are exactly its k = 32 coding shards (every data shred lost,
+  // the reference bench's shape) is skipped: its re-encoded coding shards are the received
+  // ones already in place, bit for bit.
+  for (size_t b = 0; b < n; ++b)
+    if (ok[b] && m == kDataShreds && count_flags(dpres + b * kDataShreds, kDataShreds) == 0 &&
+        count_flags(cpres + b * m, m) == m)
+      ok[b] = 0;
   for (size_t b = 0; b < n;) {
     if (!ok[b]) {
       ++b;
