@@ -877,7 +877,10 @@ def test_lowrate_window_decode(ctx, dev, k, m, S):
             if j not in keep_r:
                 d_r[b, j] = 0x22
     got = gpu_decode(ctx, dev, d_o, d_r, op, rp, rs.DECODE_ANY_K)
-    assert np.array_equal(got, blocks)@pytest.mark.gpu
+    assert np.array_equal(got, blocks)
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("extra", [0, 7])
 def test_decoder_crate_api_exact_semantics(ctx, extra):
     """The per-call decoder (zero-copy path) keeps the crate's EXACT results on arbitrary
@@ -907,6 +910,3 @@ def test_decoder_crate_api_exact_semantics(ctx, extra):
     assert sorted(res) == sorted(int(i) for i in np.flatnonzero(op == 0))
     for i, b in res.items():
         assert b == want[i].tobytes(), i
-
-
-
