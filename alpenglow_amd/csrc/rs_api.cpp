@@ -65,15 +65,16 @@ struct DevBuf {
   }
 };
 
-// Grow-only pinned host buffer: the crate-API single-call paths stage through it, so their
-// copies are DMA transfers instead of the runtime's pageable staging (one copy per direction).
+// Grow-only pinned host buffer, mapped and coherent (fine-grained: never cached in the GPU's
+// L2, so one call's kernels cannot read another call's stale bytes): the crate-API
+// single-call kernels read and write it directly (zero-copy).
 struct PinBuf {
   void* ptr = nullptr;
   size_t size = 0;
   int ensure(size_t n) {
     if (n <= size) return AG_RS_OK;
     release();
-    if (hipHostMalloc(&ptr, n, hipHostMallocMapped) != hipSuccess) {
+    if (hipHostMalloc(&ptr, n, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess) {
       ptr = nullptr;
       return AG_RS_ERR_OUT_OF_MEMORY;
     }

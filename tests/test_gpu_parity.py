@@ -910,3 +910,26 @@ def test_decoder_crate_api_exact_semantics(ctx, extra):
     assert sorted(res) == sorted(int(i) for i in np.flatnonzero(op == 0))
     for i, b in res.items():
         assert b == want[i].tobytes(), i
+
+
+@pytest.mark.gpu
+def test_crate_api_back_to_back_calls_see_fresh_bytes(ctx):
+    """The per-call paths reuse one zero-copy staging buffer: consecutive calls with
+    different bytes must each see their own (no stale cached copy of the previous call)."""
+    k, m, S = 32, 32, 1024
+    rng = np.random.default_rng(7)
+    enc = rs.ReedSolomonEncoder(ctx, k, m, S)
+    dec = rs.ReedSolomonDecoder(ctx, k, m, S)
+    for it in range(6):
+        orig = rng.integers(0, 256, (k, S), dtype=np.uint8)
+        enc.reset(k, m, S)
+        for i in range(k):
+            enc.add_original_shard(orig[i].tobytes())
+        rec = enc.encode()
+        want = ro_c.encode(orig, m)
+        assert [bytes(r) for r in rec] == [want[j].tobytes() for j in range(m)], it
+        dec.reset(k, m, S)
+        for j in range(m):
+            dec.add_recovery_shard(j, want[j].tobytes())
+        res = dec.decode()
+        assert all(res[i] == orig[i].tobytes() for i in range(k)), it
