@@ -259,7 +259,7 @@ constexpr size_t kStageGroupBytes = size_t{64} << 20;
 constexpr size_t kGenericScratchBytes = size_t{512} << 20;
 
 // Restrided shard buffer (shard sizes that are not whole 64-byte chunks), per group.
-constexpr size_t kRestrideGroupBytes = size_t{256} << 20;
+constexpr size_t kRestrideGroupBytes = size_t{2048} << 20;
 
 // Syndrome-decoder pattern (decode_syn_kernel): restore the erased originals from the
 // first e present recovery shards.  Returns false if the e x e system is singular (cannot

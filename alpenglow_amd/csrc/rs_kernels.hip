@@ -1559,10 +1559,15 @@ __global__ __launch_bounds__(256) void restride_kernel(const RestrideParams p) {
     if (whole && (reinterpret_cast<uintptr_t>(src) & 1) == 0) {
       *dst = load16_a2(src + q);
     } else {
+      // 16 independent byte loads (a zero symbol's byte reads the tail's first byte and is
+      // masked): a conditional load per byte serialised 16 memory latencies per wave
+      const int64_t tb = 64 * (p.S >> 6);
       uint32_t v[4] = {0, 0, 0, 0};
+#pragma unroll
       for (int i = 0; i < 16; ++i) {
         const int64_t o = restride_src(q + i, p.S);
-        if (o >= 0) v[i >> 2] |= static_cast<uint32_t>(src[o]) << (8 * (i & 3));
+        const uint32_t x = src[o >= 0 ? o : tb];
+        v[i >> 2] |= (o >= 0 ? x : 0u) << (8 * (i & 3));
       }
       *dst = make_uint4(v[0], v[1], v[2], v[3]);
     }
