@@ -1558,6 +1558,29 @@ __global__ __launch_bounds__(256) void restride_kernel(const RestrideParams p) {
     uint4* dst = reinterpret_cast<uint4*>(p.dst + b * p.dst_block_stride + sh * p.dst_shard_stride + q);
     if (whole && (reinterpret_cast<uintptr_t>(src) & 1) == 0) {
       *dst = load16_a2(src + q);
+    } else if (!whole && (reinterpret_cast<uintptr_t>(src) & 1) == 0) {
+      // a tail piece: L <= 16 contiguous source bytes (low or high half of the tail
+      // symbols), read as the aligned dwords holding them (never past a dword with a valid
+      // byte, so never across a page), funnel-shifted, bytes past L zeroed
+      const uint32_t tb = 64 * (p.S >> 6), h = (p.S & 63) >> 1, w = q - tb;
+      const uint32_t off = w & 31, start = tb + (w < 32 ? 0 : h) + off;
+      const uint32_t L = off < h ? min(16u, h - off) : 0u;
+      uint32_t v[4] = {0, 0, 0, 0};
+      if (L) {
+        const uintptr_t a = reinterpret_cast<uintptr_t>(src + start);
+        const uint32_t* base = reinterpret_cast<const uint32_t*>(a & ~uintptr_t{3});
+        const uint32_t sh = static_cast<uint32_t>(a & 3), nd = (sh + L + 3) >> 2;
+        uint32_t d[5];
+#pragma unroll
+        for (uint32_t j = 0; j < 5; ++j) d[j] = base[min(j, nd - 1)];
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j) {
+          const uint32_t x = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+          const uint32_t nb = L > 4 * j ? min(4u, L - 4 * j) : 0u;
+          v[j] = nb >= 4 ? x : x & ((1u << (8 * nb)) - 1);
+        }
+      }
+      *dst = make_uint4(v[0], v[1], v[2], v[3]);
     } else {
       // 16 independent byte loads (a zero symbol's byte reads the tail's first byte and is
       // masked): a conditional load per byte serialised 16 memory latencies per wave
