@@ -626,12 +626,20 @@ int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks,
   for (size_t p = 0; p < npat; ++p)  // NotEnoughShards before anything is launched
     if (count_flags(opres + p * k, k) + count_flags(rpres + p * m, m) < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
   // store masks: the absent originals of each pattern (k <= 64 on every bitsliced path)
-  std::vector<uint64_t> mask(npat);
+  // and the pack masks: only present shards are packed (decoders never read absent ones)
+  std::vector<uint64_t> mask(3 * npat);
   const uint64_t kmask = k >= 64 ? ~uint64_t{0} : (uint64_t{1} << k) - 1;
-  for (size_t p = 0; p < npat; ++p) mask[p] = ~pack_flags(opres + p * k, k) & kmask;
-  int st = c->stage_mask.ensure(npat * 8, c->stream);
+  const bool rmask = m <= 64;
+  for (size_t p = 0; p < npat; ++p) {
+    mask[p] = ~pack_flags(opres + p * k, k) & kmask;
+    mask[npat + p] = pack_flags(opres + p * k, k);
+    mask[2 * npat + p] = rmask ? pack_flags(rpres + p * m, m) : 0;
+  }
+  int st = c->stage_mask.ensure(3 * npat * 8, c->stream);
   if (st) return st;
-  AG_HIP(hipMemcpyAsync(c->stage_mask.ptr, mask.data(), npat * 8, hipMemcpyHostToDevice, c->stream));
+  AG_HIP(hipMemcpyAsync(c->stage_mask.ptr, mask.data(), 3 * npat * 8, hipMemcpyHostToDevice, c->stream));
+  const uint64_t* d_omask = c->stage_mask.as<uint64_t>() + npat;
+  const uint64_t* d_rmask = rmask ? c->stage_mask.as<uint64_t>() + 2 * npat : nullptr;
   const size_t group = std::max<size_t>(1, kRestrideGroupBytes / per_block);
   if ((st = c->stage_pad.ensure(std::min(group, nblocks) * per_block, c->stream))) return st;
   uint8_t* pad = c->stage_pad.as<uint8_t>();
@@ -639,9 +647,10 @@ int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks,
     const size_t nb = std::min(group, nblocks - b0);
     const size_t p0 = npat > 1 ? b0 : 0, np = npat > 1 ? nb : 1;
     if (ag::launch_restride(orig + b0 * ostride, ostride, S, pad, per_block, Sp, static_cast<uint32_t>(S),
-                            static_cast<uint32_t>(k), nb, false, nullptr, false, c->stream) != hipSuccess ||
+                            static_cast<uint32_t>(k), nb, false, d_omask + p0, npat > 1, c->stream) != hipSuccess ||
         ag::launch_restride(rec + b0 * rstride, rstride, S, pad + k * Sp, per_block, Sp, static_cast<uint32_t>(S),
-                            static_cast<uint32_t>(m), nb, false, nullptr, false, c->stream) != hipSuccess)
+                            static_cast<uint32_t>(m), nb, false, d_rmask ? d_rmask + p0 : nullptr, npat > 1,
+                            c->stream) != hipSuccess)
       return AG_RS_ERR_DEVICE;
     if ((st = decode_device(c, k, m, Sp, nb, pad, per_block, pad + k * Sp, per_block, opres + p0 * k, rpres + p0 * m,
                             np, mode)))

@@ -1475,7 +1475,8 @@ __global__ __launch_bounds__(256) void coder_pad_kernel(const uint8_t* __restric
 // symbols).  pack: shard (S bytes, any alignment) -> padded shard of Sp = ceil(S/64)*64
 // bytes whose last chunk holds the tail symbols in whole-chunk layout (low bytes at 0..,
 // high bytes at 32..) with zero symbols after them; unpack is the inverse and writes only
-// the shards selected by the store mask.  Zero symbols are zero columns of every linear
+// the shards selected by the store mask.  A pack mask skips shards (the decoders never read
+// an absent shard, so its padded slot may keep stale bytes).  Zero symbols are zero columns of every linear
 // transform, so the bitsliced kernels run on the padded shards unchanged.
 struct RestrideParams {
   const uint8_t* src;
@@ -1553,6 +1554,7 @@ __global__ __launch_bounds__(256) void restride_kernel(const RestrideParams p) {
   const uint32_t sh = r / per_shard, u = r - sh * per_shard;
   const uint32_t q = 16 * u;
   const bool whole = q + 16 <= 64 * (p.S >> 6);
+  if (p.mask && !((p.mask[p.mask_per_block ? b : 0] >> sh) & 1)) return;  // shard not selected
   if (!p.unpack) {
     const uint8_t* src = p.src + b * p.src_block_stride + sh * p.src_shard_stride;
     uint4* dst = reinterpret_cast<uint4*>(p.dst + b * p.dst_block_stride + sh * p.dst_shard_stride + q);
@@ -1595,7 +1597,6 @@ __global__ __launch_bounds__(256) void restride_kernel(const RestrideParams p) {
       *dst = make_uint4(v[0], v[1], v[2], v[3]);
     }
   } else {
-    if (p.mask && !((p.mask[p.mask_per_block ? b : 0] >> sh) & 1)) return;
     const uint4 v = *reinterpret_cast<const uint4*>(p.src + b * p.src_block_stride + sh * p.src_shard_stride + q);
     uint8_t* dst = p.dst + b * p.dst_block_stride + sh * p.dst_shard_stride;
     if (whole && (reinterpret_cast<uintptr_t>(dst) & 1) == 0) {
