@@ -1519,21 +1519,28 @@ int ag_aon_decrypt_batch(ag_rs_ctx* c, int scheme, size_t n, uint8_t* buffers, s
 // =====================================================================================
 // Crate API mirror: ReedSolomonEncoder / ReedSolomonDecoder (one codeword, host memory)
 // =====================================================================================
+// An object made by *_new_on_device owns its context (`owned`: created with it, destroyed by
+// its _free), so objects made that way share no state and may run on different threads at
+// once; *_new borrows the caller's context, shared with whatever else uses it.
 struct ag_rs_encoder {
   ag_rs_ctx* ctx = nullptr;
+  ag_rs_ctx* owned = nullptr;
   size_t k = 0, m = 0, S = 0;
   size_t received = 0;
   bool encoded = false;
   std::vector<uint8_t> orig, rec;
+  ~ag_rs_encoder() { ag_rs_ctx_destroy(owned); }
 };
 
 struct ag_rs_decoder {
   ag_rs_ctx* ctx = nullptr;
+  ag_rs_ctx* owned = nullptr;
   size_t k = 0, m = 0, S = 0;
   std::vector<uint8_t> orig, rec, opres, rpres;
   size_t no = 0, nr = 0;
   bool decoded = false;
   std::vector<uint8_t> restored;  // 1 where original i was restored by the last decode
+  ~ag_rs_decoder() { ag_rs_ctx_destroy(owned); }
 };
 
 namespace {
@@ -1620,6 +1627,20 @@ int ag_rs_encoder_new(ag_rs_ctx* c, size_t k, size_t m, size_t S, ag_rs_encoder*
   return AG_RS_OK;
 }
 
+int ag_rs_encoder_new_on_device(int device, size_t k, size_t m, size_t S, ag_rs_encoder** out) {
+  if (!out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  ag_rs_ctx* c = nullptr;
+  int st = ag_rs_ctx_create(device, &c);
+  if (st) return st;
+  if ((st = ag_rs_encoder_new(c, k, m, S, out))) {
+    ag_rs_ctx_destroy(c);
+    return st;
+  }
+  (*out)->owned = c;
+  return AG_RS_OK;
+}
+
 int ag_rs_encoder_add_original_shard(ag_rs_encoder* e, const uint8_t* shard, size_t len) {
   if (!e || (!shard && len)) return AG_RS_ERR_INVALID_ARGUMENT;
   if (e->encoded) {  // the crate resets the received set once a result is dropped
@@ -1681,6 +1702,20 @@ int ag_rs_decoder_new(ag_rs_ctx* c, size_t k, size_t m, size_t S, ag_rs_decoder*
     return st;
   }
   *out = d;
+  return AG_RS_OK;
+}
+
+int ag_rs_decoder_new_on_device(int device, size_t k, size_t m, size_t S, ag_rs_decoder** out) {
+  if (!out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  ag_rs_ctx* c = nullptr;
+  int st = ag_rs_ctx_create(device, &c);
+  if (st) return st;
+  if ((st = ag_rs_decoder_new(c, k, m, S, out))) {
+    ag_rs_ctx_destroy(c);
+    return st;
+  }
+  (*out)->owned = c;
   return AG_RS_OK;
 }
 
@@ -1749,12 +1784,14 @@ void ag_rs_decoder_free(ag_rs_decoder* d) { delete d; }
 // =====================================================================================
 struct ag_rs_coder {
   ag_rs_ctx* ctx = nullptr;
+  ag_rs_ctx* owned = nullptr;  // ag_rs_coder_new_on_device: shared by its encoder and decoder
   size_t num_coding = 0;
   ag_rs_encoder* enc = nullptr;
   ag_rs_decoder* dec = nullptr;
   ~ag_rs_coder() {
     ag_rs_encoder_free(enc);
     ag_rs_decoder_free(dec);
+    ag_rs_ctx_destroy(owned);
   }
 };
 
@@ -1793,6 +1830,20 @@ int ag_rs_coder_new(ag_rs_ctx* ctx, size_t num_coding, ag_rs_coder** out) {
     return st;
   }
   *out = c;
+  return AG_RS_OK;
+}
+
+int ag_rs_coder_new_on_device(int device, size_t num_coding, ag_rs_coder** out) {
+  if (!out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = nullptr;
+  ag_rs_ctx* c = nullptr;
+  int st = ag_rs_ctx_create(device, &c);
+  if (st) return st;
+  if ((st = ag_rs_coder_new(c, num_coding, out))) {
+    ag_rs_ctx_destroy(c);
+    return st;
+  }
+  (*out)->owned = c;
   return AG_RS_OK;
 }
 

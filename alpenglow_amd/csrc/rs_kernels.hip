@@ -21,20 +21,6 @@
 #include "rs_launch.hpp"
 #include "rs_xform.hpp"
 
-// Diagnostic builds only (wrong output): bit 0 skips decode_x's input multiply, bit 1 its
-// output multiply, bit 2 the formal derivative.
-// Diagnostic builds only (wrong output): AG_XF_DIAG bit 0 skips the transform's pass C, bit 1
-// keeps waves with nothing to store running through pass C, bit 2 skips the LDS exchanges,
-// bit 3 skips the pass A and B butterflies.
-#ifndef AG_XF_DIAG
-#define AG_XF_DIAG 0
-#endif
-#ifndef AG_SYN_DIAG
-#define AG_SYN_DIAG 0
-#endif
-#ifndef AG_DX_DIAG
-#define AG_DX_DIAG 0
-#endif
 
 namespace ag {
 namespace {
@@ -72,21 +58,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
     swap_halves(ra[decltype(T)::value]);
     dev::planes_from_raw(ra[decltype(T)::value]);
   });
-#if !(AG_XF_DIAG & 8)
   xf_pass_a<NW, DIN>(wave, ra);
-#endif
-#if !(AG_XF_DIAG & 4)
   Regs8 rb;
   xf_exchange_ab<NW>(wave, lane, lds, ra, rb);
-#else
-  Regs8& rb = ra;
-#endif
-#if !(AG_XF_DIAG & 8)
   xf_pass_b<NW, DIN, DOUT>(rb);
-#endif
-#if !(AG_XF_DIAG & 4)
   xf_exchange_bc<NW>(wave, lane, lds, rb, ra);
-#endif
 
   // pass C only where some lane of the wave stores one of its 8 shards (a decode restores
   // only the erased originals)
@@ -97,12 +73,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
     const uint32_t s = 8 * wave + t;
     if (s < p.n_out && store_qmask(out_io, mask, s)) need = 1;
   });
-#if !(AG_XF_DIAG & 2)
   if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
-#endif
-#if !(AG_XF_DIAG & 1)
   xf_pass_c<NW, DOUT>(wave, ra);
-#endif
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = 8 * wave + t;  // wave-uniform
@@ -152,25 +124,13 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
     swap_halves(r[decltype(T)::value]);
     dev::planes_from_raw(r[decltype(T)::value]);
   });
-#if !(AG_XF_DIAG & 8)
   x8_layer<0, 0, true, DIN>(wave, r);
   x8_layer<0, 1, true, DIN>(wave, r);
-#endif
-#if !(AG_XF_DIAG & 4)
   x8_swap<0, 0, 1>(wave, lane, lds, &flags, r);
-#endif
-#if !(AG_XF_DIAG & 8)
   x8_layer<1, 2, true, DIN>(wave, r);
-#endif
-#if !(AG_XF_DIAG & 4)
   x8_swap<1, 1, 2>(wave, lane, lds, &flags, r);
-#endif
-#if !(AG_XF_DIAG & 8)
   x8_layer<2, 3, true, DIN>(wave, r);
-#endif
-#if !(AG_XF_DIAG & 4)
   x8_swap<0, 2, 3>(wave, lane, lds, &flags, r);
-#endif
   if constexpr (HALF) {
     using H3 = X8Lay<4, 3, 0, 1, 2>;
     using H2 = X8Lay<4, 2, 0, 1, 3>;
@@ -209,26 +169,14 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
     });
     return;
   }
-#if !(AG_XF_DIAG & 8)
   x8_layer<3, 4, true, DIN>(wave, r);
   x8_layer<3, 4, false, DOUT>(wave, r);
   x8_layer<3, 3, false, DOUT>(wave, r);
-#endif
-#if !(AG_XF_DIAG & 4)
   x8_swap<0, 2, 4>(wave, lane, lds, &flags, r);
-#endif
-#if !(AG_XF_DIAG & 8)
   x8_layer<2, 2, false, DOUT>(wave, r);
-#endif
-#if !(AG_XF_DIAG & 4)
   x8_swap<1, 1, 5>(wave, lane, lds, &flags, r);
-#endif
-#if !(AG_XF_DIAG & 8)
   x8_layer<1, 1, false, DOUT>(wave, r);
-#endif
-#if !(AG_XF_DIAG & 4)
   x8_swap<0, 0, 6>(wave, lane, lds, &flags, r);
-#endif
   // store masks fetched only now: live across the transform they cost registers (spills)
   const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
   uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
@@ -245,12 +193,8 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
     const uint32_t sh = 4 * wave + decltype(T)::value;
     if (sh < p.n_out && store_qmask(out_io, mask, sh)) need = 1;
   });
-#if !(AG_XF_DIAG & 2)
   if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
-#endif
-#if !(AG_XF_DIAG & 1)
   x8_layer<0, 0, false, DOUT>(wave, r);
-#endif
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t sh = 4 * wave + t;  // wave-uniform
@@ -691,18 +635,14 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     if ((in_mask >> j) & 1) {
       if constexpr (!PL) swap_halves(ra[t]);
       dev::planes_from_raw(ra[t]);
-#if !(AG_DX_DIAG & 1)
       if constexpr (PL) mul_rt_lane(ra[t], rows + j * 16); else mul_rt_dx(ra[t], rows + j * 16);
-#endif
     }
   });
   xf_pass_a<NW, 0>(wave, ra);
   Regs8 rb;
   xf_exchange_ab<NW>(wave, lane, lds, ra, rb);
   xf_pass_b_ifft<NW, 0>(rb);
-#if !(AG_DX_DIAG & 4)
   xf_derivative<NW>(wave, lane, lds, rb);
-#endif
   xf_pass_b_fft<NW, 0>(rb);
   xf_exchange_bc<NW>(wave, lane, lds, rb, ra);
   const uint32_t mine = static_cast<uint32_t>(out_mask >> (8 * wave)) & 0xFF;
@@ -718,14 +658,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     if ((out_mask >> j) & 1) {
       uint8_t* dst = p.orig + (j - (p.low_rate ? 0 : p.chunk)) * p.orig_shard_stride;
       if constexpr (PL) {
-#if !(AG_DX_DIAG & 2)
         mul_rt_lane(ra[t], rows + j * 16);
-#endif
         dev::store_chunk(dst + off_o, ra[t]);
       } else {
-#if !(AG_DX_DIAG & 2)
         mul_rt_dx(ra[t], rows + j * 16);
-#endif
         store_shard(dst, io_o, io_o.valid, ra[t]);
       }
     }
@@ -1155,20 +1091,7 @@ __global__ __launch_bounds__(256, 2) void decode_syn_kernel(const DecodeSynParam
       });
     }
   });
-#if AG_SYN_DIAG & 2  // bit-matrix form: one v_bitop3 per matrix entry
-  static_for<C>([&](auto A) {
-    constexpr int a = decltype(A)::value;
-    if (a < e) {
-      uint32_t out[16];
-      static_for<16>([&](auto P) { out[decltype(P)::value] = 0; });
-      static_for<C>([&](auto B) {
-        constexpr int b = decltype(B)::value;
-        if (b < e) mul_rt_acc(out, raw[0][b], sp->rows[a][b]);
-      });
-      store_shard(p.orig + sp->out[a] * p.orig_shard_stride, io, io.valid, out);
-    }
-  });
-#elif AG_SYN_RT4
+#if AG_SYN_RT4
   // Four Russians in registers (mul_rt4's scheme): per syndrome b, the 16 XOR combinations
   // of each 4-plane group (44 VALU) serve all e outputs; output plane o of Minv[a][b] S_b is
   // the XOR of 4 entries picked by row o's wave-uniform nibbles (one v_movrels each).

@@ -41,9 +41,6 @@ __device__ __forceinline__ void bfly(uint32_t* x, uint32_t* y) {
 }
 template <int BASE, bool INV, int NW>
 __device__ __forceinline__ void bfly_w(int wave, uint32_t* x, uint32_t* y) {
-#ifdef AG_XF_DIAG_ONE_ROLE
-  wave = 0;  // diagnostic build only: every wave runs role 0's code (wrong output)
-#endif
   if constexpr (NW == 4) {
     switch (wave) {
       case 0: bfly<BASE, INV>(x, y); break;

@@ -49,9 +49,9 @@ __global__ __launch_bounds__(256) void slice_frame_kernel(const SliceFrameParams
     if (wsrc && i0 >= hdr && i0 + 16 <= total && (i0 - hdr) + 20 <= p.data_stride) {
       const uint32_t j = i0 - hdr, sh = j & 3, q = j >> 2;
       const uint4 x = *reinterpret_cast<const uint4*>(sw + q);  // 4-byte aligned: fine for dwordx4
-      const uint32_t e = sw[q + 4];
       uint4 o = x;
-      if (sh) {
+      if (sh) {  // the fifth word holds a valid data byte only when sh != 0
+        const uint32_t e = sw[q + 4];
         o.x = __builtin_amdgcn_alignbyte(x.y, x.x, sh);
         o.y = __builtin_amdgcn_alignbyte(x.z, x.y, sh);
         o.z = __builtin_amdgcn_alignbyte(x.w, x.z, sh);

@@ -73,6 +73,7 @@ EXPORTS = (
     "ag_rs_decoder_add_recovery_shard", "ag_rs_decoder_decode",
     "ag_rs_decoder_restored_original", "ag_rs_decoder_free",
     "ag_rs_coder_new", "ag_rs_coder_free", "ag_rs_coder_shred", "ag_rs_coder_deshred",
+    "ag_rs_encoder_new_on_device", "ag_rs_decoder_new_on_device", "ag_rs_coder_new_on_device",
     "ag_rs_coder_shred_batch", "ag_rs_coder_deshred_batch",
     "ag_merkle_empty_root", "ag_merkle_height", "ag_merkle_node_count", "ag_merkle_build_batch",
     "ag_merkle_verify_batch",
@@ -136,6 +137,9 @@ def load():
         "ag_rs_decoder_restored_original": ([p, sz, pp, psz], i),
         "ag_rs_decoder_free": ([p], None),
         "ag_rs_coder_new": ([p, sz, pp], i),
+        "ag_rs_encoder_new_on_device": ([i, sz, sz, sz, pp], i),
+        "ag_rs_decoder_new_on_device": ([i, sz, sz, sz, pp], i),
+        "ag_rs_coder_new_on_device": ([i, sz, pp], i),
         "ag_rs_coder_free": ([p], None),
         "ag_rs_coder_shred": ([p, p, sz, p, p, psz], i),
         "ag_rs_coder_deshred": ([p, sz, p, p, p, p, psz, p, p, psz], i),
@@ -275,7 +279,7 @@ def _flags(f):
     import numpy as np
 
     if isinstance(f, np.ndarray) and f.dtype == np.uint8 and f.flags.c_contiguous:
-        return f
+        return f.reshape(-1)  # (nblocks, k) arrays: one flat pattern list
     return bytes(bytearray(f))
 
 
@@ -331,14 +335,22 @@ def fill_splitmix(ctx: Context, device_dst, nblocks: int, block_bytes: int, dst_
 # ---- crate API mirror ----------------------------------------------------------------
 
 class ReedSolomonEncoder:
-    """reed_solomon_simd::ReedSolomonEncoder (one codeword, host memory)."""
+    """reed_solomon_simd::ReedSolomonEncoder (one codeword, host memory).  ``ctx=None``: the
+    encoder owns a private context on ``device`` (ag_rs_encoder_new_on_device) and may run
+    on its own thread concurrently with other such objects."""
 
-    def __init__(self, ctx: Context, original_count: int, recovery_count: int, shard_bytes: int):
+    def __init__(self, ctx: Context | None, original_count: int, recovery_count: int, shard_bytes: int,
+                 device: int = 0):
         self._lib = load()
         self.ctx = ctx
         h = ctypes.c_void_p()
-        _check(self._lib.ag_rs_encoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
-                                           ctypes.byref(h)), "ReedSolomonEncoder::new")
+        if ctx is None:
+            st = self._lib.ag_rs_encoder_new_on_device(device, original_count, recovery_count, shard_bytes,
+                                                       ctypes.byref(h))
+        else:
+            st = self._lib.ag_rs_encoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
+                                             ctypes.byref(h))
+        _check(st, "ReedSolomonEncoder::new")
         self.handle = h
         self.recovery_count = recovery_count
 
@@ -370,14 +382,21 @@ class ReedSolomonEncoder:
 
 
 class ReedSolomonDecoder:
-    """reed_solomon_simd::ReedSolomonDecoder (one codeword, host memory)."""
+    """reed_solomon_simd::ReedSolomonDecoder (one codeword, host memory).  ``ctx=None``: a
+    private context on ``device``, as for ReedSolomonEncoder."""
 
-    def __init__(self, ctx: Context, original_count: int, recovery_count: int, shard_bytes: int):
+    def __init__(self, ctx: Context | None, original_count: int, recovery_count: int, shard_bytes: int,
+                 device: int = 0):
         self._lib = load()
         self.ctx = ctx
         h = ctypes.c_void_p()
-        _check(self._lib.ag_rs_decoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
-                                           ctypes.byref(h)), "ReedSolomonDecoder::new")
+        if ctx is None:
+            st = self._lib.ag_rs_decoder_new_on_device(device, original_count, recovery_count, shard_bytes,
+                                                       ctypes.byref(h))
+        else:
+            st = self._lib.ag_rs_decoder_new(ctx.handle, original_count, recovery_count, shard_bytes,
+                                             ctypes.byref(h))
+        _check(st, "ReedSolomonDecoder::new")
         self.handle = h
         self.original_count = original_count
 
@@ -424,15 +443,20 @@ class RawShreds:
 
 
 class ReedSolomonCoder:
-    """ReedSolomonCoder (reed_solomon.rs:47-232) for DATA_SHREDS = 32 data shreds."""
+    """ReedSolomonCoder (reed_solomon.rs:47-232) for DATA_SHREDS = 32 data shreds.
+    ``ctx=None``: the coder owns a private context on ``device`` (one per ShredderPool
+    entry; such coders may run concurrently on different threads)."""
 
-    def __init__(self, ctx: Context, num_coding: int):
+    def __init__(self, ctx: Context | None, num_coding: int, device: int = 0):
         self._lib = load()
         self.ctx = ctx
         self.num_coding = num_coding
         h = ctypes.c_void_p()
-        _check(self._lib.ag_rs_coder_new(ctx.handle, num_coding, ctypes.byref(h)),
-               "ReedSolomonCoder::new")
+        if ctx is None:
+            st = self._lib.ag_rs_coder_new_on_device(device, num_coding, ctypes.byref(h))
+        else:
+            st = self._lib.ag_rs_coder_new(ctx.handle, num_coding, ctypes.byref(h))
+        _check(st, "ReedSolomonCoder::new")
         self.handle = h
 
     def shred(self, payload: bytes) -> RawShreds:

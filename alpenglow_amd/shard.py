@@ -28,6 +28,18 @@ def max_over_ranks(value: float, dist=None, device=None) -> float:
     return float(t.item())
 
 
+def gather_over_ranks(value: float, dist=None, device=None) -> list:
+    """``value`` of every rank, in rank order (the bench's per-rank wall times)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [value]
+    import torch
+
+    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    out = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(out, t)
+    return [float(x.item()) for x in out]
+
+
 # ---- the bench's per-rank plan (bench.py; tested under gloo in tests/test_dist.py) ----
 
 SEED_BASE = 0x5EED_A19E_0000_0000  # SURVEY.md §8(d): block b is seeded SEED_BASE + b

@@ -8,9 +8,13 @@ Workload (BASELINE.json configs[1] + configs[2]): per GPU, 4096 random 1 MiB blo
 through the C ABI (libalpenglow_rs.so).  value = block payload bytes that went through
 encode AND reconstruct, summed over ranks, per second of the max-over-ranks wall time.
 
-Multi-GPU: one process per GPU (torchrun), each rank shards its own independent blocks
-(weak scaling, no data-path collective; the only collectives are the timing barrier and
-the max-over-ranks reduction).
+Multi-GPU: one process per GPU.  Under an external launcher (torchrun: WORLD_SIZE set) the
+launcher's world must equal --gpus; without one, `--gpus N` (N > 1) makes this process a
+launcher that starts N fresh rank processes before any GPU call and exits non-zero if any
+rank fails.  Each rank shards its own independent blocks (weak scaling, or --stream-blocks
+for BASELINE configs[4]'s one stream split over the GPUs); there is no data-path collective,
+the only collectives are the timing barrier, the max-over-ranks reduction and the gather of
+per-rank wall times reported in the line.
 
 Also printed in the JSON line: per-kernel HIP-event timings on the launch stream with the
 HBM roofline, a CPU baseline (the C oracle, a restatement of the reference algorithm, on a
@@ -61,26 +65,127 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-settle", action="store_true",
                     help="skip the untimed clock-settle steps that follow the W warmup steps")
+    ap.add_argument("--dry-device", action="store_true",
+                    help="launcher / rank plumbing only (gloo, no GPU call, no kernel): the timed "
+                         "steps are empty and the line reports no throughput (tests/test_dist.py)")
+    ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _spawn_ranks(args) -> int:
+    """`--gpus N` without an external launcher: start N fresh rank processes (this process
+    makes no GPU call), one per GPU, and wait for them.  Returns the exit status: 0 only if
+    every rank exited 0; the first failure stops the other ranks (their exact PIDs)."""
+    import subprocess
+
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__), *sys.argv[1:]], env=env))
+    status = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            rc = p.poll()
+            if rc is None:
+                continue
+            live.remove(p)
+            if rc != 0 and status == 0:
+                status = rc if rc > 0 else 1
+                print(f"bench.py: rank {procs.index(p)} exited with {rc}; stopping the other ranks",
+                      file=sys.stderr, flush=True)
+                for q in live:
+                    q.terminate()
+        time.sleep(0.05)
+    return status
+
+
+def _dry_main(args, world: int, rank: int):
+    """The multi-rank harness without a device: gloo group, rank plan, barrier-bracketed
+    empty steps, max-over-ranks wall time, gathered per-rank walls, one JSON line."""
+    import torch.distributed as dist
+
+    from alpenglow_amd.shard import RankPlan, gather_over_ranks, max_over_ranks
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    if rank == args.dry_fail_rank:
+        raise SystemExit(3)
+    plan = RankPlan(rank, world, args.nblocks, args.stream_blocks)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        pass
+    if world > 1:
+        dist.barrier()
+    wall = time.perf_counter() - t0
+    d = dist if world > 1 else None
+    wall_max = max_over_ranks(wall, d)
+    walls = gather_over_ranks(wall, d)
+    firsts = gather_over_ranks(plan.first, d)
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": wall_max * 1e3 / max(args.steps, 1), "higher_is_better": True,
+            "scaling": plan.scaling, "vs_baseline": None, "dry_device": True,
+            "ranks": {"backend": "gloo" if world > 1 else None, "world_size": world, "wall_s": walls,
+                      "first_block": [int(f) for f in firsts], "blocks_per_rank": plan.nblocks},
+            "config": {"workload": _workload(args, world, plan.nblocks)},
+        }), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+METRIC = "GiB/s device-resident RS shred encode+reconstruct, batched 1 MiB blocks"
+
+
+def _workload(args, world, n, e=None, lc=0):
+    B = args.block_bytes
+    s = (f"{args.stream_blocks} x {B >> 20} MiB block stream over {world} GPU(s)" if args.stream_blocks
+         else f"{n} x {B >> 20} MiB blocks per GPU")
+    if e is None:
+        return s
+    return (s + f", {args.k}:{args.m} encode + reconstruct with {e}/{args.k} data shreds erased"
+            + (f" and {lc}/{args.m} coding shreds lost" if lc else "")
+            + (" (random pattern per block)" if args.random_patterns else ""))
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_spawn_ranks(args))  # launcher: no GPU call in this process
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
+    if args.dry_device:
+        return _dry_main(args, world, rank)
     import torch
     import torch.distributed as dist
 
     from alpenglow_amd import rs
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
 
-    from alpenglow_amd.shard import RankPlan, erasure_patterns, max_over_ranks
+    from alpenglow_amd.shard import RankPlan, erasure_patterns, gather_over_ranks, max_over_ranks
 
     k, m, B = args.k, args.m, args.block_bytes
     plan = RankPlan(rank, world, args.nblocks, args.stream_blocks)
@@ -152,6 +257,7 @@ def main():
     dec_ms = sum(ev[s][1].elapsed_time(ev[s][2]) for s in range(args.steps)) / args.steps
 
     wall_max = max_over_ranks(wall, dist if world > 1 else None, dev)
+    walls = gather_over_ranks(wall, dist if world > 1 else None, dev)
     ms_per_step = wall_max * 1e3 / args.steps
 
     # full-size property check: zero the erased shards, reconstruct, compare with a fresh
@@ -189,7 +295,7 @@ def main():
         traffic = _pmc_traffic(dom, k, m, S, n)
         ach = kern[dom]["achieved_GBps"]
         line = {
-            "metric": "GiB/s device-resident RS shred encode+reconstruct, batched 1 MiB blocks",
+            "metric": METRIC,
             "value": processed / (wall_max) / GIB,
             "unit": "GiB/s",
             "n_gpus": world,
@@ -202,11 +308,10 @@ def main():
             "vs_baseline": None,
             "dtype": "u8 (GF(2^16) symbols, bitsliced u32 planes)",
             "data": "synthetic (splitmix64 random blocks, device-generated)",
-            "config": {"workload": (f"{args.stream_blocks} x {B >> 20} MiB block stream over {world} GPU(s)"
-                                    if args.stream_blocks else f"{n} x {B >> 20} MiB blocks per GPU")
-                                   + f", {k}:{m} encode + reconstruct with {e}/{k} data shreds erased"
-                                   + (f" and {lc}/{m} coding shreds lost" if lc else "")
-                                   + (" (random pattern per block)" if args.random_patterns else ""),
+            "ranks": {"backend": "nccl (RCCL)" if world > 1 else None,
+                      "world_size": dist.get_world_size() if world > 1 else 1,
+                      "wall_s": walls, "blocks_per_rank": n},
+            "config": {"workload": _workload(args, world, n, e, lc),
                        "blocks_per_gpu": n, "block_bytes": B, "shard_bytes": S,
                        "data_shreds": k, "coding_shreds": m, "erased_data_shreds": e,
                        "lost_coding_shreds": lc, "random_patterns": bool(args.random_patterns),

@@ -29,7 +29,11 @@
  * Conventions: the caller owns every buffer; the library borrows them for the call
  * (reed_solomon.rs copies out of the crate's borrowed results, :118,125,187,226).  A
  * context binds one device and one HIP stream; it is not thread-safe, like a
- * ReedSolomonCoder checked out of ShredderPool (pool.rs:33-93).  Calls fail loudly
+ * ReedSolomonCoder checked out of ShredderPool (pool.rs:33-93).  Encoders, decoders and
+ * coders made with *_new_on_device own a private context each, so they may run
+ * concurrently on different threads (the reference builds its coders on one thread and
+ * drives them from separate tokio tasks, consensus.rs:180-266); those made with *_new on a
+ * shared context must not be used concurrently with anything else on it.  Calls fail loudly
  * (AG_RS_ERR_NO_DEVICE / AG_RS_ERR_DEVICE) when no GPU is usable: there is no CPU
  * fallback.  On error, caller-visible outputs are left untouched (shredder.rs:274).
  */
@@ -146,6 +150,10 @@ int ag_rs_encoder_encode(ag_rs_encoder* enc);
 int ag_rs_encoder_recovery(const ag_rs_encoder* enc, size_t index, const uint8_t** shard,
                            size_t* len);
 void ag_rs_encoder_free(ag_rs_encoder* enc);
+/* ReedSolomonEncoder::new on a private context of `device` (created here, destroyed by
+ * ag_rs_encoder_free): no state shared with any other object. */
+int ag_rs_encoder_new_on_device(int device, size_t original_count, size_t recovery_count,
+                                size_t shard_bytes, ag_rs_encoder** out);
 
 /* ReedSolomonDecoder::{new,reset,add_original_shard,add_recovery_shard,decode} +
  * DecoderResult::restored_original (AG_RS_ERR_NOT_RESTORED for None). */
@@ -162,6 +170,9 @@ int ag_rs_decoder_decode(ag_rs_decoder* dec);
 int ag_rs_decoder_restored_original(const ag_rs_decoder* dec, size_t index,
                                     const uint8_t** shard, size_t* len);
 void ag_rs_decoder_free(ag_rs_decoder* dec);
+/* ReedSolomonDecoder::new on a private context of `device` (destroyed by ag_rs_decoder_free). */
+int ag_rs_decoder_new_on_device(int device, size_t original_count, size_t recovery_count,
+                                size_t shard_bytes, ag_rs_decoder** out);
 
 /* ---- 2. ReedSolomonCoder mirror (reed_solomon.rs:47-232) ----------------------------- */
 #define AG_RS_DATA_SHREDS 32                 /* shredder.rs:43 */
@@ -173,6 +184,9 @@ typedef struct ag_rs_coder ag_rs_coder;
 /* ReedSolomonCoder::new(num_coding) -- 32 data shreds, num_coding <= 64. */
 int ag_rs_coder_new(ag_rs_ctx* ctx, size_t num_coding, ag_rs_coder** out);
 void ag_rs_coder_free(ag_rs_coder* coder);
+/* ReedSolomonCoder::new on a private context of `device` (its encoder and decoder share it;
+ * destroyed by ag_rs_coder_free): one per ShredderPool entry (pool.rs:33-93). */
+int ag_rs_coder_new_on_device(int device, size_t num_coding, ag_rs_coder** out);
 
 /* ReedSolomonCoder::shred: pads payload with 0x80 00.. to a multiple of 64 bytes, splits
  * it into 32 shards of *shred_bytes and encodes num_coding coding shards.  data_out must

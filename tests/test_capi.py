@@ -105,3 +105,15 @@ def test_no_device_fails_loudly(lib):
     with pytest.raises(rs.RSError) as e:
         rs.Context(0)
     assert e.value.kind == "NoDevice"
+
+
+def test_private_context_objects_fail_loudly_without_device(lib):
+    """The per-object contexts (ReedSolomonCoder / Encoder / Decoder with ctx=None) take the
+    same loud path: no GPU, no object, never a CPU fallback."""
+    if rs.device_count() > 0:
+        pytest.skip("a GPU is present")
+    for make in (lambda: rs.ReedSolomonCoder(None, 32), lambda: rs.ReedSolomonEncoder(None, 32, 32, 1024),
+                 lambda: rs.ReedSolomonDecoder(None, 32, 32, 1024)):
+        with pytest.raises(rs.RSError) as e:
+            make()
+        assert e.value.kind == "NoDevice"

@@ -130,3 +130,44 @@ def test_gloo_world2_bench_rank_logic():
         assert wall == 1.0
         assert processed == 1001 * (1 << 20) * 5
         assert ranges == [(0, 501), (501, 500)]  # contiguous, disjoint, covering the stream
+
+
+# ---- bench.py's own launcher (`--gpus N` without torchrun) ------------------------------
+
+import json  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*argv, env_extra=None):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), *argv], env=env, cwd=ROOT,
+                          capture_output=True, text=True, timeout=300)
+
+
+@pytest.mark.parametrize("extra,firsts", [((), [0, 4096]), (("--stream-blocks", "65536"), [0, 32768])])
+def test_bench_launcher_world2(extra, firsts):
+    """`python bench.py --gpus 2` (the driver's form without torchrun) starts two fresh rank
+    processes (gloo here, --dry-device: no GPU call) and rank 0 reports the 2-rank world,
+    both ranks' wall times and their disjoint block ranges in its one JSON line."""
+    r = _bench("--gpus", "2", "--dry-device", "--steps", "3", "--warmup", "0", *extra)
+    assert r.returncode == 0, r.stderr
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and line["ranks"]["world_size"] == 2 and line["ranks"]["backend"] == "gloo"
+    assert len(line["ranks"]["wall_s"]) == 2 and line["ranks"]["first_block"] == firsts
+    assert line["scaling"] == ("strong" if extra else "weak")
+
+
+def test_bench_launcher_fails_loudly():
+    """A rank that fails makes the launcher exit non-zero; an external launcher whose world
+    differs from --gpus is refused."""
+    r = _bench("--gpus", "2", "--dry-device", "--steps", "1", "--dry-fail-rank", "1")
+    assert r.returncode != 0
+    r = _bench("--gpus", "2", "--dry-device", "--steps", "1", env_extra={"WORLD_SIZE": "1", "RANK": "0"})
+    assert r.returncode != 0 and "launcher started 1 rank" in r.stderr

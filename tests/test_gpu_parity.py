@@ -826,6 +826,7 @@ def test_tail_chunk_encode_decode(ctx, dev, k, m, S):
     blocks = np.stack([np.frombuffer(o.block_bytes(3100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
     rec = gpu_encode(ctx, dev, blocks, m)
     assert np.array_equal(rec, ro_c.encode_blocks(blocks, m, threads=8))
+    other = np.stack([np.frombuffer(o.block_bytes(9100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
     rng = random.Random(k * 10007 + m * 101 + S)
     for per_block in (False, True):
         op, rp = [], []
@@ -843,6 +844,9 @@ def test_tail_chunk_encode_decode(ctx, dev, k, m, S):
                 if not rp[pb * m + j]:
                     d_r[b, j] = 0xC3
         for mode in (rs.DECODE_ANY_K, rs.DECODE_EXACT):
+            # the restride staging buffer keeps its bytes between calls: fill it with another
+            # codeword set first, so a decoder reading an absent (unpacked) slot would fail
+            gpu_encode(ctx, dev, other, m)
             got = gpu_decode(ctx, dev, d_o, d_r, op, rp, mode)
             assert np.array_equal(got, blocks), (per_block, mode)
 
