@@ -2478,6 +2478,53 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   }
   return AG_RS_OK;
 }
+// Step 6b of ag_shredder_deshred_batch for slice s: its datagram rows are parsed again into
+// the codeword (the pass before rewrote the restored and re-encoded rows), the kept shreds
+// (present bit mask) go through ReedSolomonCoder::deshred with the crate's EXACT decoder,
+// and the Merkle rebuild (roots2 row s, the slice's proof rows), root comparison and
+// SlicePayload parse are redone for this slice.  Outputs replace slice s's entries.
+int pipe_rerun_exact(ag_rs_ctx* c, size_t s, size_t S, const uint8_t* packets, size_t packet_stride,
+                     const uint32_t* packet_lens, const ag::ShredColumns& cols, uint8_t* wire, uint8_t* codewords,
+                     uint8_t* proof, uint8_t* roots2, const uint8_t* sroot, uint8_t* same, int64_t* plen,
+                     uint8_t* h_same, uint8_t* sstat, uint8_t* parent_flag, uint8_t* parent_id, uint32_t* data_offset,
+                     uint32_t* data_len, uint64_t present) {
+  constexpr size_t kRows = ag::kPipeShreds;
+  const size_t r0 = s * kRows, cw_stride = kRows * S;
+  uint8_t* cw = codewords + s * cw_stride;
+  ag::ShredColumns rc = cols;
+  rc.kind += r0;
+  rc.slot += r0;
+  rc.slice_index += r0;
+  rc.is_last += r0;
+  rc.shred_index += r0;
+  rc.data = cw;
+  rc.data_len += r0;
+  rc.sig += 64 * r0;
+  rc.proof += r0 * cols.proof_stride;
+  rc.height += r0;
+  if (ag::launch_shred_deserialize(packets + r0 * packet_stride, packet_stride, packet_lens + r0, kRows, rc, wire + r0,
+                                   c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  uint8_t dp[ag::kPipeData], cp[kRows - ag::kPipeData];
+  for (uint32_t j = 0; j < kRows; ++j) {
+    const uint8_t bit = static_cast<uint8_t>((present >> j) & 1);
+    if (j < ag::kPipeData) dp[j] = bit;
+    else cp[j - ag::kPipeData] = bit;
+  }
+  int st = ag_rs_coder_deshred_batch(c, kRows - ag::kPipeData, 1, S, cw, cw_stride, dp, cp, AG_RS_DECODE_EXACT, plen);
+  if (st) return st;
+  *h_same = 0;
+  if (*plen < 0) return AG_RS_OK;
+  if ((st = ag_merkle_build_batch(c, kRows, S, 1, cw, S, cw_stride, roots2 + 32 * s, nullptr, 0,
+                                  proof + r0 * cols.proof_stride, kRows * cols.proof_stride)))
+    return st;
+  if (ag::launch_pipe_root_cmp(roots2 + 32 * s, sroot + 32 * s, 1, same + s, c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  AG_HIP(hipMemcpyAsync(h_same, same + s, 1, hipMemcpyDeviceToHost, c->stream));
+  // synchronous: h_same has landed when it returns
+  return ag_slice_parse_batch(c, 1, cw, cw_stride, plen, sstat, parent_flag, parent_id, data_offset, data_len);
+}
+
 }  // namespace
 
 extern "C" {
@@ -2681,6 +2728,24 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   if ((st = ag_slice_parse_batch(c, n, codewords, cw_stride, plen.data(), sstat.data(), parent_flags_out,
                                  parent_ids_out, data_offsets_out, data_lens_out)))
     return st;  // synchronous: h_same has landed
+  // 6b. The crate's decoder reads every kept shred (reed_solomon.rs:154-166); the pass above
+  //     reads 32 of them (ANY_K).  On a consistent slice both restore the same bytes (MDS), and
+  //     a slice that passed check_merkle_tree is consistent: the rebuilt codeword matches the
+  //     signed root that commits every kept shred.  A slice that failed the padding or the
+  //     Merkle check with more than 32 kept shreds may hold an inconsistent shred the ANY_K
+  //     pass did not read (a leader signing a non-codeword), and the crate's bytes -- hence
+  //     the error, BadEncoding vs InvalidMerkleTree -- can differ.  Such slices are decoded
+  //     again from their received bytes with EXACT and re-checked, one by one (honest
+  //     leaders never produce them).
+  for (size_t s = 0; s < n; ++s) {
+    const bool failed = plen[s] == -AG_RS_ERR_INVALID_PADDING || (plen[s] >= 0 && !h_same[s]);
+    if (!failed || __builtin_popcountll(h_present[s]) <= static_cast<int>(ag::kPipeData)) continue;
+    if ((st = pipe_rerun_exact(c, s, S, packets, packet_stride, packet_lens, cols, wire, codewords, proof, roots2,
+                               sroot, same, &plen[s], &h_same[s], &sstat[s], parent_flags_out + s,
+                               parent_ids_out + AG_SLICE_BLOCK_ID_BYTES * s, data_offsets_out + s,
+                               data_lens_out + s, h_present[s])))
+      return st;
+  }
   std::vector<uint8_t> ok(n);
   for (size_t s = 0; s < n; ++s) {
     int32_t r = AG_RS_OK;

@@ -8,8 +8,15 @@ Follows /root/reference/src/shredder.rs:
        sign(SliceCommitment(header, root)) (:540, :206-222), assemble_output_shreds /
        fill_missing_shreds (:551-611): shred j carries the header, index j, its raw shred,
        the slice signature and tree.create_proof(j); data shreds first.
-  Shredder::deshred (:282-311): ValidatedShreds layout -> ReedSolomonCoder::deshred ->
-    check_merkle_tree (:616-625) -> SlicePayload::try_from -> fill_missing_shreds.
+  Shredder::deshred (:282-311): ValidatedShreds layout -> ReedSolomonCoder::deshred (the
+    crate's decoder over EVERY kept shred, reed_solomon.rs:154-166: rs_oracle.decode) ->
+    check_merkle_tree (:616-625) -> SlicePayload::try_from -> fill_missing_shreds (:576-611).
+  The receiver in front of it (`receive`): network::deserialize, the datagram's slot
+    (shred index, kind, shred size, path length), ValidatedShred::try_new
+    (validated_shred.rs:52-81) with the blockstore's cached commitment -- the first fitting
+    shred of a slice is checked by signature and caches its commitment -- and the shreds kept
+    for the slice: the valid ones with the first valid one's commitment.  This is the
+    receive model ag_shredder_deshred_batch documents (include/alpenglow_rs.h section 9).
 Datagrams are network::serialize(&Shred) (shred_wire_oracle).  Each stage is the pinned or
 restated oracle of its own row (slice_oracle, rs_oracle, merkle_oracle, ed25519_oracle,
 shred_wire_oracle); this module only composes them.
@@ -41,3 +48,68 @@ def shred(parent, data: bytes, slot: int, slice_index: int, is_last: bool, seed:
     raw = o.coder_shred(so.payload_bytes(parent, data), TOTAL_SHREDS - DATA_SHREDS)
     pkts, root, sig = datagrams(raw.data, raw.coding, slot, slice_index, is_last, seed)
     return pkts, raw, root, sig
+
+
+# ---- the receive side ---------------------------------------------------------------------
+
+HEIGHT = 6  # Merkle path length of a 64-leaf slice tree
+
+# per-slice results (AG_RS_OK / AG_RS_ERR_* of include/alpenglow_rs.h)
+OK, NOT_ENOUGH_SHARDS, TOO_MUCH_DATA, BAD_ENCODING, INVALID_MERKLE_TREE = 0, 9, 20, 23, 24
+
+
+def receive(rows, pk: bytes, shred_bytes: int):
+    """The shreds a receiver keeps for one slice from its 64 datagram slots (bytes or None):
+    a list of 64 entries, None or dict(kind, slot, slice_index, is_last, data, sig, root)."""
+    parsed = [wire.deserialize(p) if p else None for p in rows]
+
+    def fits(j):
+        x = parsed[j]
+        return (x is not None and x[4] == j and x[0] == (wire.CODING if j >= DATA_SHREDS else wire.DATA) and
+                len(x[5]) == shred_bytes and len(x[7]) == HEIGHT)
+
+    commit, root = [None] * TOTAL_SHREDS, [None] * TOTAL_SHREDS
+    for j in range(TOTAL_SHREDS):
+        if fits(j):
+            _, slot, si, last, _, data, _, proof = parsed[j]
+            root[j] = mk.derive_root(data, j, proof)  # Shred::slice_root (shredder.rs:169-175)
+            commit[j] = ed.slice_commitment(slot, si, last, root[j])
+    fitting = [j for j in range(TOTAL_SHREDS) if commit[j] is not None]
+    if not fitting:
+        return [None] * TOTAL_SHREDS
+    first = fitting[0]
+    cached = commit[first] if ed.validate_shred(commit[first], parsed[first][6], pk, None) == ed.OK else None
+    valid = [j for j in fitting if ed.validate_shred(commit[j], parsed[j][6], pk, cached) == ed.OK]
+    out = [None] * TOTAL_SHREDS
+    for j in valid:
+        if commit[j] == commit[valid[0]]:
+            kind, slot, si, last, _, data, sig, _ = parsed[j]
+            out[j] = dict(kind=kind, slot=slot, slice_index=si, is_last=last, data=data, sig=sig, root=root[j])
+    return out
+
+
+def deshred(kept):
+    """Shredder::deshred (shredder.rs:282-311) for RegularShredder on the kept shreds.
+    Returns (status, result): result = dict(payload parse, raw shreds, the 64 datagrams with
+    the missing ones filled in) for OK, else None."""
+    if all(x is None for x in kept):
+        return NOT_ENOUGH_SHARDS, None
+    shreds = [(j < DATA_SHREDS, x["data"]) if x is not None else None for j, x in enumerate(kept)]
+    try:
+        payload, raw = o.coder_deshred(shreds, DATA_SHREDS, TOTAL_SHREDS - DATA_SHREDS)
+    except o.RSError as e:
+        return {"NotEnoughShreds": NOT_ENOUGH_SHARDS, "TooMuchData": TOO_MUCH_DATA,
+                "InvalidPadding": BAD_ENCODING}[e.kind], None
+    any_shred = next(x for x in kept if x is not None)
+    tree = mk.slice_tree(raw.data, raw.coding)
+    if tree.root() != any_shred["root"]:
+        return INVALID_MERKLE_TREE, None
+    st, parent, data = so.try_from(payload)
+    if st != so.OK:
+        return (TOO_MUCH_DATA if st == so.TOO_LARGE else BAD_ENCODING), None
+    shards = raw.data + raw.coding
+    dgrams = [wire.serialize(wire.DATA if j < DATA_SHREDS else wire.CODING, any_shred["slot"],
+                             any_shred["slice_index"], any_shred["is_last"], j, shards[j], any_shred["sig"],
+                             tree.create_proof(j)) for j in range(TOTAL_SHREDS)]
+    return OK, dict(parent=parent, data=data, raw=raw, header=(any_shred["slot"], any_shred["slice_index"],
+                                                               any_shred["is_last"]), datagrams=dgrams)

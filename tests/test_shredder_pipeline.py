@@ -111,19 +111,62 @@ def _deshred(ctx, dev, rows, pk, S):
     return res, _packets(d_buf, d_ln, n), cw.cpu().numpy()
 
 
+def _expect(rows, pk_bytes, S):
+    """The oracle's verdict for every slice: receive (the receiver's checks) + Shredder::deshred
+    with the crate's decoder over every kept shred, and the datagram slots after the call
+    (kept ones as received, the others filled for a successful slice, untouched otherwise)."""
+    out = []
+    for r in rows:
+        kept = so.receive(r, pk_bytes, S)
+        st, res = so.deshred(kept)
+        if st == so.OK:
+            slots = [r[j] if kept[j] is not None else res["datagrams"][j] for j in range(64)]
+        else:
+            slots = [x if x is not None else b"" for x in r]
+        out.append((st, res, slots))
+    return out
+
+
+def _check_against_oracle(res, out, cw, want):
+    assert res.status.tolist() == [w[0] for w in want], \
+        ([rs.STATUS_KIND.get(int(x), int(x)) for x in res.status], [w[0] for w in want])
+    for b, (st, r, slots) in enumerate(want):
+        assert out[b] == slots, b
+        if st != so.OK:
+            continue
+        assert (int(res.slots[b]), int(res.slice_indices[b]), bool(res.is_last[b])) == r["header"]
+        assert res.parents[b] == r["parent"]
+        off, n = int(res.data_offsets[b]), int(res.data_lens[b])
+        assert cw[b, off:off + n].tobytes() == r["data"]
+        assert cw[b].tobytes() == b"".join(r["raw"].data + r["raw"].coding)
+
+
+def _non_codeword(slice_, tamper):
+    """The 64 datagrams of a leader that signs shreds which are no codeword: the slice's raw
+    shreds with shred `tamper` altered after encoding."""
+    p, d, slot, si, last = slice_
+    raw = o.coder_shred(sl.payload_bytes(p, d), 32)
+    shards = list(raw.data) + list(raw.coding)
+    shards[tamper] = bytes(x ^ 0x5A for x in shards[tamper])
+    return so.datagrams(shards[:32], shards[32:], slot, si, last, SEED)[0]
+
+
 def test_deshred_batch_matches_oracle(ctx, dev):
-    """Shredder::deshred behind the receiver's checks, one slice per outcome: all present,
-    a random half, 31 shreds (NotEnoughShreds), a tampered datagram (dropped), a leader whose
-    signed shreds are no codeword (InvalidMerkleTree), a payload that is no SlicePayload
-    and one without padding marker (BadEncoding), a datagram in the wrong slot, a shred
-    signed by another key.  Failed slices keep their datagrams; successful ones get every
-    missing datagram, byte-exact."""
+    """Shredder::deshred behind the receiver's checks, one slice per outcome, the expected
+    verdicts and bytes from the oracle (oracle/shredder_oracle.py: receive + deshred with the
+    crate's decoder over every kept shred): all present, a random half, 31 shreds, a tampered
+    datagram (dropped), leaders signing non-codewords (with the inconsistent shred withheld,
+    held together with surplus shreds so that decoding from all kept shreds and from any 32
+    of them disagree, and held with the last data shred present), a payload that is no
+    SlicePayload and one without padding marker, a datagram in the wrong slot, a shred signed
+    by another key.  Failed slices keep their datagrams; successful ones get every missing
+    datagram, byte-exact."""
     S = 1024
     rng = random.Random(77)
-    slices = _slices(rng, 9, S)
+    slices = _slices(rng, 12, S)
     clean = [so.shred(p, d, slot, si, last, SEED) for p, d, slot, si, last in slices]
     rows = [list(c[0]) for c in clean]
-    keep = [None] * 9
+    keep = [None] * 12
     # 1: a random half; 2: 31 shreds; 3: 40 shreds, one tampered
     for b, cnt in ((1, 32), (2, 31), (3, 40)):
         keep[b] = set(rng.sample(range(64), cnt))
@@ -132,11 +175,7 @@ def test_deshred_batch_matches_oracle(ctx, dev):
     bad[40] ^= 1  # payload byte: the Merkle path no longer derives the signed root
     rows[3][t] = bytes(bad)
     # 4: the leader signs shreds that are no codeword; the receiver lacks the odd one
-    p4, d4, slot4, si4, last4 = slices[4]
-    raw = o.coder_shred(sl.payload_bytes(p4, d4), 32)
-    coding = list(raw.coding)
-    coding[8] = bytes(x ^ 0x5A for x in coding[8])
-    rows[4], _, _ = so.datagrams(raw.data, coding, slot4, si4, last4, SEED)
+    rows[4] = _non_codeword(slices[4], 40)
     keep[4] = set(range(64)) - {40}
     # 5: valid padding, but the payload is no SlicePayload (Option tag 7)
     payload5 = b"\x07" + bytes(rng.randrange(256) for _ in range(32705))  # pads to S = 1024
@@ -154,21 +193,45 @@ def test_deshred_batch_matches_oracle(ctx, dev):
     seed8 = bytes(range(100, 132))
     other, _, _ = so.datagrams(clean[8][1].data, clean[8][1].coding, slices[8][2], slices[8][3], slices[8][4], seed8)
     rows[8][0] = other[0]
+    # 9: non-codeword (coding shred 62 altered) held by the receiver with data shreds 16..31
+    #    missing: any 32 survivors (data 0..15 + coding 32..47) restore the honest data, which
+    #    pads fine and then fails the Merkle check; the crate decodes from all 48 and restores
+    #    other bytes, whose padding decides first
+    rows[9] = _non_codeword(slices[9], 62)
+    keep[9] = set(range(16)) | set(range(32, 64))
+    # 10: the same with the last data shred held (data 8..23 missing): padding on received bytes
+    rows[10] = _non_codeword(slices[10], 62)
+    keep[10] = (set(range(8)) | set(range(24, 32))) | set(range(32, 64))
+    # 11: the leader altered data shred 5; the receiver holds it and 40 others
+    rows[11] = _non_codeword(slices[11], 5)
+    keep[11] = {5} | set(rng.sample([j for j in range(64) if j != 5], 40))
     inp = [[r[j] if keep[b] is None or j in keep[b] else None for j in range(64)] for b, r in enumerate(rows)]
-    pk = _dev(np.frombuffer(ed.secret_to_public(SEED), np.uint8), dev)
+    pk_bytes = ed.secret_to_public(SEED)
+    want = _expect(inp, pk_bytes, S)
+    assert [w[0] for w in want][:9] == [0, 0, 9, 0, 24, 23, 23, 0, 0]  # the outcomes named above
+    assert want[9][0] == 23 and want[10][0] == 24  # the crate's decoder decides case 9
+    pk = _dev(np.frombuffer(pk_bytes, np.uint8), dev)
     res, out, cw = _deshred(ctx, dev, inp, pk, S)
-    want = [0, 0, 9, 0, 24, 23, 23, 0, 0]  # OK, NotEnoughShards, InvalidMerkleTree, BadEncoding
-    assert res.status.tolist() == want, [rs.STATUS_KIND.get(int(x), int(x)) for x in res.status]
-    for b, (parent, data, slot, si, last) in enumerate(slices):
-        if want[b] != 0:
-            assert out[b] == [x if x is not None else b"" for x in inp[b]], b  # untouched
-            continue
-        assert out[b] == clean[b][0], b  # present ones intact, missing ones filled
-        assert (int(res.slots[b]), int(res.slice_indices[b]), bool(res.is_last[b])) == (slot, si, last)
-        assert res.parents[b] == parent
-        off, n = int(res.data_offsets[b]), int(res.data_lens[b])
-        assert cw[b, off:off + n].tobytes() == data
-        assert cw[b].tobytes() == b"".join(clean[b][1].data + clean[b][1].coding)
+    _check_against_oracle(res, out, cw, want)
+
+
+def test_deshred_batch_adversarial_random(ctx, dev):
+    """24 slices, about half of them from a leader that altered one random shred after
+    encoding, each received as a random 32..64 of its datagrams: verdicts, filled datagrams
+    and raw shreds equal the oracle's (every kept shred through the crate's decoder)."""
+    S = 1024
+    rng = random.Random(2024)
+    slices = _slices(rng, 24, S)
+    inp = []
+    for b, sl_ in enumerate(slices):
+        rows = _non_codeword(sl_, rng.randrange(64)) if b % 2 else so.shred(*sl_[:5], SEED)[0]
+        keep = set(rng.sample(range(64), rng.randrange(32, 65)))
+        inp.append([rows[j] if j in keep else None for j in range(64)])
+    pk_bytes = ed.secret_to_public(SEED)
+    want = _expect(inp, pk_bytes, S)
+    pk = _dev(np.frombuffer(pk_bytes, np.uint8), dev)
+    res, out, cw = _deshred(ctx, dev, inp, pk, S)
+    _check_against_oracle(res, out, cw, want)
 
 
 def test_pipeline_roundtrip_random_arrival(ctx, dev):

@@ -13,7 +13,7 @@ stop_on_fatal() {  # $1 = exit code of a GPU step
   esac
 }
 rocm-smi --showproductname > $OUT/rocm_smi.txt 2>&1 || true
-timeout -k 10 900 python -m pytest tests -m gpu -x -q -p no:cacheprovider > $OUT/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -p no:cacheprovider --timeout 120 --timeout-method thread ${PYTEST_ARGS:-} > $OUT/pytest_gpu.log 2>&1
 rc=$?; echo "pytest gpu exit $rc"; tail -5 $OUT/pytest_gpu.log; stop_on_fatal $rc
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
 rc=$?; echo "smoke exit $rc"; tail -3 $OUT/smoke.log; stop_on_fatal $rc
