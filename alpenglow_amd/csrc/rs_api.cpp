@@ -108,7 +108,6 @@ int check_geometry(size_t k, size_t m, size_t S) {
   return AG_RS_OK;
 }
 
-bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 // Single-chunk HighRate geometries served by the bitsliced N-point transform kernel:
 // k <= N, next_pow2(m) == N, N in {32, 64}, whole 64-byte chunks.  Returns N or 0.
@@ -174,6 +173,7 @@ struct ag_rs_ctx {
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
   std::vector<uint64_t> xmask_host;       // last general-decode masks (d_xmask), W = xmask_w
   size_t xmask_w = 0;
+  bool xmask_poly = false;                // d_rows holds polynomial-basis constants (per-lane)
   std::vector<uint8_t> syn_key;             // (k, m, present flags) of the patterns in d_syn
   std::vector<uint8_t> corr_key;            // (k, m, present flags) of the patterns in d_corr
 
@@ -490,54 +490,56 @@ bool corr_enabled() {
 int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
                   size_t ostride, uint8_t* rec, size_t rstride);
 
-// Shard sizes that are not whole 64-byte chunks (a slice's tail, reed_solomon.rs:94-95), or
-// unaligned buffers: restride groups of blocks into padded shards (restride_kernel), run
-// the bitsliced kernels there, restride the outputs back.  Taken when the padded geometry
-// has a bitsliced path.
+// Shard sizes that are not whole 64-byte chunks (a slice's tail, reed_solomon.rs:94-95):
+// the whole chunks of every shard run in place on the bitsliced kernels (shard stride S,
+// chunks_per_shard = S / 64: the kernels take any alignment), and only the T = S mod 64 tail
+// bytes of each shard -- in the crate's tail layout exactly a T-byte shard --
+// are restrided into a padded 64-byte chunk per shard (restride_kernel), run there and
+// restrided back.  Taken when the padded geometry has a bitsliced path.
 size_t padded_shard(size_t S) { return (S + 63) / 64 * 64; }
-bool restride_wanted(size_t S, const void* a, const void* b, size_t sa, size_t sb) {
-  return S % 64 != 0 || !aligned16(a) || !aligned16(b) || sa % 16 != 0 || sb % 16 != 0;
+// Byte-odd buffers or strides: every shard goes through the restride (its byte path)
+bool odd_layout(const void* a, const void* b, size_t sa, size_t sb) {
+  return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | sa | sb) & 1) != 0;
 }
 
-int encode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
-                     size_t ostride, uint8_t* rec, size_t rstride) {
-  const size_t Sp = padded_shard(S), per_block = (k + m) * Sp;
+// Virtual shards of Sv bytes at byte `off` of every shard (shard stride sstride) are packed
+// into padded shards, encoded there, and the recovery shards' pieces unpacked.
+int encode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t Sv, size_t sstride, size_t off, size_t nblocks,
+                     const uint8_t* orig, size_t ostride, uint8_t* rec, size_t rstride) {
+  const size_t Sp = padded_shard(Sv), per_block = (k + m) * Sp;
   const size_t group = std::max<size_t>(1, kRestrideGroupBytes / per_block);
   int st = c->stage_pad.ensure(std::min(group, nblocks) * per_block, c->stream);
   if (st) return st;
   uint8_t* pad = c->stage_pad.as<uint8_t>();
   for (size_t b0 = 0; b0 < nblocks; b0 += group) {
     const size_t nb = std::min(group, nblocks - b0);
-    if (ag::launch_restride(orig + b0 * ostride, ostride, S, pad, per_block, Sp, static_cast<uint32_t>(S),
+    if (ag::launch_restride(orig + b0 * ostride + off, ostride, sstride, pad, per_block, Sp, static_cast<uint32_t>(Sv),
                             static_cast<uint32_t>(k), nb, false, nullptr, false, c->stream) != hipSuccess)
       return AG_RS_ERR_DEVICE;
     if ((st = encode_device(c, k, m, Sp, nb, pad, per_block, pad + k * Sp, per_block))) return st;
-    if (ag::launch_restride(pad + k * Sp, per_block, Sp, rec + b0 * rstride, rstride, S, static_cast<uint32_t>(S),
-                            static_cast<uint32_t>(m), nb, true, nullptr, false, c->stream) != hipSuccess)
+    if (ag::launch_restride(pad + k * Sp, per_block, Sp, rec + b0 * rstride + off, rstride, sstride,
+                            static_cast<uint32_t>(Sv), static_cast<uint32_t>(m), nb, true, nullptr, false,
+                            c->stream) != hipSuccess)
       return AG_RS_ERR_DEVICE;
   }
   return AG_RS_OK;
 }
 
-int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
-                  size_t ostride, uint8_t* rec, size_t rstride) {
-  if (nblocks == 0) return AG_RS_OK;
-  if (restride_wanted(S, orig, rec, ostride, rstride)) {
-    const size_t Sp = padded_shard(S);
-    if (xform_points(k, m, Sp) || mc_chunk(k, m, Sp) || lowrate_chunk(k, m, Sp))
-      return encode_restrided(c, k, m, S, nblocks, orig, ostride, rec, rstride);
-  }
+// The encode over the first S bytes of every shard (S % 64 == 0 on the bitsliced paths;
+// shards sstride >= S bytes apart).
+int encode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size_t nblocks, const uint8_t* orig,
+                size_t ostride, uint8_t* rec, size_t rstride) {
   const unsigned npts = xform_points(k, m, S);
   const unsigned mc = mc_chunk(k, m, S);
   const unsigned lr = lowrate_chunk(k, m, S);
-  if ((npts || mc || lr) && aligned16(orig) && aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0) {
+  if (npts || mc || lr) {
     ag::XformParams p{};
     p.in = orig;
     p.in_block_stride = ostride;
-    p.in_shard_stride = S;
+    p.in_shard_stride = sstride;
     p.out = rec;
     p.out_block_stride = rstride;
-    p.out_shard_stride = S;
+    p.out_shard_stride = sstride;
     p.n_in = static_cast<uint32_t>(k);
     p.n_out = static_cast<uint32_t>(m);
     p.chunks_per_shard = static_cast<uint32_t>(S / 64);
@@ -550,7 +552,7 @@ int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
     } else {
       for (size_t j = 0; j * lr < m && e == hipSuccess; ++j) {  // one launch per recovery chunk
         ag::XformParams pj = p;
-        pj.out = rec + j * lr * S;
+        pj.out = rec + j * lr * sstride;
         pj.n_out = static_cast<uint32_t>(std::min<size_t>(lr, m - j * lr));
         e = ag::launch_xform_lowrate(lr, static_cast<unsigned>(j), pj, c->stream);
       }
@@ -571,10 +573,10 @@ int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
     ag::GenericEncodeParams p{};
     p.orig = orig + b0 * ostride;
     p.orig_block_stride = ostride;
-    p.orig_shard_stride = S;
+    p.orig_shard_stride = sstride;
     p.rec = rec + b0 * rstride;
     p.rec_block_stride = rstride;
-    p.rec_shard_stride = S;
+    p.rec_shard_stride = sstride;
     p.k = static_cast<uint32_t>(k);
     p.m = static_cast<uint32_t>(m);
     p.high_rate = static_cast<uint32_t>(hr);
@@ -588,6 +590,22 @@ int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
     if (ag::launch_generic_encode(p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   }
   return AG_RS_OK;
+}
+
+int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
+                  size_t ostride, uint8_t* rec, size_t rstride) {
+  if (nblocks == 0) return AG_RS_OK;
+  const size_t Sp = padded_shard(S);
+  if (S % 2 == 0 && (xform_points(k, m, Sp) || mc_chunk(k, m, Sp) || lowrate_chunk(k, m, Sp))) {
+    if (odd_layout(orig, rec, ostride, rstride))
+      return encode_restrided(c, k, m, S, S, 0, nblocks, orig, ostride, rec, rstride);
+    const size_t full = S / 64 * 64, tail = S - full;
+    int st;
+    if (full && (st = encode_cols(c, k, m, full, S, nblocks, orig, ostride, rec, rstride))) return st;
+    if (tail && (st = encode_restrided(c, k, m, tail, S, full, nblocks, orig, ostride, rec, rstride))) return st;
+    return AG_RS_OK;
+  }
+  return encode_cols(c, k, m, S, S, nblocks, orig, ostride, rec, rstride);
 }
 
 // Host flag arrays (0 / nonzero bytes, one per shard) -> bit masks, 8 flags per step:
@@ -619,10 +637,10 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
 // The decode counterpart of encode_restrided: originals and recovery shards of a group of
 // blocks go to one padded buffer, the bitsliced decoders run there, and only the restored
 // originals are restrided back (a store mask per pattern).
-int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
-                     const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
-                     int mode) {
-  const size_t Sp = padded_shard(S), per_block = (k + m) * Sp;
+int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t Sv, size_t sstride, size_t off, size_t nblocks,
+                     uint8_t* orig, size_t ostride, const uint8_t* rec, size_t rstride, const uint8_t* opres,
+                     const uint8_t* rpres, size_t npat, int mode) {
+  const size_t Sp = padded_shard(Sv), per_block = (k + m) * Sp;
   for (size_t p = 0; p < npat; ++p)  // NotEnoughShards before anything is launched
     if (count_flags(opres + p * k, k) + count_flags(rpres + p * m, m) < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
   // store masks: the absent originals of each pattern (k <= 64 on every bitsliced path)
@@ -646,16 +664,16 @@ int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks,
   for (size_t b0 = 0; b0 < nblocks; b0 += group) {
     const size_t nb = std::min(group, nblocks - b0);
     const size_t p0 = npat > 1 ? b0 : 0, np = npat > 1 ? nb : 1;
-    if (ag::launch_restride(orig + b0 * ostride, ostride, S, pad, per_block, Sp, static_cast<uint32_t>(S),
+    if (ag::launch_restride(orig + b0 * ostride + off, ostride, sstride, pad, per_block, Sp, static_cast<uint32_t>(Sv),
                             static_cast<uint32_t>(k), nb, false, d_omask + p0, npat > 1, c->stream) != hipSuccess ||
-        ag::launch_restride(rec + b0 * rstride, rstride, S, pad + k * Sp, per_block, Sp, static_cast<uint32_t>(S),
-                            static_cast<uint32_t>(m), nb, false, d_rmask ? d_rmask + p0 : nullptr, npat > 1,
-                            c->stream) != hipSuccess)
+        ag::launch_restride(rec + b0 * rstride + off, rstride, sstride, pad + k * Sp, per_block, Sp,
+                            static_cast<uint32_t>(Sv), static_cast<uint32_t>(m), nb, false,
+                            d_rmask ? d_rmask + p0 : nullptr, npat > 1, c->stream) != hipSuccess)
       return AG_RS_ERR_DEVICE;
     if ((st = decode_device(c, k, m, Sp, nb, pad, per_block, pad + k * Sp, per_block, opres + p0 * k, rpres + p0 * m,
                             np, mode)))
       return st;
-    if (ag::launch_restride(pad, per_block, Sp, orig + b0 * ostride, ostride, S, static_cast<uint32_t>(S),
+    if (ag::launch_restride(pad, per_block, Sp, orig + b0 * ostride + off, ostride, sstride, static_cast<uint32_t>(Sv),
                             static_cast<uint32_t>(k), nb, true, c->stage_mask.as<uint64_t>() + p0, npat > 1,
                             c->stream) != hipSuccess)
       return AG_RS_ERR_DEVICE;
@@ -664,17 +682,36 @@ int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks,
   return AG_RS_OK;
 }
 
+// The decode over the first S bytes of every shard (S % 64 == 0 on the bitsliced paths;
+// shards sstride >= S bytes apart; any alignment).
+int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size_t nblocks, uint8_t* orig,
+                size_t ostride, const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres,
+                size_t npat, int mode);
+
 int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
                   const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
                   int mode) {
   if (nblocks == 0) return AG_RS_OK;
-  if (k <= 64 && restride_wanted(S, orig, rec, ostride, rstride)) {
+  const bool odd = odd_layout(orig, rec, ostride, rstride);
+  if (k <= 64 && (S % 64 != 0 || odd) && S % 2 == 0) {
     const size_t Sp = padded_shard(S);
     const int hr = ag::use_high_rate(k, m);
     const size_t xw = hr == 1 ? next_pow2(next_pow2(m) + k) : 0;
-    if (xform_points(k, m, Sp) || mc_chunk(k, m, Sp) || lowrate_chunk(k, m, Sp) || xw == 32 || xw == 64)
-      return decode_restrided(c, k, m, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
+    if (xform_points(k, m, Sp) || mc_chunk(k, m, Sp) || lowrate_chunk(k, m, Sp) || xw == 32 || xw == 64) {
+      if (odd) return decode_restrided(c, k, m, S, S, 0, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
+      const size_t full = S / 64 * 64, tail = S - full;
+      int st;
+      if (full && (st = decode_cols(c, k, m, full, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode)))
+        return st;
+      return decode_restrided(c, k, m, tail, S, full, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
+    }
   }
+  return decode_cols(c, k, m, S, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
+}
+
+int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size_t nblocks, uint8_t* orig,
+                size_t ostride, const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres,
+                size_t npat, int mode) {
   const int hr = ag::use_high_rate(k, m);
   // one erasure pattern repeated for every block (a repair batch, a uniform loss) is one
   // pattern: uniform store masks, and the bitsliced kernels regardless of block alignment
@@ -689,7 +726,7 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   // The transform inverts the encoder only when all N recovery points exist (m == N):
   // with m < N the points m..N-1 were never stored.
   std::vector<uint8_t> cls(npat);
-  const bool aligned = aligned16(orig) && aligned16(rec) && ostride % 16 == 0 && rstride % 16 == 0;
+  const bool aligned = true;  // the bitsliced kernels take any alignment (16-byte pieces, unaligned mode)
   const unsigned npts = xform_points(k, m, S);
   const bool fast_geo = mode == AG_RS_DECODE_ANY_K && npts != 0 && m == npts && aligned;
   // decode_x window: HighRate, W = next_pow2(chunk + k) in {32, 64}; or the LowRate
@@ -782,10 +819,10 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     ag::XformParams p{};
     p.in = rec;
     p.in_block_stride = rstride;
-    p.in_shard_stride = S;
+    p.in_shard_stride = sstride;
     p.out = orig;
     p.out_block_stride = ostride;
-    p.out_shard_stride = S;
+    p.out_shard_stride = sstride;
     p.out_mask = c->d_mask.as<uint64_t>();
     p.pattern_per_block = npat > 1 ? 1u : 0u;
     p.n_in = static_cast<uint32_t>(m);
@@ -814,12 +851,12 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
       c->mask_host = mask;
       AG_HIP(hipMemcpyAsync(c->d_mask.ptr, c->mask_host.data(), mask.size() * 8, hipMemcpyHostToDevice, c->stream));
       ag::XformParams p{};
-      p.in = rec + static_cast<size_t>(32) * j * S;
+      p.in = rec + static_cast<size_t>(32) * j * sstride;
       p.in_block_stride = rstride;
-      p.in_shard_stride = S;
+      p.in_shard_stride = sstride;
       p.out = orig;
       p.out_block_stride = ostride;
-      p.out_shard_stride = S;
+      p.out_shard_stride = sstride;
       p.out_mask = c->d_mask.as<uint64_t>();
       p.pattern_per_block = npat > 1 ? 1u : 0u;
       p.n_in = 32;
@@ -850,10 +887,10 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     ag::DecodeSynParams p{};
     p.rec = rec;
     p.rec_block_stride = rstride;
-    p.rec_shard_stride = S;
+    p.rec_shard_stride = sstride;
     p.orig = orig;
     p.orig_block_stride = ostride;
-    p.orig_shard_stride = S;
+    p.orig_shard_stride = sstride;
     p.pat = c->d_syn.as<ag::SynPattern>();
     p.k = static_cast<uint32_t>(k);
     p.chunks_per_shard = static_cast<uint32_t>(cps);
@@ -908,10 +945,10 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     ag::DecodeCParams p{};
     p.rec = rec;
     p.rec_block_stride = rstride;
-    p.rec_shard_stride = S;
+    p.rec_shard_stride = sstride;
     p.orig = orig;
     p.orig_block_stride = ostride;
-    p.orig_shard_stride = S;
+    p.orig_shard_stride = sstride;
     p.pat = c->d_corr.as<ag::CorrPattern>();
     p.kpool = c->d_corrk.as<uint32_t>();
     p.k = static_cast<uint32_t>(k);
@@ -968,25 +1005,28 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
       xm[npat + 2 * p] = in;
       xm[npat + 2 * p + 1] = out;
     }
-    if (xm != c->xmask_host || xw != c->xmask_w) {
+    // per-lane patterns multiply by polynomial-basis constants (one word per position)
+    const bool poly = npat > 1 && x_per_lane;
+    if (xm != c->xmask_host || xw != c->xmask_w || poly != c->xmask_poly) {
       AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read xmask_host
       if ((st = c->d_xmask.ensure(xm.size() * 8, c->stream))) return st;
-      if ((st = c->d_rows.ensure(npat * xw * 16 * 4, c->stream))) return st;
+      if ((st = c->d_rows.ensure(npat * xw * (poly ? 1 : 16) * 4, c->stream))) return st;
       c->xmask_host = xm;
       c->xmask_w = xw;
+      c->xmask_poly = poly;
       AG_HIP(hipMemcpyAsync(c->d_xmask.ptr, c->xmask_host.data(), xm.size() * 8, hipMemcpyHostToDevice, c->stream));
       const uint64_t* dx = c->d_xmask.as<uint64_t>();
       if (ag::launch_decode_rows(dx, dx + npat, static_cast<uint32_t>(npat), static_cast<uint32_t>(xw), c->dtables(),
-                                 c->d_rows.as<uint32_t>(), c->stream) != hipSuccess)
+                                 c->d_rows.as<uint32_t>(), poly, c->stream) != hipSuccess)
         return AG_RS_ERR_DEVICE;
     }
     ag::DecodeXParams p{};
     p.rec = rec;
     p.rec_block_stride = rstride;
-    p.rec_shard_stride = S;
+    p.rec_shard_stride = sstride;
     p.orig = orig;
     p.orig_block_stride = ostride;
-    p.orig_shard_stride = S;
+    p.orig_shard_stride = sstride;
     p.pmask = c->d_xmask.as<uint64_t>() + npat;
     p.rows = c->d_rows.as<uint32_t>();
     p.k = static_cast<uint32_t>(k);
@@ -1068,10 +1108,10 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
     ag::GenericDecodeParams p{};
     p.orig = orig;
     p.orig_block_stride = ostride;
-    p.orig_shard_stride = S;
+    p.orig_shard_stride = sstride;
     p.rec = rec;
     p.rec_block_stride = rstride;
-    p.rec_shard_stride = S;
+    p.rec_shard_stride = sstride;
     p.orig_present = dflags;
     p.rec_present = dflags + npat * k;
     p.pattern_per_block = npat > 1 ? 1u : 0u;
@@ -2421,7 +2461,7 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   const size_t cps = S / 64;
   int st;
   if ((st = c->ensure_tables()) || (st = c->d_xmask.ensure(3 * n * 8, c->stream)) ||
-      (st = c->d_rows.ensure(n * W * 16 * 4, c->stream)) || (st = c->d_pipe_few.ensure(n, c->stream)) ||
+      (st = c->d_rows.ensure(n * W * 4, c->stream)) || (st = c->d_pipe_few.ensure(n, c->stream)) ||
       (st = c->d_pipe_mask.ensure(8 * n, c->stream)) || (st = c->d_strip.ensure(8 * n, c->stream)))
     return st;
   c->xmask_host.clear();  // d_xmask / d_rows no longer hold decode_device's cached patterns
@@ -2430,7 +2470,7 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   uint8_t* few = c->d_pipe_few.as<uint8_t>();
   if (ag::launch_pipe_patterns(d_present, n, xm, few, c->stream) != hipSuccess ||
       ag::launch_decode_rows(xm, xm + n, static_cast<uint32_t>(n), static_cast<uint32_t>(W), c->dtables(),
-                             c->d_rows.as<uint32_t>(), c->stream) != hipSuccess)
+                             c->d_rows.as<uint32_t>(), true, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   ag::DecodeXParams p{};
   p.rec = cw + k * S;

@@ -83,6 +83,65 @@ __device__ __forceinline__ void mul_acc(uint32_t* x, const uint32_t* y) {
   });
 }
 
+// out = B x for the basis changes of rs_consts.inc (B = 0: Cantor -> polynomial basis,
+// 1: back), out of place, as a CSE'd XOR network.
+template <int B>
+__device__ __forceinline__ void basis_apply(const uint32_t* x, uint32_t* out) {
+  constexpr int NT = kBasisNTemps[B];
+  uint32_t sig[16 + kBasisMaxTemps];
+  static_for<16>([&](auto I) { sig[decltype(I)::value] = x[decltype(I)::value]; });
+  static_for<NT>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    constexpr int a = kBasisTemp[B][j][0], b = kBasisTemp[B][j][1], c = kBasisTemp[B][j][2];
+    if constexpr (c == 255) sig[16 + j] = sig[a] ^ sig[b]; else sig[16 + j] = xor3(sig[a], sig[b], sig[c]);
+  });
+  static_for<16>([&](auto O) {
+    constexpr int o = decltype(O)::value;
+    constexpr uint64_t row = kBasisRow[B][o];
+    constexpr int first = __builtin_ctzll(row);
+    out[o] = xsum64<row & (row - 1)>(sig[first], sig);
+  });
+}
+
+// x <- c x for a runtime constant c that differs per lane (per-lane erasure patterns).
+// `coef` holds c in the polynomial basis (bit i: coefficient of a^i).  Horner over the 16
+// coefficients in the polynomial basis, where a multiply by a is a plane shift plus 3
+// XORs (a^16 = a^5 + a^3 + a^2 + 1): 16 x 16 masked XORs, 45 XORs, 16 masks and the two
+// basis changes (~70 XORs), against 256 masks + 256 masked XORs for a row matrix.
+__device__ __forceinline__ void mul_rt_poly(uint32_t* x, uint32_t coef) {
+  uint32_t X[16], acc[16];
+  basis_apply<0>(x, X);
+  {
+    const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(coef), 15, 1));
+    static_for<16>([&](auto P) { acc[decltype(P)::value] = X[decltype(P)::value] & m; });
+  }
+  static_for<15>([&](auto I) {
+    constexpr int i = 14 - decltype(I)::value;
+    const uint32_t top = acc[15];
+    static_for<15>([&](auto P) {
+      constexpr int q = 15 - decltype(P)::value;  // 15 .. 1
+      acc[q] = acc[q - 1];
+    });
+    acc[0] = top;
+    acc[2] ^= top;
+    acc[3] ^= top;
+    acc[5] ^= top;
+    const uint32_t m = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(coef), i, 1));
+    static_for<16>([&](auto P) {
+      constexpr int q = decltype(P)::value;
+      acc[q] = __builtin_amdgcn_bitop3_b32(acc[q], X[q], m, 0x78);  // acc ^ (X & m)
+    });
+  });
+  basis_apply<1>(acc, x);
+}
+
+// the polynomial-basis form of a Cantor-coordinate element (host or device)
+__host__ __device__ constexpr uint32_t to_poly(uint32_t c) {
+  uint32_t r = 0;
+  for (int o = 0; o < 16; ++o) r |= static_cast<uint32_t>(__builtin_popcount(kBasisMat[0][o] & c) & 1) << o;
+  return r;
+}
+
 __device__ __forceinline__ void xor_planes(uint32_t* y, const uint32_t* x) {
   static_for<16>([&](auto P) {
     constexpr int p = decltype(P)::value;

@@ -110,7 +110,7 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
       const uint8_t* base = p.in + sh * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        const uint4 x = ld_piece(base + io.off[q]);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -537,33 +537,6 @@ __device__ __forceinline__ void xf_derivative(int wave, int lane, uint4* lds, Re
   });
 }
 
-// x <- M x for a runtime matrix that differs per lane (per-lane erasure patterns): rows
-// are this lane's 16 row words; every term is one v_bitop3 with a v_bfe_i32 mask.
-template <typename RowPtr>
-__device__ __forceinline__ void mul_rt_lane(uint32_t* x, RowPtr rows) {
-  uint32_t r[16];
-  static_for<4>([&](auto Q) {
-    constexpr int q = decltype(Q)::value;
-    const uint4 v = reinterpret_cast<const uint4*>(rows)[q];
-    r[4 * q] = v.x;
-    r[4 * q + 1] = v.y;
-    r[4 * q + 2] = v.z;
-    r[4 * q + 3] = v.w;
-  });
-  uint32_t y[16];
-  static_for<16>([&](auto O) {
-    constexpr int o = decltype(O)::value;
-    uint32_t acc = 0;
-    static_for<16>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const uint32_t msk = static_cast<uint32_t>(__builtin_amdgcn_sbfe(static_cast<int>(r[o]), i, 1));
-      acc = __builtin_amdgcn_bitop3_b32(acc, x[i], msk, 0x78);  // acc ^ (x & msk)
-    });
-    y[o] = acc;
-  });
-  static_for<16>([&](auto O) { x[decltype(O)::value] = y[decltype(O)::value]; });
-}
-
 // PL: per-lane patterns (tiles straddle blocks: shard sizes below 4 KiB, e.g. the 1 KiB
 // shreds of the reference's slices).  Every lane then owns one whole 64-byte chunk of one
 // block (four 16-byte loads of its own chunk, no lane exchange), reads its block's pattern
@@ -587,7 +560,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
     in_mask = ok ? p.pmask[2 * blk] : 0;
     out_mask = ok ? p.pmask[2 * blk + 1] : 0;
-    rows = p.rows + blk * (W * 16);
+    rows = p.rows + blk * W;  // polynomial-basis constants, one word per position
     off_r = blk * p.rec_block_stride + col * 64;
     off_o = blk * p.orig_block_stride + col * 64;
   } else {
@@ -635,7 +608,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     if ((in_mask >> j) & 1) {
       if constexpr (!PL) swap_halves(ra[t]);
       dev::planes_from_raw(ra[t]);
-      if constexpr (PL) mul_rt_lane(ra[t], rows + j * 16); else mul_rt_dx(ra[t], rows + j * 16);
+      if constexpr (PL) dev::mul_rt_poly(ra[t], rows[j]); else mul_rt_dx(ra[t], rows + j * 16);
     }
   });
   xf_pass_a<NW, 0>(wave, ra);
@@ -658,7 +631,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     if ((out_mask >> j) & 1) {
       uint8_t* dst = p.orig + (j - (p.low_rate ? 0 : p.chunk)) * p.orig_shard_stride;
       if constexpr (PL) {
-        mul_rt_lane(ra[t], rows + j * 16);
+        dev::mul_rt_poly(ra[t], rows[j]);
         dev::store_chunk(dst + off_o, ra[t]);
       } else {
         mul_rt_dx(ra[t], rows + j * 16);
@@ -692,38 +665,36 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
   constexpr int W = 64;
   __shared__ uint4 lds[32 * 4 * kXfLanes];  // 16 waves x 2 slots x 4 KiB
   __shared__ XFlags<16> flags;
-  // PL with 16 or 32 chunks per shard: the tile's 4 (2) blocks' multiply rows, staged once
-  // by the workgroup (one 16-byte load per thread) instead of 48 dependent 64-byte loads
-  // per lane, each exposing its latency to the product that waits on it
-  __shared__ uint4 lrows[4 * W * 4];
+  // PL: the polynomial-basis constants (one word per position) of the <= 64 blocks the
+  // tile's columns belong to, staged once by the workgroup instead of a dependent global
+  // load per product
+  __shared__ uint32_t lcoef[kXfLanes * W];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
-  const bool staged = PL && (p.chunks_per_shard == 16 || p.chunks_per_shard == 32);
-  if (staged) {
-    const uint32_t nbt = kXfLanes / p.chunks_per_shard;
-    const uint64_t b0 = static_cast<uint64_t>(tile) * kXfLanes / p.chunks_per_shard;
-    const uint64_t nblocks = p.total_columns / p.chunks_per_shard;
-    const uint32_t lb = threadIdx.x / (W * 4);
-    if (lb < nbt && b0 + lb < nblocks)
-      lrows[threadIdx.x] = reinterpret_cast<const uint4*>(p.rows + (b0 + lb) * (W * 16))[threadIdx.x % (W * 4)];
+  uint64_t sb0 = 0;  // PL: first block of the tile
+  if constexpr (PL) {
+    const uint64_t c0 = static_cast<uint64_t>(tile) * kXfLanes;
+    const uint64_t c1 = c0 + kXfLanes - 1 < p.total_columns ? c0 + kXfLanes - 1 : p.total_columns - 1;
+    sb0 = c0 / p.chunks_per_shard;
+    const uint32_t nbt = static_cast<uint32_t>(c1 / p.chunks_per_shard - sb0 + 1);  // <= 64
+    for (uint32_t i = threadIdx.x; i < nbt * W; i += blockDim.x) lcoef[i] = p.rows[(sb0 + i / W) * W + i % W];
   }
   if (threadIdx.x < 32) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
   uint64_t in_mask, out_mask;
   const uint32_t* rows;
-  const uint4* rows_l = lrows;
+  const uint32_t* coef_l = lcoef;
   TileIO io_r, io_o;
   uint64_t off_r = 0, off_o = 0;
   if constexpr (PL) {
     const uint64_t gc = static_cast<uint64_t>(tile) * kXfLanes + lane;
     const bool ok = gc < p.total_columns;
-    const uint64_t blk = ok ? gc / p.chunks_per_shard : 0;
+    const uint64_t blk = ok ? gc / p.chunks_per_shard : sb0;
     const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
     in_mask = ok ? p.pmask[2 * blk] : 0;
     out_mask = ok ? p.pmask[2 * blk + 1] : 0;
-    rows = p.rows + blk * (W * 16);
-    rows_l = lrows + (lane / p.chunks_per_shard) * (W * 4);  // staged: the lane's block in the tile
+    coef_l = lcoef + (blk - sb0) * W;  // the lane's block among the staged ones
     off_r = blk * p.rec_block_stride + col * 64;
     off_o = blk * p.orig_block_stride + col * 64;
   } else {
@@ -770,7 +741,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
       if constexpr (!PL) swap_halves(r[t]);
       dev::planes_from_raw(r[t]);
       if constexpr (PL) {
-        if (staged) mul_rt_lane(r[t], rows_l + 4 * j); else mul_rt_lane(r[t], rows + j * 16);
+        dev::mul_rt_poly(r[t], coef_l[j]);
       } else {
         mul_rt_dx(r[t], rows + j * 16);
       }
@@ -843,7 +814,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
     if ((out_mask >> j) & 1) {
       uint8_t* dst = p.orig + (j - opos) * p.orig_shard_stride;
       if constexpr (PL) {
-        if (staged) mul_rt_lane(r[t], rows_l + 4 * j); else mul_rt_lane(r[t], rows + j * 16);
+        dev::mul_rt_poly(r[t], coef_l[j]);
         dev::store_chunk(dst + off_o, r[t]);
       } else {
         mul_rt_dx(r[t], rows + j * 16);
@@ -857,21 +828,27 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
 // multiply matrix.  loc(x) = sum_{e erased, e != x} log(x ^ e) (mod 65535) -- the crate's
 // eval_poly over the window up to one constant factor, which cancels between the input
 // multiply (present x: exp(loc)) and the output multiply (restored x: exp(-loc)).
+// poly: one word per position instead -- the constant in the polynomial basis (mul_rt_poly).
 __global__ __launch_bounds__(64) void decode_rows_kernel(const uint64_t* __restrict__ emask,
                                                          const uint64_t* __restrict__ pmask, uint32_t W,
                                                          const uint16_t* __restrict__ log_t,
-                                                         const uint16_t* __restrict__ exp_t, uint32_t* rows) {
+                                                         const uint16_t* __restrict__ exp_t, uint32_t* rows,
+                                                         uint32_t poly) {
   const uint64_t pat = blockIdx.x;
   const uint32_t x = threadIdx.x;
   if (x >= W) return;
   const uint64_t e = emask[pat], in = pmask[2 * pat], out = pmask[2 * pat + 1];
   const bool is_in = (in >> x) & 1, is_out = (out >> x) & 1;
-  uint32_t* dst = rows + (pat * W + x) * 16;
   if (!is_in && !is_out) return;
   uint32_t acc = 0;
   for (uint32_t y = 0; y < W; ++y)
     if (((e >> y) & 1) && y != x) acc = dev::add_mod(acc, log_t[x ^ y]);
   const uint16_t lg = is_in ? static_cast<uint16_t>(acc) : static_cast<uint16_t>(65535 - acc);
+  if (poly) {
+    rows[pat * W + x] = dev::to_poly(exp_t[lg]);  // exp[lg] = the constant (lg < 65535)
+    return;
+  }
+  uint32_t* dst = rows + (pat * W + x) * 16;
   uint32_t r[16] = {};
   for (int i = 0; i < 16; ++i) {
     const uint16_t prod = dev::gmul(exp_t, log_t, static_cast<uint16_t>(1u << i), lg);
@@ -1670,9 +1647,10 @@ hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, 
 }
 
 hipError_t launch_decode_rows(const uint64_t* emask, const uint64_t* pmask, uint32_t npat, uint32_t W,
-                              const GfDeviceTables& t, uint32_t* rows, hipStream_t stream) {
+                              const GfDeviceTables& t, uint32_t* rows, bool poly, hipStream_t stream) {
   if (npat == 0) return hipSuccess;
-  hipLaunchKernelGGL(decode_rows_kernel, dim3(npat), dim3(64), 0, stream, emask, pmask, W, t.log, t.exp, rows);
+  hipLaunchKernelGGL(decode_rows_kernel, dim3(npat), dim3(64), 0, stream, emask, pmask, W, t.log, t.exp, rows,
+                     poly ? 1u : 0u);
   return hipGetLastError();
 }
 

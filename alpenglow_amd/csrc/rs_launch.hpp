@@ -139,7 +139,8 @@ struct DecodeXParams {
   uint64_t orig_block_stride;
   uint64_t orig_shard_stride;
   const uint64_t* pmask;      // [pattern][2]: positions present (loaded), positions restored
-  const uint32_t* rows;       // [pattern][W][16] multiply matrices (decode_rows_kernel)
+  const uint32_t* rows;       // [pattern][W][16] multiply matrices (decode_rows_kernel); per_lane:
+                              // [pattern][W] polynomial-basis constants (decode_rows poly)
   const uint32_t* block_ids;  // per_block: blocks processed (null = 0..)
   uint32_t per_block;         // 1: pattern = block, tiles_per_block tiles per block
   uint32_t tiles_per_block;   // chunks_per_shard / 64 (per_block mode)
@@ -153,7 +154,7 @@ struct DecodeXParams {
 hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream);
 // rows for npat patterns: emask[p] = erased positions (locator), pmask as above.
 hipError_t launch_decode_rows(const uint64_t* emask, const uint64_t* pmask, uint32_t npat, uint32_t W,
-                              const GfDeviceTables& t, uint32_t* rows, hipStream_t stream);
+                              const GfDeviceTables& t, uint32_t* rows, bool poly, hipStream_t stream);
 
 // Generic (any geometry) table-driven kernels.  One thread per (block, symbol).
 

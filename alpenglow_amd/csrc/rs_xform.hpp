@@ -153,6 +153,30 @@ __device__ __forceinline__ void lds_get(const uint4* lds, int slot, int lane, ui
 }
 
 // ---- tile I/O -------------------------------------------------------------------
+// Streamed shard pieces: read once, written once.  AG_NT_LOAD / AG_NT_STORE: non-temporal
+// forms (A/B builds).
+#ifndef AG_NT_LOAD
+#define AG_NT_LOAD 0
+#endif
+#ifndef AG_NT_STORE
+#define AG_NT_STORE 0
+#endif
+__device__ __forceinline__ uint4 ld_piece(const uint8_t* p) {
+#if AG_NT_LOAD
+  const dev::u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const dev::u32x4*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+#else
+  return *reinterpret_cast<const uint4*>(p);
+#endif
+}
+__device__ __forceinline__ void st_piece(uint8_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
+#if AG_NT_STORE
+  const dev::u32x4 v = {a, b, c, d};
+  __builtin_nontemporal_store(v, reinterpret_cast<dev::u32x4*>(p));
+#else
+  *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
+#endif
+}
 // A tile is 64 consecutive 64-byte chunks (global chunk index g = 64 * tile + c; chunk g
 // is chunk g % C of block g / C, C = chunks per shard).  Each of a lane's four 16-byte
 // loads per shard is one slice of a lane-linear 1 KiB wave access: instruction q covers
@@ -205,7 +229,7 @@ __device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& 
       const uint8_t* base = p.in + s * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        const uint4 x = ld_piece(base + io.off[q]);
         raw[t][4 * q] = x.x;
         raw[t][4 * q + 1] = x.y;
         raw[t][4 * q + 2] = x.z;
@@ -230,8 +254,7 @@ __device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const Ti
   swap_halves(v);
   static_for<4>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
-    if (qmask & (1u << q))
-      *reinterpret_cast<uint4*>(base + io.off[q]) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    if (qmask & (1u << q)) st_piece(base + io.off[q], v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
   });
 }
 

@@ -152,10 +152,14 @@ def _dry_main(args, world: int, rank: int):
 METRIC = "GiB/s device-resident RS shred encode+reconstruct, batched 1 MiB blocks"
 
 
+def _size(B):
+    return f"{B >> 20} MiB" if B % (1 << 20) == 0 else f"{B / 1024:g} KiB" if B % 1024 == 0 else f"{B} B"
+
+
 def _workload(args, world, n, e=None, lc=0):
     B = args.block_bytes
-    s = (f"{args.stream_blocks} x {B >> 20} MiB block stream over {world} GPU(s)" if args.stream_blocks
-         else f"{n} x {B >> 20} MiB blocks per GPU")
+    s = (f"{args.stream_blocks} x {_size(B)} block stream over {world} GPU(s)" if args.stream_blocks
+         else f"{n} x {_size(B)} blocks per GPU")
     if e is None:
         return s
     return (s + f", {args.k}:{args.m} encode + reconstruct with {e}/{args.k} data shreds erased"

@@ -937,3 +937,51 @@ def test_crate_api_back_to_back_calls_see_fresh_bytes(ctx):
             dec.add_recovery_shard(j, want[j].tobytes())
         res = dec.decode()
         assert all(res[i] == orig[i].tobytes() for i in range(k)), it
+
+
+# ------------------------------------------------ buffers at any alignment, odd strides
+
+@pytest.mark.parametrize("k,m,S,shift,pad", [(32, 32, 1024, 2, 0), (32, 32, 1024, 8, 16), (32, 32, 1000, 0, 0),
+                                             (32, 32, 1000, 6, 2), (16, 4, 1024, 4, 2), (32, 64, 1000, 2, 0),
+                                             (64, 64, 192, 10, 4), (32, 32, 1024, 1, 1), (32, 32, 1022, 3, 0),
+                                             (20, 30, 130, 2, 6)])
+def test_unaligned_codewords(ctx, dev, k, m, S, shift, pad):
+    """Codeword buffers at a byte offset `shift` with block stride (k + m) S + pad: the whole
+    64-byte chunks run in place on the bitsliced kernels (any even alignment), the tail bytes
+    (S mod 64) and byte-odd layouts go through the restride.  Encode against the C oracle;
+    per-block random erasures (both modes), absent shards filled with garbage, against the
+    originals."""
+    n = 9
+    stride = (k + m) * S + pad
+    blocks = np.stack([np.frombuffer(o.block_bytes(7100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    want = ro_c.encode_blocks(blocks, m, threads=8)
+    img = np.full(n * stride + shift + 64, 0xEE, np.uint8)
+    for b in range(n):
+        img[shift + b * stride: shift + b * stride + k * S] = blocks[b].reshape(-1)
+    d = to_dev(img, dev)
+    base = d.data_ptr() + shift
+    rs.encode_batch(ctx, k, m, S, n, base, stride, base + k * S, stride)
+    got = d.cpu().numpy()
+    for b in range(n):
+        cwb = got[shift + b * stride: shift + b * stride + (k + m) * S].reshape(k + m, S)
+        assert np.array_equal(cwb[k:], want[b]), b
+        assert np.array_equal(cwb[:k], blocks[b]), b
+    assert np.all(got[:shift] == 0xEE) and np.all(got[shift + (n - 1) * stride + (k + m) * S:] == 0xEE)
+    rng = random.Random(S * 7 + shift)
+    for mode in (rs.DECODE_ANY_K, rs.DECODE_EXACT):
+        op, rp = [], []
+        img2 = got.copy()
+        for b in range(n):
+            keep = set(rng.sample(range(k + m), k + rng.randint(0, min(2, m))))
+            op += [1 if i in keep else 0 for i in range(k)]
+            rp += [1 if k + j in keep else 0 for j in range(m)]
+            for s in range(k + m):
+                if s not in keep:
+                    o0 = shift + b * stride + s * S
+                    img2[o0:o0 + S] = 0x5A
+        d2 = to_dev(img2, dev)
+        base = d2.data_ptr() + shift
+        rs.decode_batch(ctx, k, m, S, n, base, stride, base + k * S, stride, op, rp, mode=mode)
+        out = d2.cpu().numpy()
+        for b in range(n):
+            assert np.array_equal(out[shift + b * stride: shift + b * stride + k * S].reshape(k, S), blocks[b]), (b, mode)

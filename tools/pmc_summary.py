@@ -10,6 +10,7 @@ import csv
 import glob
 import json
 import os
+import re
 from collections import defaultdict
 
 ap = argparse.ArgumentParser()
@@ -24,7 +25,8 @@ for f in sorted(glob.glob(os.path.join(args.dir, "p*", "pmc_counter_collection.c
         name = r["Kernel_Name"]
         short = "encode" if ("xform8_kernel<32, 0" in name or "xform_kernel<4, 32, 0" in name) else \
                 "reconstruct" if ("xform8_kernel<0, 32" in name or "xform_kernel<4, 0, 32" in name) else \
-                name.split("(")[0].split("::")[-1][:60]
+                (re.search(r"(\w+(<[^()]*>)?)\(", name.replace("(anonymous namespace)", "")) or
+                 re.search(r"(\w+)", name)).group(1)[:60]
         vals[short][r["Counter_Name"]].append(float(r["Counter_Value"]))
 summary = {}
 for k, cs in vals.items():
