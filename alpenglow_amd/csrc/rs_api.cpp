@@ -148,6 +148,8 @@ struct ag_rs_ctx {
   DevBuf scratch;                         // generic-kernel work rows
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
+  DevBuf d_x128, d_rows128;                 // W = 128 two-pass decode: masks, constants
+  uint64_t last_classes[16] = {};           // patterns per decoder class of the last decode
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
   DevBuf d_corr, d_corrk, d_corrblocks;     // correction decoder: patterns, K picks, block ids
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
@@ -241,7 +243,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_x128, &d_rows128, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
                       &one_out, &d_pipe_few, &d_pipe_mask})
       b->release();
     for (DevBuf& b : pipe) b.release();
@@ -766,7 +768,15 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
   const bool corr_geo = mode == AG_RS_DECODE_ANY_K && hr == 1 && m == 32 && k <= 32 && S % 64 == 0 && aligned &&
                         (npat == 1 || cps % 64 == 0) && static_cast<uint64_t>(nblocks) * cps < (uint64_t{1} << 31) &&
                         corr_enabled();
-  bool any_fast = false, any_generic = false, any_x = false, any_syn = false, any_corr = false;
+  // W = 128 windows as two 64-point passes (decode_x16 PASS 1 / 2): the originals in one
+  // window half -- HighRate with next_pow2(m) = 64 (originals at 64..127), LowRate with
+  // next_pow2(k) <= 64 and next_pow2(k) + m in (64, 128] (originals at 0..k-1).  Any k
+  // survivors (exactly k: the codeword is then unique, so the pass split's own erasure set
+  // gives the crate's bytes)
+  const size_t c128 = hr == 1 ? next_pow2(m) : next_pow2(k);
+  const bool x128_geo = S % 64 == 0 && k <= 64 &&
+                        (hr == 1 ? c128 == 64 : (c128 <= 64 && c128 + m > 64 && c128 + m <= 128));
+  bool any_fast = false, any_generic = false, any_x = false, any_syn = false, any_corr = false, any_x128 = false;
   for (size_t p = 0; p < npat; ++p) {
     const size_t no = count_flags(opres + p * k, k), nr = count_flags(rpres + p * m, m);
     if (no + nr < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;  // nothing launched yet
@@ -797,11 +807,16 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
     } else if (x_geo && (hr == 1 || count_flags(opres + p * k, k) + count_flags(rpres + p * m, xm_rec) >= k)) {
       cls[p] = 3;
       any_x = true;
+    } else if (x128_geo && (mode == AG_RS_DECODE_ANY_K || no + nr == k)) {
+      cls[p] = 8;
+      any_x128 = true;
     } else {
       cls[p] = 2;
       any_generic = true;
     }
   }
+  std::fill(std::begin(c->last_classes), std::end(c->last_classes), uint64_t{0});
+  for (size_t p = 0; p < npat; ++p) ++c->last_classes[cls[p]];
   int st;
   if (any_fast) {
     // store mask word per pattern: restore original i iff the pattern is fast and i is absent
@@ -1005,8 +1020,9 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
       xm[npat + 2 * p] = in;
       xm[npat + 2 * p + 1] = out;
     }
-    // per-lane patterns multiply by polynomial-basis constants (one word per position)
-    const bool poly = npat > 1 && x_per_lane;
+    // polynomial-basis constants (one word per position) for decode_x16 (W = 64) and for
+    // per-lane patterns; bitsliced matrices for decode_x<4>'s wave-uniform four-Russians products
+    const bool poly = xw == 64 || (npat > 1 && x_per_lane);
     if (xm != c->xmask_host || xw != c->xmask_w || poly != c->xmask_poly) {
       AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read xmask_host
       if ((st = c->d_xmask.ensure(xm.size() * 8, c->stream))) return st;
@@ -1035,6 +1051,7 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
     p.low_rate = hr == 1 ? 0u : 1u;
     p.chunks_per_shard = static_cast<uint32_t>(cps);
     p.total_columns = static_cast<uint64_t>(nblocks) * cps;
+    p.rows_w = static_cast<uint32_t>(xw);
     uint64_t ntiles;
     if (npat == 1) {
       ntiles = (p.total_columns + 63) / 64;
@@ -1055,7 +1072,120 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
       }
       ntiles = static_cast<uint64_t>(ids.size()) * p.tiles_per_block;
     }
-    if (ag::launch_decode_x(static_cast<unsigned>(xw), p, ntiles, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    if (ag::launch_decode_x(static_cast<unsigned>(xw), 0, p, ntiles, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
+  if (any_x128) {
+    if ((st = c->ensure_tables())) return st;
+    // per pattern: m6 = {erased, present, restored} as (positions 0..63, 64..127) pairs, then
+    // the two passes' (present in the loaded half, restored) pairs
+    const size_t oh = hr == 1 ? 1 : 0;  // the output (originals') window half
+    std::vector<uint64_t> xm(10 * npat, 0);
+    for (size_t p = 0; p < npat; ++p) {
+      if (cls[p] != 8) continue;
+      const uint64_t ob = pack_flags(opres + p * k, k), kmask = k >= 64 ? ~uint64_t{0} : (uint64_t{1} << k) - 1;
+      uint64_t rb[2] = {pack_flags(rpres + p * m, std::min<size_t>(m, 64)), m > 64 ? pack_flags(rpres + p * m + 64, m - 64) : 0};
+      // exactly k survivors: the present originals, then recovery shards in index order
+      size_t budget = k - static_cast<size_t>(__builtin_popcountll(ob));
+      for (int w = 0; w < 2; ++w) {
+        uint64_t keep = 0;
+        for (uint64_t b = rb[w]; b && budget; b &= b - 1, --budget) keep |= b & (~b + 1);
+        rb[w] = keep;
+      }
+      uint64_t in[2], out[2], e[2];
+      if (hr == 1) {  // recovery j at j (j < m <= 64), original i at 64 + i
+        in[0] = rb[0];
+        in[1] = ob;
+        out[0] = 0;
+        out[1] = ~ob & kmask;
+        e[0] = ~rb[0];  // lost / surplus recovery and the virtual points m..63
+        e[1] = out[1];  // positions 64 + k.. are the encoder's zeros, not erasures
+      } else {  // original i at i, zero padding k..c-1, recovery j at c + j, erasures from c + m
+        uint64_t rw[2] = {0, 0}, valid[2] = {0, 0};  // recovery positions in the window
+        for (size_t j = 0; j < m; ++j) {
+          const size_t g = c128 + j;
+          if ((rb[j >> 6] >> (j & 63)) & 1) rw[g >> 6] |= uint64_t{1} << (g & 63);
+          valid[g >> 6] |= uint64_t{1} << (g & 63);
+        }
+        const uint64_t cm = c128 >= 64 ? ~uint64_t{0} : (uint64_t{1} << c128) - 1;  // originals + padding
+        in[0] = ob | rw[0];
+        in[1] = rw[1];
+        out[0] = ~ob & kmask;
+        out[1] = 0;
+        e[0] = out[0] | (~rw[0] & ~cm);  // lost / surplus recovery, positions past c + m
+        e[1] = ~rw[1];
+        (void)valid;
+      }
+      uint64_t* q = &xm[10 * p];
+      q[0] = e[0];
+      q[1] = e[1];
+      q[2] = in[0];
+      q[3] = in[1];
+      q[4] = out[0];
+      q[5] = out[1];
+      q[6] = in[1 - oh];  // pass 1: the other half's inputs
+      q[7] = out[oh];
+      q[8] = in[oh];      // pass 2: the output half's inputs
+      q[9] = out[oh];
+    }
+    // device: m6 [npat][6], pass-1 pairs [npat][2], pass-2 pairs [npat][2]
+    std::vector<uint64_t> dev(10 * npat);
+    for (size_t p = 0; p < npat; ++p) {
+      for (int i = 0; i < 6; ++i) dev[6 * p + i] = xm[10 * p + i];
+      dev[6 * npat + 2 * p] = xm[10 * p + 6];
+      dev[6 * npat + 2 * p + 1] = xm[10 * p + 7];
+      dev[8 * npat + 2 * p] = xm[10 * p + 8];
+      dev[8 * npat + 2 * p + 1] = xm[10 * p + 9];
+    }
+    AG_HIP(hipStreamSynchronize(c->stream));  // a previous upload may still be pending
+    if ((st = c->d_x128.ensure(dev.size() * 8, c->stream)) || (st = c->d_rows128.ensure(npat * 128 * 4, c->stream)))
+      return st;
+    AG_HIP(hipMemcpy(c->d_x128.ptr, dev.data(), dev.size() * 8, hipMemcpyHostToDevice));
+    const uint64_t* d6 = c->d_x128.as<uint64_t>();
+    if (ag::launch_decode_rows128(d6, static_cast<uint32_t>(npat), c->dtables(), c->d_rows128.as<uint32_t>(),
+                                  c->stream) != hipSuccess)
+      return AG_RS_ERR_DEVICE;
+    ag::DecodeXParams p{};
+    p.rec = rec;
+    p.rec_block_stride = rstride;
+    p.rec_shard_stride = sstride;
+    p.orig = orig;
+    p.orig_block_stride = ostride;
+    p.orig_shard_stride = sstride;
+    p.rows = c->d_rows128.as<uint32_t>();
+    p.rows_w = 128;
+    p.k = static_cast<uint32_t>(k);
+    p.m = static_cast<uint32_t>(m);
+    p.chunk = static_cast<uint32_t>(c128);
+    p.low_rate = hr == 1 ? 0u : 1u;
+    p.chunks_per_shard = static_cast<uint32_t>(cps);
+    p.total_columns = static_cast<uint64_t>(nblocks) * cps;
+    uint64_t ntiles;
+    std::vector<uint32_t> ids;
+    if (npat == 1) {
+      ntiles = (p.total_columns + 63) / 64;
+    } else if (x_per_lane) {
+      p.per_lane = 1;  // lanes of blocks outside class 8 find all-zero masks: no loads, no stores
+      ntiles = (p.total_columns + 63) / 64;
+    } else {
+      p.per_block = 1;
+      p.tiles_per_block = static_cast<uint32_t>(cps / 64);
+      for (size_t b = 0; b < nblocks; ++b)
+        if (cls[b] == 8) ids.push_back(static_cast<uint32_t>(b));
+      if (ids.size() != nblocks) {
+        if ((st = c->d_xblocks.ensure(ids.size() * 4, c->stream))) return st;
+        AG_HIP(hipMemcpy(c->d_xblocks.ptr, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+        p.block_ids = c->d_xblocks.as<uint32_t>();
+      }
+      ntiles = static_cast<uint64_t>(ids.size()) * p.tiles_per_block;
+    }
+    // recovery shards beyond the window half the kernel loads are addressed from p.rec with
+    // the window position; launch_decode_x checks the geometry
+    p.m = static_cast<uint32_t>(std::min<size_t>(m, p.chunk));
+    for (int pass = 1; pass <= 2; ++pass) {
+      p.pmask = d6 + (pass == 1 ? 6 : 8) * npat;
+      if (ag::launch_decode_x(128, pass, p, ntiles, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    }
+    AG_HIP(hipStreamSynchronize(c->stream));  // host vectors above are read by the copies
   }
   if (!any_generic) return AG_RS_OK;
 
@@ -1223,6 +1353,16 @@ int ag_rs_ctx_synchronize(ag_rs_ctx* c) {
 int ag_rs_use_high_rate(size_t k, size_t m) {
   const int hr = ag::use_high_rate(k, m);
   return hr < 0 ? -AG_RS_ERR_UNSUPPORTED_SHARD_COUNT : hr;
+}
+
+// Test aid (not in the public header's contract): patterns per decoder class in the last
+// decode on this context -- 0 nothing to restore, 1 full-recovery transform, 2 table-driven
+// generic, 3 W <= 64 window (decode_x / decode_x16), 4 syndrome, 5 LowRate chunk transform,
+// 6 correction (decode_c), 8 W = 128 two-pass window.
+int ag_rs_internal_last_decode_classes(ag_rs_ctx* c, uint64_t* out16) {
+  if (!c || !out16) return AG_RS_ERR_INVALID_ARGUMENT;
+  std::memcpy(out16, c->last_classes, sizeof c->last_classes);
+  return AG_RS_OK;
 }
 
 int ag_rs_has_fast_path(size_t k, size_t m, size_t S) {
@@ -2488,7 +2628,8 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   p.chunks_per_shard = static_cast<uint32_t>(cps);
   p.total_columns = static_cast<uint64_t>(n) * cps;
   p.per_lane = 1;
-  if (ag::launch_decode_x(static_cast<unsigned>(W), p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
+  p.rows_w = static_cast<uint32_t>(W);
+  if (ag::launch_decode_x(static_cast<unsigned>(W), 0, p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   int64_t* strip = c->d_strip.as<int64_t>();
   if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(k * S), n, strip, c->stream) != hipSuccess ||

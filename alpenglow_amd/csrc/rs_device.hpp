@@ -221,8 +221,9 @@ __device__ __forceinline__ void planes_from_raw(uint32_t* v) {
 }
 using u32x4 = uint32_t __attribute__((ext_vector_type(4)));
 
-// NT: non-temporal stores (streamed once; keeps L2 for the loads).
-template <bool NT = false>
+// NT: non-temporal stores (streamed once; keeps L2 for the loads).  ACC: XOR into the bytes
+// already at dst (a partial result stored by an earlier pass).
+template <bool NT = false, bool ACC = false>
 __device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, const uint32_t* planes) {
   uint32_t v[16];
   static_for<16>([&](auto P) {
@@ -234,7 +235,8 @@ __device__ __forceinline__ void store_chunk(uint8_t* __restrict__ dst, const uin
   u32x4* d = reinterpret_cast<u32x4*>(dst);
   static_for<4>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
-    const u32x4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+    u32x4 x = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+    if constexpr (ACC) x ^= d[q];
     if constexpr (NT) {
       __builtin_nontemporal_store(x, d + q);
     } else {

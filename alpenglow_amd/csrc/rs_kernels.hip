@@ -96,6 +96,9 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
   __shared__ X8Flags flags;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+#if AG_X8_PRIO  // A/B: static priority for the second-dispatched half (MI355X_MICROARCH.md)
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
 #if AG_X8_PAIRSYNC
   if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
@@ -642,9 +645,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
 }
 
 // =====================================================================================
-// decode_x16<PL>: the W = 64 window decoder (decode_x's algorithm) on xform16's layout:
-// 16 waves x 4 slots, one 1024-thread workgroup per CU at 4 waves/SIMD (decode_x<8> keeps 8
-// slots per lane at 216 VGPRs: 2 waves/SIMD and one 8-wave workgroup per CU, latency-bound).
+// decode_x16<PL, PASS, DIN, DOUT>: the window decoder (decode_x's algorithm) on xform16's
+// layout: 16 waves x 4 slots, one 1024-thread workgroup per CU at 4 waves/SIMD (decode_x<8>
+// keeps 8 slots per lane at 216 VGPRs: 2 waves/SIMD, latency-bound).
 // Positions by layout (X8Lay: slot bits | wave bits):
 //   G0 slots p0 p1 | waves p2 p3 p4 p5   loads + locator multiplies, IFFT b0 b1; FFT b0, stores
 //   G1 slots p2 p1 | waves p0 p3 p4 p5   IFFT b2 / FFT b1
@@ -654,37 +657,53 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
 // The derivative w'[j] = w[j] ^ XOR_{b : bit b of j clear} w[j | 2^b] (pre-derivative terms)
 // in G4: slot bits in-lane, wave bits from the partner waves' pre-derivative copies in LDS,
 // two slots per round (2 x 128 KiB would not fit).
+//
+// PASS 0: the W <= 64 window (DIN = DOUT = 0).
+// PASS 1 / 2: the W = 128 window as two 64-point passes.  With u_h = IFFT_64 of window half h
+// (skew delta 64 h) and P = the derivative without its self term (D = I + P), the crate's
+// IFFT_128 -> derivative -> FFT_128 gives output half o as FFT_64,64o(P u_o ^ u_{1-o}): the
+// size-128 layer's skew factor (index 63) is zero, so the halves meet only there
+// (tests/test_oracle.py pins the identity against the oracle's 128-point decoder).  Pass 1
+// (DIN = the other half, DOUT = the output half): IFFT, no derivative, FFT, output multiply,
+// the partial stored.  Pass 2 (DIN = DOUT = the output half): IFFT, P, FFT, output multiply,
+// XOR-ed into the stored partial (the multiply is linear).  Loads, masks and staged constants
+// are the pass's loaded half (window positions DIN + j); outputs are window positions DOUT + j.
+// Multiplies by the per-position constants are Horner products in the polynomial basis
+// (mul_rt_poly); PL: per-lane constants staged in LDS, else one wave-uniform word.
 // =====================================================================================
-template <bool PL>
+template <bool PL, int PASS, int DIN, int DOUT>
 __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams p) {
   using G0 = X8Lay<0, 1, 2, 3, 4, 5>;
   using G1 = X8Lay<2, 1, 0, 3, 4, 5>;
   using G2 = X8Lay<2, 3, 0, 1, 4, 5>;
   using G3 = X8Lay<4, 3, 0, 1, 2, 5>;
   using G4 = X8Lay<4, 5, 0, 1, 2, 3>;
-  constexpr int W = 64;
+  static_assert(PASS != 0 || (DIN == 0 && DOUT == 0), "the one-pass window starts at 0");
+  static_assert(PASS != 2 || DIN == DOUT, "pass 2 loads its output half");
+  constexpr int W = 64;  // positions per pass
   __shared__ uint4 lds[32 * 4 * kXfLanes];  // 16 waves x 2 slots x 4 KiB
   __shared__ XFlags<16> flags;
-  // PL: the polynomial-basis constants (one word per position) of the <= 64 blocks the
+  // PL: the polynomial-basis constants of the pass's 64 positions for the <= 64 blocks the
   // tile's columns belong to, staged once by the workgroup instead of a dependent global
   // load per product
-  __shared__ uint32_t lcoef[kXfLanes * W];
+  __shared__ uint32_t lcoef[PL ? kXfLanes * W : 1];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
+  const uint32_t rw = p.rows_w;  // constants per pattern (64 or 128)
   uint64_t sb0 = 0;  // PL: first block of the tile
   if constexpr (PL) {
     const uint64_t c0 = static_cast<uint64_t>(tile) * kXfLanes;
     const uint64_t c1 = c0 + kXfLanes - 1 < p.total_columns ? c0 + kXfLanes - 1 : p.total_columns - 1;
     sb0 = c0 / p.chunks_per_shard;
     const uint32_t nbt = static_cast<uint32_t>(c1 / p.chunks_per_shard - sb0 + 1);  // <= 64
-    for (uint32_t i = threadIdx.x; i < nbt * W; i += blockDim.x) lcoef[i] = p.rows[(sb0 + i / W) * W + i % W];
+    for (uint32_t i = threadIdx.x; i < nbt * W; i += blockDim.x) lcoef[i] = p.rows[(sb0 + i / W) * rw + DIN + i % W];
   }
   if (threadIdx.x < 32) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
   uint64_t in_mask, out_mask;
-  const uint32_t* rows;
-  const uint32_t* coef_l = lcoef;
+  const uint32_t* coef = lcoef;  // PL: the lane's staged constants; else the pattern's (global)
+  const uint32_t* coef_out;      // the output half's constants (PASS 1: global, not staged)
   TileIO io_r, io_o;
   uint64_t off_r = 0, off_o = 0;
   if constexpr (PL) {
@@ -694,7 +713,8 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
     const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
     in_mask = ok ? p.pmask[2 * blk] : 0;
     out_mask = ok ? p.pmask[2 * blk + 1] : 0;
-    coef_l = lcoef + (blk - sb0) * W;  // the lane's block among the staged ones
+    coef = lcoef + (blk - sb0) * W;  // the lane's block among the staged ones
+    coef_out = PASS == 1 ? p.rows + blk * rw + DOUT : coef;
     off_r = blk * p.rec_block_stride + col * 64;
     off_o = blk * p.orig_block_stride + col * 64;
   } else {
@@ -707,18 +727,24 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
     }
     in_mask = p.pmask[2 * pat];
     out_mask = p.pmask[2 * pat + 1];
-    rows = p.rows + pat * (W * 16);
+    coef = p.rows + pat * rw + DIN;
+    coef_out = p.rows + pat * rw + DOUT;
     io_r = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.rec_block_stride);
     io_o = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.orig_block_stride);
   }
   const uint32_t opos = p.low_rate ? 0 : p.chunk, rpos = p.low_rate ? p.chunk : 0;
+  // shard base of window position g (recovery shards below the originals in HighRate)
+  auto shard_src = [&](uint32_t g, bool& is_rec) -> const uint8_t* {
+    is_rec = p.low_rate ? g >= p.chunk : g < p.chunk;
+    return is_rec ? p.rec + (g - rpos) * p.rec_shard_stride : p.orig + (g - opos) * p.orig_shard_stride;
+  };
   Regs4 r;
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
-    const uint32_t j = 4 * wave + t;  // G0 position (wave-uniform)
+    const uint32_t j = 4 * wave + t;  // G0 position in the pass (wave-uniform)
     if ((in_mask >> j) & 1) {          // PL: per lane
-      const bool is_rec = p.low_rate ? j >= p.chunk : j < p.chunk;
-      const uint8_t* base = is_rec ? p.rec + (j - rpos) * p.rec_shard_stride : p.orig + (j - opos) * p.orig_shard_stride;
+      bool is_rec;
+      const uint8_t* base = shard_src(DIN + j, is_rec);
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
         const uint8_t* src;
@@ -740,66 +766,66 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
     if ((in_mask >> j) & 1) {
       if constexpr (!PL) swap_halves(r[t]);
       dev::planes_from_raw(r[t]);
-      if constexpr (PL) {
-        dev::mul_rt_poly(r[t], coef_l[j]);
-      } else {
-        mul_rt_dx(r[t], rows + j * 16);
-      }
+      dev::mul_rt_poly(r[t], coef[j]);
     }
   });
-  // IFFT_64 (skew delta 0)
-  x8_layer_t<G0, 0, true, 0>(wave, r);
-  x8_layer_t<G0, 1, true, 0>(wave, r);
+  // IFFT_64 (skew delta DIN)
+  x8_layer_t<G0, 0, true, DIN>(wave, r);
+  x8_layer_t<G0, 1, true, DIN>(wave, r);
   x8_swap<0, 0, 1>(wave, lane, lds, &flags, r);
-  x8_layer_t<G1, 2, true, 0>(wave, r);
+  x8_layer_t<G1, 2, true, DIN>(wave, r);
   x8_swap<1, 1, 2>(wave, lane, lds, &flags, r);
-  x8_layer_t<G2, 3, true, 0>(wave, r);
+  x8_layer_t<G2, 3, true, DIN>(wave, r);
   x8_swap<0, 2, 3>(wave, lane, lds, &flags, r);
-  x8_layer_t<G3, 4, true, 0>(wave, r);
+  x8_layer_t<G3, 4, true, DIN>(wave, r);
   x8_swap<1, 3, 4>(wave, lane, lds, &flags, r);
-  x8_layer_t<G4, 5, true, 0>(wave, r);
-  // formal derivative in G4 (slot t: position bits p4 = t & 1, p5 = t >> 1; wave bits p0..p3)
-  __syncthreads();  // every wave's swap reads are done: the exchange buffer is free
-  static_for<2>([&](auto Rho) {
-    constexpr int rho = decltype(Rho)::value;
-    // slot = 2 * wave + u holds this wave's pre-derivative slot 2 rho + u
-    static_for<2>([&](auto U) { lds_put(lds, 2 * wave + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
-    // slot-bit terms of slots 2 rho, 2 rho + 1 from pre-derivative partners (ascending t: a
-    // partner t | 2^i > t is unmodified; slots 2, 3 are untouched until round 1)
-    static_for<2>([&](auto U) {
-      constexpr int t = 2 * rho + decltype(U)::value;
-      if constexpr (!(t & 1)) dev::xor_planes(r[t], r[t | 1]);
-      if constexpr (!(t & 2)) dev::xor_planes(r[t], r[t | 2]);
-    });
-    __syncthreads();
-    static_for<4>([&](auto B) {
-      constexpr int b = decltype(B)::value;
-      if (!((wave >> b) & 1)) {
-        const int pw = wave | (1 << b);
-        static_for<2>([&](auto U) {
-          constexpr int u = decltype(U)::value;
-          static_for<4>([&](auto Q) {
-            constexpr int q = decltype(Q)::value;
-            const uint4 x = lds[((2 * pw + u) * 4 + q) * kXfLanes + lane];
-            r[2 * rho + u][4 * q] ^= x.x;
-            r[2 * rho + u][4 * q + 1] ^= x.y;
-            r[2 * rho + u][4 * q + 2] ^= x.z;
-            r[2 * rho + u][4 * q + 3] ^= x.w;
+  x8_layer_t<G4, 5, true, DIN>(wave, r);
+  if constexpr (PASS != 1) {
+    // formal derivative in G4 (slot t: position bits p4 = t & 1, p5 = t >> 1; wave bits p0..p3)
+    __syncthreads();  // every wave's swap reads are done: the exchange buffer is free
+    static_for<2>([&](auto Rho) {
+      constexpr int rho = decltype(Rho)::value;
+      // slot = 2 * wave + u holds this wave's pre-derivative slot 2 rho + u
+      static_for<2>([&](auto U) { lds_put(lds, 2 * wave + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+      // slot-bit terms of slots 2 rho, 2 rho + 1 from pre-derivative partners (ascending t: a
+      // partner t | 2^i > t is unmodified; slots 2, 3 are untouched until round 1)
+      static_for<2>([&](auto U) {
+        constexpr int t = 2 * rho + decltype(U)::value;
+        if constexpr (PASS == 2) {
+          // P = D ^ I: the partner terms only (the slot's own value stays in LDS for the
+          // partner waves; lower slots never need a higher slot's register after this)
+          static_for<16>([&](auto P) {
+            constexpr int q = decltype(P)::value;
+            if constexpr (!(t & 1) && !(t & 2)) r[t][q] = r[t | 1][q] ^ r[t | 2][q];
+            else if constexpr (!(t & 1)) r[t][q] = r[t | 1][q];
+            else if constexpr (!(t & 2)) r[t][q] = r[t | 2][q];
+            else r[t][q] = 0;
           });
-        });
-      }
+        } else {
+          if constexpr (!(t & 1)) dev::xor_planes(r[t], r[t | 1]);
+          if constexpr (!(t & 2)) dev::xor_planes(r[t], r[t | 2]);
+        }
+      });
+      __syncthreads();
+      static_for<4>([&](auto B) {
+        constexpr int b = decltype(B)::value;
+        if (!((wave >> b) & 1)) {
+          const int pw = wave | (1 << b);
+          static_for<2>([&](auto U) { lds_get_xor(lds, 2 * pw + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+        }
+      });
+      __syncthreads();
     });
-    __syncthreads();
-  });
-  // FFT_64 (skew delta 0), ending in G0
-  x8_layer_t<G4, 5, false, 0>(wave, r);
-  x8_layer_t<G4, 4, false, 0>(wave, r);
+  }
+  // FFT_64 (skew delta DOUT), ending in G0
+  x8_layer_t<G4, 5, false, DOUT>(wave, r);
+  x8_layer_t<G4, 4, false, DOUT>(wave, r);
   x8_swap<1, 3, 5>(wave, lane, lds, &flags, r);
-  x8_layer_t<G3, 3, false, 0>(wave, r);
+  x8_layer_t<G3, 3, false, DOUT>(wave, r);
   x8_swap<0, 2, 6>(wave, lane, lds, &flags, r);
-  x8_layer_t<G2, 2, false, 0>(wave, r);
+  x8_layer_t<G2, 2, false, DOUT>(wave, r);
   x8_swap<1, 1, 7>(wave, lane, lds, &flags, r);
-  x8_layer_t<G1, 1, false, 0>(wave, r);
+  x8_layer_t<G1, 1, false, DOUT>(wave, r);
   x8_swap<0, 0, 8>(wave, lane, lds, &flags, r);
   const uint32_t mine = static_cast<uint32_t>(out_mask >> (4 * wave)) & 0xF;
   if constexpr (PL) {
@@ -807,19 +833,17 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
   } else {
     if (mine == 0) return;
   }
-  x8_layer_t<G0, 0, false, 0>(wave, r);
+  x8_layer_t<G0, 0, false, DOUT>(wave, r);
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = 4 * wave + t;
     if ((out_mask >> j) & 1) {
-      uint8_t* dst = p.orig + (j - opos) * p.orig_shard_stride;
-      if constexpr (PL) {
-        dev::mul_rt_poly(r[t], coef_l[j]);
-        dev::store_chunk(dst + off_o, r[t]);
-      } else {
-        mul_rt_dx(r[t], rows + j * 16);
-        store_shard(dst, io_o, io_o.valid, r[t]);
-      }
+      uint8_t* dst = p.orig + (DOUT + j - opos) * p.orig_shard_stride;
+      // the output multiply is linear: pass 1 stores its multiplied partial, pass 2 adds its
+      // own to the stored bytes (no extra planes live across the multiply)
+      dev::mul_rt_poly(r[t], coef_out[j]);
+      if constexpr (PL) dev::store_chunk<false, PASS == 2>(dst + off_o, r[t]);
+      else store_shard<PASS == 2>(dst, io_o, io_o.valid, r[t]);
     }
   });
 }
@@ -1619,30 +1643,61 @@ hipError_t launch_xform_lowrate_decode(unsigned j, const XformParams& p, hipStre
   return hipGetLastError();
 }
 
-hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
+hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
   if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
   if (p.k + p.chunk > W || p.m > p.chunk || (p.low_rate && (p.k > p.chunk || p.m + p.chunk > W)))
     return hipErrorInvalidValue;
   const dim3 grid(static_cast<unsigned>(ntiles));
   const bool pl = p.per_lane != 0;
-  switch (W) {
-    case 32:
-      if (pl) hipLaunchKernelGGL((decode_x_kernel<4, true>), grid, dim3(256), 0, stream, p);
-      else hipLaunchKernelGGL((decode_x_kernel<4>), grid, dim3(256), 0, stream, p);
-      break;
-    case 64:
-      // the 16-wave layout (decode_x16); A/B variant 15 = decode_x<8>
-      if (xform_variant() == 15) {
-        if (pl) hipLaunchKernelGGL((decode_x_kernel<8, true>), grid, dim3(512), 0, stream, p);
-        else hipLaunchKernelGGL((decode_x_kernel<8>), grid, dim3(512), 0, stream, p);
-      } else {
-        if (pl) hipLaunchKernelGGL((decode_x16_kernel<true>), grid, dim3(1024), 0, stream, p);
-        else hipLaunchKernelGGL((decode_x16_kernel<false>), grid, dim3(1024), 0, stream, p);
-      }
-      break;
-    default: return hipErrorInvalidValue;
+  if (W == 32 && pass == 0) {
+    if (pl) hipLaunchKernelGGL((decode_x_kernel<4, true>), grid, dim3(256), 0, stream, p);
+    else hipLaunchKernelGGL((decode_x_kernel<4>), grid, dim3(256), 0, stream, p);
+  } else if (W == 64 && pass == 0) {
+    if (p.rows_w != 64) return hipErrorInvalidValue;
+    if (pl) hipLaunchKernelGGL((decode_x16_kernel<true, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
+    else hipLaunchKernelGGL((decode_x16_kernel<false, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
+  } else if (W == 128 && (pass == 1 || pass == 2)) {
+    // the originals must lie in one window half: LowRate k <= 64 (half 0); HighRate chunk 64
+    // (half 1)
+    if (p.rows_w != 128 || (p.low_rate ? p.k > 64 : p.chunk != 64)) return hipErrorInvalidValue;
+#define AG_DX128(PLV, PS, DI, DO) hipLaunchKernelGGL((decode_x16_kernel<PLV, PS, DI, DO>), grid, dim3(1024), 0, stream, p)
+    if (p.low_rate) {  // outputs in half 0
+      if (pass == 1) { if (pl) AG_DX128(true, 1, 64, 0); else AG_DX128(false, 1, 64, 0); }
+      else { if (pl) AG_DX128(true, 2, 0, 0); else AG_DX128(false, 2, 0, 0); }
+    } else {           // outputs in half 1
+      if (pass == 1) { if (pl) AG_DX128(true, 1, 0, 64); else AG_DX128(false, 1, 0, 64); }
+      else { if (pl) AG_DX128(true, 2, 64, 64); else AG_DX128(false, 2, 64, 64); }
+    }
+#undef AG_DX128
+  } else {
+    return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// W = 128 windows: m6[pat] = {erased lo, hi, present lo, hi, restored lo, hi} (position bits
+// 0..63, 64..127); rows [pat][128] polynomial-basis constants (decode_rows poly form).
+__global__ __launch_bounds__(128) void decode_rows128_kernel(const uint64_t* __restrict__ m6,
+                                                            const uint16_t* __restrict__ log_t,
+                                                            const uint16_t* __restrict__ exp_t, uint32_t* rows) {
+  const uint64_t pat = blockIdx.x;
+  const uint32_t x = threadIdx.x;
+  const uint64_t* m = m6 + 6 * pat;
+  const uint32_t h = x >> 6, xl = x & 63;
+  const bool is_in = (m[2 + h] >> xl) & 1, is_out = (m[4 + h] >> xl) & 1;
+  if (!is_in && !is_out) return;
+  uint32_t acc = 0;
+  for (uint32_t y = 0; y < 128; ++y)
+    if (((m[y >> 6] >> (y & 63)) & 1) && y != x) acc = dev::add_mod(acc, log_t[x ^ y]);
+  const uint16_t lg = is_in ? static_cast<uint16_t>(acc) : static_cast<uint16_t>(65535 - acc);
+  rows[pat * 128 + x] = dev::to_poly(exp_t[lg]);
+}
+
+hipError_t launch_decode_rows128(const uint64_t* m6, uint32_t npat, const GfDeviceTables& t, uint32_t* rows,
+                                 hipStream_t stream) {
+  if (npat == 0) return hipSuccess;
+  hipLaunchKernelGGL(decode_rows128_kernel, dim3(npat), dim3(128), 0, stream, m6, t.log, t.exp, rows);
   return hipGetLastError();
 }
 

@@ -150,8 +150,13 @@ struct DecodeXParams {
                               // 1: original i at i, recovery j at chunk + j (LowRate sub-window)
   uint32_t chunks_per_shard;
   uint64_t total_columns;  // batch blocks * chunks_per_shard
+  uint32_t rows_w;         // constants per pattern in rows (W = 64: 64; W = 128: 128)
 };
-hipError_t launch_decode_x(unsigned W, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream);
+// W = 32 / 64: pass 0.  W = 128: pass 1 (the other half's inputs, raw partial outputs), then
+// pass 2 (the output half's inputs, the partial added, output multiply); masks per pass.
+hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream);
+hipError_t launch_decode_rows128(const uint64_t* m6, uint32_t npat, const GfDeviceTables& t, uint32_t* rows,
+                                 hipStream_t stream);
 // rows for npat patterns: emask[p] = erased positions (locator), pmask as above.
 hipError_t launch_decode_rows(const uint64_t* emask, const uint64_t* pmask, uint32_t npat, uint32_t W,
                               const GfDeviceTables& t, uint32_t* rows, bool poly, hipStream_t stream);

@@ -153,13 +153,16 @@ __device__ __forceinline__ void lds_get(const uint4* lds, int slot, int lane, ui
 }
 
 // ---- tile I/O -------------------------------------------------------------------
-// Streamed shard pieces: read once, written once.  AG_NT_LOAD / AG_NT_STORE: non-temporal
-// forms (A/B builds).
+// Streamed shard pieces: read once, written once, so the transform kernels load and store
+// them non-temporally (nt).  Measured on the headline (profiles/r03_nt_ab.txt, two
+// interleaved rounds): encode 5.67 -> 5.81-5.85 TB/s, reconstruct 5.44-5.47 -> 5.89-5.93 TB/s
+// with both; loads alone +1-2 %, stores alone +2-5 %.  AG_NT_LOAD / AG_NT_STORE = 0: the
+// default-policy forms (A/B builds).
 #ifndef AG_NT_LOAD
-#define AG_NT_LOAD 0
+#define AG_NT_LOAD 1
 #endif
 #ifndef AG_NT_STORE
-#define AG_NT_STORE 0
+#define AG_NT_STORE 1
 #endif
 __device__ __forceinline__ uint4 ld_piece(const uint8_t* p) {
 #if AG_NT_LOAD
@@ -241,7 +244,9 @@ __device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& 
   });
 }
 
-// Planes -> bytes -> lane-linear pieces, stored where the input pieces were read.
+// Planes -> bytes -> lane-linear pieces, stored where the input pieces were read.  ACC: XOR
+// into the bytes already there (a partial result stored by an earlier pass).
+template <bool ACC = false>
 __device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const TileIO& io, uint32_t qmask,
                                             const uint32_t* planes) {
   uint32_t v[16];
@@ -254,7 +259,14 @@ __device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const Ti
   swap_halves(v);
   static_for<4>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
-    if (qmask & (1u << q)) st_piece(base + io.off[q], v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    if (qmask & (1u << q)) {
+      if constexpr (ACC) {
+        const uint4 o = ld_piece(base + io.off[q]);
+        st_piece(base + io.off[q], v[4 * q] ^ o.x, v[4 * q + 1] ^ o.y, v[4 * q + 2] ^ o.z, v[4 * q + 3] ^ o.w);
+      } else {
+        st_piece(base + io.off[q], v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      }
+    }
   });
 }
 
@@ -542,6 +554,9 @@ __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, Flags* f
 #endif
 }
 
+#ifndef AG_X8_PRIO
+#define AG_X8_PRIO 0
+#endif
 #ifndef AG_X8_WAVES_PER_EU
 #define AG_X8_WAVES_PER_EU 4
 #endif

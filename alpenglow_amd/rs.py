@@ -167,6 +167,7 @@ def load():
         "ag_shredder_shred_batch": ([p, sz, sz, p, p, p, sz, p, p, p, p, p, p, p, p, p, p, sz, p], i),
         "ag_shredder_deshred_batch": ([p, sz, sz, p, sz, p, p, p, p, p, p, p, p, p, p, p], i),
     }
+    sigs["ag_rs_internal_last_decode_classes"] = ([p, p], i)  # test aid, not in the header
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
             continue              # check the shipped library exports everything
@@ -324,6 +325,19 @@ def coder_deshred_batch(ctx: Context, num_coding: int, nslices: int, shred_bytes
     if as_array:
         return out
     return [int(v) if v >= 0 else STATUS_KIND.get(int(-v), f"Status{int(-v)}") for v in out]
+
+
+DECODE_CLASSES = {0: "none", 1: "transform", 2: "generic", 3: "window64", 4: "syndrome", 5: "lowrate_chunk",
+                  6: "correction", 8: "window128"}
+
+
+def last_decode_classes(ctx: Context) -> dict:
+    """Patterns per decoder class of the last decode on ``ctx`` (test aid): name -> count."""
+    import numpy as np
+
+    out = np.zeros(16, np.uint64)
+    _check(load().ag_rs_internal_last_decode_classes(ctx.handle, out.ctypes.data), "last_decode_classes")
+    return {DECODE_CLASSES.get(i, str(i)): int(v) for i, v in enumerate(out) if v}
 
 
 def fill_splitmix(ctx: Context, device_dst, nblocks: int, block_bytes: int, dst_block_stride: int,

@@ -59,14 +59,16 @@ def main():
     if args.coding_only:  # output shreds are the 64 coding shreds; the first 32 are dropped
         cpres = np.tile(np.array([0] * 32 + [1] * 32, np.uint8), n)
     if args.random_patterns:
-        if args.coding_only:
-            raise SystemExit("--random-patterns is for the RegularShredder shape")
         rng = np.random.default_rng(0xA221)
         arrived = np.argsort(rng.random((n, 64)), axis=1)[:, :32]  # first 32 arrivals per slice
         present = np.zeros((n, 64), np.uint8)
         np.put_along_axis(present, arrived, 1, axis=1)
-        dpres = np.ascontiguousarray(present[:, :32]).reshape(-1)
-        cpres = np.ascontiguousarray(present[:, 32:]).reshape(-1)
+        if args.coding_only:  # the 64 output shreds are the coding shreds (shredder.rs:362-395)
+            dpres = np.zeros(32 * n, np.uint8)
+            cpres = np.ascontiguousarray(present).reshape(-1)
+        else:
+            dpres = np.ascontiguousarray(present[:, :32]).reshape(-1)
+            cpres = np.ascontiguousarray(present[:, 32:]).reshape(-1)
     mode = rs.DECODE_EXACT if args.exact else rs.DECODE_ANY_K
 
     def shred():
@@ -112,7 +114,7 @@ def main():
         spot &= host[i, :32 * S].tobytes() == b"".join(raw.data)
         spot &= host[i, 32 * S:].tobytes() == b"".join(raw.coding)
     line = {
-        "metric": ("slices/s ReedSolomonCoder shred + deshred (random 32 of 64 shreds per slice), max slices"
+        "metric": ("slices/s ReedSolomonCoder shred + deshred (random 32 of 64 output shreds per slice), max slices"
                    if args.random_patterns else
                    "slices/s ReedSolomonCoder shred + deshred (first 32 output shreds lost), max slices"),
         "value": n * args.steps / wall,
@@ -127,7 +129,9 @@ def main():
         "dtype": "u8 (GF(2^16) symbols)",
         "data": "synthetic (splitmix64 payloads, device-generated)",
         "config": {"workload": f"{n} slices x {L} B payload, 32:{m} shreds of {S} B, deshred from "
-                               + ("coding shreds 32..63 (CodingOnlyShredder)" if args.coding_only else
+                               + ("a random 32 of the 64 coding shreds per slice (CodingOnlyShredder)"
+                      if args.coding_only and args.random_patterns else
+                      "coding shreds 32..63 (CodingOnlyShredder)" if args.coding_only else
                                   "a random 32 of the 64 shreds per slice (RegularShredder)" if args.random_patterns
                                   else "the 32 coding shreds (RegularShredder)"),
                    "mode": "EXACT" if args.exact else "ANY_K"},

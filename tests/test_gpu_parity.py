@@ -985,3 +985,62 @@ def test_unaligned_codewords(ctx, dev, k, m, S, shift, pad):
         out = d2.cpu().numpy()
         for b in range(n):
             assert np.array_equal(out[shift + b * stride: shift + b * stride + k * S].reshape(k, S), blocks[b]), (b, mode)
+
+
+# ------------------------------------------------ W = 128 windows (two 64-point passes)
+
+def _w128_case(k, m, S, n, per_block, rng, lose_originals=None, lose_coding=None):
+    blocks = np.stack([np.frombuffer(o.block_bytes(11000 + 97 * k + m + b, k * S), np.uint8).reshape(k, S)
+                       for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    op, rp = [], []
+    d_o, d_r = blocks.copy(), rec.copy()
+    for b in range(n if per_block else 1):
+        lo = lose_originals if lose_originals is not None else rng.randint(1, k)
+        lc = lose_coding if lose_coding is not None else m - (k - (k - lo)) - rng.randint(0, 2)
+        lc = max(0, min(lc, m - lo))
+        lost_o = set(rng.sample(range(k), lo))
+        lost_r = set(rng.sample(range(m), lc))
+        op += [0 if i in lost_o else 1 for i in range(k)]
+        rp += [0 if j in lost_r else 1 for j in range(m)]
+    for b in range(n):
+        pb = b if per_block else 0
+        for i in range(k):
+            if not op[pb * k + i]:
+                d_o[b, i] = 0x6B
+        for j in range(m):
+            if not rp[pb * m + j]:
+                d_r[b, j] = 0xB6
+    return blocks, d_o, d_r, op, rp
+
+
+@pytest.mark.parametrize("k,m,S,n,per_block,lo,lc", [
+    (32, 64, 1024, 96, True, 32, None),    # CodingOnly: every data shred lost, random 32 of 64 coding
+    (32, 64, 1024, 48, True, None, None),  # CodingOnly mixed losses across both recovery chunks
+    (64, 64, 4096, 6, True, 16, 8),        # 64:64, 8 lost coding shreds, per-block patterns
+    (64, 64, 4096, 6, False, 16, 16),      # 64:64, 16 lost coding shreds, one pattern
+    (64, 64, 1024, 40, True, 32, 12),      # 64:64 on 1 KiB shards: per-lane patterns
+    (40, 64, 2048, 10, True, 20, 10),      # HighRate, originals at 64..103
+    (20, 80, 2048, 10, True, 20, None),    # LowRate chunk 32, recovery up to position 111
+])
+def test_window128_decode(ctx, dev, k, m, S, n, per_block, lo, lc):
+    """W = 128 windows (CodingOnly 32:64 arrival across both recovery chunks, 64:64 with lost
+    coding shreds, LowRate past 64 positions) on the bitsliced two-pass decoder, ANY_K (and
+    EXACT with exactly k survivors), absent shards filled with garbage, against the originals;
+    the decode-class record shows the two-pass window served every pattern."""
+    rng = random.Random(k * 1000 + m * 10 + S)
+    blocks, d_o, d_r, op, rp = _w128_case(k, m, S, n, per_block, rng, lo, lc)
+    got = gpu_decode(ctx, dev, d_o, d_r, op, rp, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
+    classes = rs.last_decode_classes(ctx)
+    assert set(classes) <= {"window128", "none", "correction", "window64"} and classes.get("window128", 0) > 0, classes
+    # EXACT with exactly k survivors per pattern: the same kernels, the crate's bytes
+    op2, rp2 = list(op), list(rp)
+    for b in range(len(op) // k):
+        surplus = sum(op2[b * k:(b + 1) * k]) + sum(rp2[b * m:(b + 1) * m]) - k
+        for j in reversed(range(m)):
+            if surplus and rp2[b * m + j]:
+                rp2[b * m + j] = 0
+                surplus -= 1
+    got = gpu_decode(ctx, dev, d_o, d_r, op2, rp2, rs.DECODE_EXACT)
+    assert np.array_equal(got, blocks)

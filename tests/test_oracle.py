@@ -343,3 +343,33 @@ def test_avx2_engine_matches_scalar_oracle(k, m, S):
         damaged[:, :k][:, op == 0] = 0
         got = ro_c.decode_blocks(damaged, k, op, rp, engine="avx2")
         assert np.array_equal(got, blocks)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_window128_two_pass_split(seed):
+    """The identity decode_x16's W = 128 passes rely on (rs_kernels.hip decode_x16 PASS 1/2):
+    the crate decoder's IFFT_128 -> formal derivative -> FFT_128 equals, per output half o,
+    FFT_64 (skew delta 64 o) of P(u_o) ^ u_(1-o), where u_h = IFFT_64 of window half h (delta
+    64 h) and P = the derivative without its self term -- because the size-128 layer's skew
+    factor (index 63) is zero.  Checked on random work vectors with the oracle's transforms."""
+    _, _, skew, _ = o.tables()
+    assert int(skew[63]) == o.GF_MODULUS
+    rng = np.random.default_rng(seed)
+    work = rng.integers(0, 65536, size=(128, 5), dtype=np.uint16)
+    ref = work.copy()
+    o.ifft(ref, 0, 128, 128, 0)
+    o.formal_derivative(ref)
+    o.fft(ref, 0, 128, 128, 0)
+    u = work.copy()
+    o.ifft(u, 0, 64, 64, 0)
+    o.ifft(u, 64, 64, 64, 64)
+
+    def P(v):
+        d = v.copy()
+        o.formal_derivative(d)
+        return d ^ v
+
+    for h in (0, 1):
+        x = P(u[64 * h:64 * h + 64]) ^ u[64 * (1 - h):64 * (1 - h) + 64]
+        o.fft(x, 0, 64, 64, 64 * h)
+        assert np.array_equal(x, ref[64 * h:64 * h + 64])
