@@ -159,6 +159,7 @@ struct ag_rs_ctx {
   DevBuf stage_pad, stage_mask;                  // restrided shards (sizes not whole 64-byte chunks)
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf d_pipe_few, d_pipe_mask;           // composed deshred: too-few flags, re-encode store masks
+  DevBuf d_present;                         // coder batches: per-slice present masks
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
   static constexpr int kPipeBufs = 25;
   DevBuf pipe[kPipeBufs];                   // composed shredder scratch (ag_shredder_*_batch)
@@ -244,7 +245,7 @@ struct ag_rs_ctx {
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
                       &d_xmask, &d_rows, &d_xblocks, &d_x128, &d_rows128, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
-                      &one_out, &d_pipe_few, &d_pipe_mask})
+                      &one_out, &d_pipe_few, &d_pipe_mask, &d_present})
       b->release();
     for (DevBuf& b : pipe) b.release();
     one_pin.release();
@@ -2129,6 +2130,11 @@ int ag_rs_coder_shred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, const ui
   return encode_device(c, kDataShreds, m, S, n, cw, cw_stride, cw + kDataShreds * S, cw_stride);
 }
 
+namespace {
+int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
+                       int64_t* plen);
+}  // namespace
+
 int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
                               const uint8_t* dpres, const uint8_t* cpres, int mode, int64_t* out) {
   if (!c || (n && (!cw || !dpres || !cpres || !out))) return AG_RS_ERR_INVALID_ARGUMENT;
@@ -2140,6 +2146,27 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   if (n == 0) return AG_RS_OK;
   int st = c->enter();
   if (st) return st;
+  // Per-slice patterns of RegularShredder's 32:32 on whole-chunk shreds (the follower's
+  // random arrival): one 64-bit present mask per slice goes to the device, and the window
+  // patterns, locator constants, per-lane decode, padding strip and re-encode run there
+  // (pipe_coder_deshred, the composed deshred's coder stage) -- no per-slice host work past
+  // the packing.  ANY_K, or EXACT where no slice holds more than 32 shreds (k shreds fix the
+  // codeword, so both decoders agree).  One pattern for the whole batch stays on the host
+  // path below (a single transform launch).
+  if (m == kDataShreds && S % 64 == 0 && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
+    std::vector<uint64_t> pres(n);
+    bool uniform = true, surplus = false;
+    for (size_t b = 0; b < n; ++b) {
+      pres[b] = pack_flags(dpres + b * kDataShreds, kDataShreds) | (pack_flags(cpres + b * m, m) << 32);
+      uniform = uniform && pres[b] == pres[0];
+      surplus = surplus || __builtin_popcountll(pres[b]) > static_cast<int>(kDataShreds);
+    }
+    if (!uniform && (mode == AG_RS_DECODE_ANY_K || !surplus)) {
+      if ((st = c->d_present.ensure(n * 8, c->stream))) return st;
+      AG_HIP(hipMemcpyAsync(c->d_present.ptr, pres.data(), n * 8, hipMemcpyHostToDevice, c->stream));
+      return pipe_coder_deshred(c, n, S, cw, cw_stride, c->d_present.as<uint64_t>(), out);  // synchronous
+    }
+  }
   // slices with fewer than 32 shreds: reported, and decoded as "nothing missing" (untouched)
   std::vector<uint8_t> op(dpres, dpres + n * kDataShreds);
   std::vector<uint8_t> ok(n, 1);

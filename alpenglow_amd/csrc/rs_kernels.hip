@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #include "rs_device.hpp"
@@ -848,6 +849,224 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
   });
 }
 
+// =====================================================================================
+// decode_h8<OUTH>: the W = 64 per-lane window decoder (decode_x16<true, 0>'s algorithm) on
+// 32-column tiles with the lane half as a position bit: 8 waves x 4 slots x 2 lane halves,
+// 64 KiB of swap buffer, so two workgroups share a CU and one's loads, swaps and barriers
+// overlap the other's arithmetic (decode_x16 runs one 1024-thread workgroup per CU).
+// Lane l holds column l & 31 of the tile; h = l >> 5 is a position bit.  Layouts (slot bits
+// | lane half | wave bits):
+//   A  slots p0 p1 | h p2 | waves p3 p4 p5   loads, locator multiplies, IFFT b0; FFT b0, stores
+//   B  slots p2 p1 | h p0 | waves p3 p4 p5   IFFT b1 b2 / FFT b1      (A <-> B: v_permlane32_swap)
+//   C  slots p2 p3 | h p0 | waves p1 p4 p5   IFFT b3 / FFT b2
+//   D  slots p4 p3 | h p0 | waves p1 p2 p5   IFFT b4 / FFT b3
+//   E  slots p4 p5 | h p0 | waves p1 p2 p3   IFFT b5, formal derivative, FFT b5 b4
+// A layer-b skew constant depends on the position bits above b.  From B on the lane half is
+// p0, below every layer's bit; layer 0 in A has a constant per lane half (both halves' XOR
+// programs run under the exec mask).  The derivative's p0 term crosses lane halves
+// (v_permlane32_swap of the pre-derivative slot).  OUTH = the window half (p5) holding the
+// restored originals (1 HighRate chunk 32, 0 the LowRate sub-window, -1 both): after FFT b4
+// the waves whose p5 is the other half send their live slots and retire.
+// =====================================================================================
+template <typename Lay, int B, bool INV, int DELTA, int T, int V, int HPOS>
+__device__ __forceinline__ void h8_bfly(uint32_t* x, uint32_t* y) {
+  constexpr int w = x8_expand(V, Lay::rel(B));
+  constexpr int S = ((Lay::pos(w, T) | HPOS) & ~((2 << B) - 1)) + (1 << B) + DELTA - 1;
+  if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(x, y);
+}
+// layer 0 in layout A: butterflies on slots (0, 1) and (2, 3); the lane half is p2
+template <bool INV, int DELTA>
+__device__ __forceinline__ void h8_layer0(int wave, int h, Regs4& r) {
+  using LA = X8Lay<0, 1, 3, 4, 5>;
+  static_for<2>([&](auto TT) {
+    constexpr int t = 2 * decltype(TT)::value;
+    if constexpr (INV) dev::xor_planes(r[t + 1], r[t]);
+    auto mul = [&](auto Vc) {
+      constexpr int v = decltype(Vc)::value;
+      if (h) h8_bfly<LA, 0, INV, DELTA, t, v, 4>(r[t], r[t + 1]);
+      else h8_bfly<LA, 0, INV, DELTA, t, v, 0>(r[t], r[t + 1]);
+    };
+    switch (wave) {  // every wave bit lies above bit 0
+      case 0: mul(std::integral_constant<int, 0>{}); break;
+      case 1: mul(std::integral_constant<int, 1>{}); break;
+      case 2: mul(std::integral_constant<int, 2>{}); break;
+      case 3: mul(std::integral_constant<int, 3>{}); break;
+      case 4: mul(std::integral_constant<int, 4>{}); break;
+      case 5: mul(std::integral_constant<int, 5>{}); break;
+      case 6: mul(std::integral_constant<int, 6>{}); break;
+      default: mul(std::integral_constant<int, 7>{}); break;
+    }
+    if constexpr (!INV) dev::xor_planes(r[t + 1], r[t]);
+  });
+}
+// A <-> B: slot bit 0 and the lane half trade places (an involution)
+__device__ __forceinline__ void h8_relayout(Regs4& r) {
+  static_for<2>([&](auto TT) {
+    constexpr int t = 2 * decltype(TT)::value;
+    static_for<16>([&](auto P) {
+      constexpr int q = decltype(P)::value;
+      const auto s = __builtin_amdgcn_permlane32_swap(r[t][q], r[t + 1][q], false, false);
+      r[t][q] = s[0];
+      r[t + 1][q] = s[1];
+    });
+  });
+}
+
+template <int OUTH>
+__global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p) {
+  using LB = X8Lay<2, 1, 3, 4, 5>;
+  using LC = X8Lay<2, 3, 1, 4, 5>;
+  using LD = X8Lay<4, 3, 1, 2, 5>;
+  using LE = X8Lay<4, 5, 1, 2, 3>;
+  constexpr int W = 64, kCols = 32;
+  __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
+  __shared__ X8Flags flags;
+  __shared__ uint32_t lcoef[kCols * W];     // the constants of the <= 32 blocks of the tile
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
+  const uint64_t c0 = static_cast<uint64_t>(tile) * kCols;
+  const uint64_t c1 = c0 + kCols - 1 < p.total_columns ? c0 + kCols - 1 : p.total_columns - 1;
+  const uint64_t sb0 = c0 / p.chunks_per_shard;
+  {
+    const uint32_t nbt = static_cast<uint32_t>(c1 / p.chunks_per_shard - sb0 + 1);  // <= 32
+    for (uint32_t i = threadIdx.x; i < nbt * W; i += blockDim.x) lcoef[i] = p.rows[(sb0 + i / W) * W + i % W];
+  }
+  if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t gc = c0 + (lane & 31);
+  const bool ok = gc < p.total_columns;
+  const uint64_t blk = ok ? gc / p.chunks_per_shard : sb0;
+  const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
+  const uint64_t in_mask = ok ? p.pmask[2 * blk] : 0;
+  const uint64_t out_mask = ok ? p.pmask[2 * blk + 1] : 0;
+  const uint32_t* coef = lcoef + (blk - sb0) * W;
+  const uint64_t off_r = blk * p.rec_block_stride + col * 64;
+  const uint64_t off_o = blk * p.orig_block_stride + col * 64;
+  const uint32_t opos = p.low_rate ? 0 : p.chunk, rpos = p.low_rate ? p.chunk : 0;
+  // layout A position of slot t in this lane
+  auto posA = [&](int t) -> uint32_t {
+    return static_cast<uint32_t>((t & 1) | ((t >> 1) << 1) | (h << 2) | (wave << 3));
+  };
+  Regs4 r;
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = posA(t);
+    if ((in_mask >> j) & 1) {
+      const bool is_rec = p.low_rate ? j >= p.chunk : j < p.chunk;
+      const uint8_t* src = is_rec ? p.rec + (j - rpos) * p.rec_shard_stride + off_r
+                                  : p.orig + (j - opos) * p.orig_shard_stride + off_o;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = *reinterpret_cast<const uint4*>(src + 16 * q);
+        r[t][4 * q] = x.x;
+        r[t][4 * q + 1] = x.y;
+        r[t][4 * q + 2] = x.z;
+        r[t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { r[t][decltype(P)::value] = 0; });
+    }
+  });
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = posA(t);
+    if ((in_mask >> j) & 1) {
+      dev::planes_from_raw(r[t]);
+      dev::mul_rt_poly(r[t], coef[j]);
+    }
+  });
+  // IFFT_64 (skew delta 0)
+  h8_layer0<true, 0>(wave, h, r);
+  h8_relayout(r);
+  x8_layer_t<LB, 1, true, 0>(wave, r);
+  x8_layer_t<LB, 2, true, 0>(wave, r);
+  x8_swap<1, 0, 1>(wave, lane, lds, &flags, r);
+  x8_layer_t<LC, 3, true, 0>(wave, r);
+  x8_swap<0, 1, 2>(wave, lane, lds, &flags, r);
+  x8_layer_t<LD, 4, true, 0>(wave, r);
+  x8_swap<1, 2, 3>(wave, lane, lds, &flags, r);
+  x8_layer_t<LE, 5, true, 0>(wave, r);
+  // formal derivative in E (slot t: p4 = t & 1, p5 = t >> 1; lane half p0; waves p1 p2 p3)
+  __syncthreads();  // every wave's swap reads are done: the exchange buffer is free
+  static_for<2>([&](auto Rho) {
+    constexpr int rho = decltype(Rho)::value;
+    static_for<2>([&](auto U) { lds_put(lds, 2 * wave + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+    static_for<2>([&](auto U) {
+      constexpr int t = 2 * rho + decltype(U)::value;
+      // p0 term: the lower half (p0 clear) adds the upper half's pre-derivative value
+      uint32_t hi[16];
+      static_for<16>([&](auto P) {
+        constexpr int q = decltype(P)::value;
+        hi[q] = __builtin_amdgcn_permlane32_swap(r[t][q], 0u, false, false)[1];
+      });
+      // slot bits, ascending t: partners t | 1, t | 2 > t still hold pre-derivative values
+      if constexpr (!(t & 1)) dev::xor_planes(r[t], r[t | 1]);
+      if constexpr (!(t & 2)) dev::xor_planes(r[t], r[t | 2]);
+      dev::xor_planes(r[t], hi);
+    });
+    __syncthreads();
+    static_for<3>([&](auto Bb) {
+      constexpr int b = decltype(Bb)::value;
+      if (!((wave >> b) & 1)) {
+        const int pw = wave | (1 << b);
+        static_for<2>([&](auto U) { lds_get_xor(lds, 2 * pw + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+      }
+    });
+    __syncthreads();
+  });
+  // FFT_64 (skew delta 0), ending in A
+  x8_layer_t<LE, 5, false, 0>(wave, r);
+  x8_layer_t<LE, 4, false, 0>(wave, r);
+  if constexpr (OUTH < 0) {
+    x8_swap<1, 2, 4>(wave, lane, lds, &flags, r);
+  } else {
+    // E -> D: slot bit 1 (p5) <-> wave bit 2 (p3).  After it a wave's slots all have p5 =
+    // its wave bit 2; the other half's waves only send the slots the live partner needs.
+    const int partner = wave ^ 4;
+    if (((wave >> 2) & 1) != OUTH) {
+      x8_wait_ge(&flags.done[partner], 3);
+      static_for<4>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        if constexpr (((t >> 1) & 1) == (OUTH > 0 ? 1 : 0)) {
+          lds_put(lds, 2 * partner + (t & 1), lane, r[t]);
+          __asm__ volatile("; h8 put %0" ::"n"(t));
+        }
+      });
+      x8_signal(&flags.ready[wave], 4, lane);
+      return;
+    }
+    x8_wait_ge(&flags.ready[partner], 4);
+    static_for<4>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      if constexpr (((t >> 1) & 1) != (OUTH > 0 ? 1 : 0)) {
+        lds_get(lds, 2 * wave + (t & 1), lane, r[t]);
+        __asm__ volatile("; h8 get %0" ::"n"(t));
+      }
+    });
+    x8_signal(&flags.done[wave], 4, lane);
+  }
+  x8_layer_t<LD, 3, false, 0>(wave, r);
+  x8_swap<0, 1, 5>(wave, lane, lds, &flags, r);
+  x8_layer_t<LC, 2, false, 0>(wave, r);
+  x8_swap<1, 0, 6>(wave, lane, lds, &flags, r);
+  x8_layer_t<LB, 1, false, 0>(wave, r);
+  uint32_t mine = 0;
+  static_for<4>([&](auto T) { mine |= static_cast<uint32_t>((out_mask >> posA(decltype(T)::value)) & 1); });
+  if (__builtin_amdgcn_ballot_w64(mine != 0) == 0) return;  // nothing to restore in this wave
+  h8_relayout(r);
+  h8_layer0<false, 0>(wave, h, r);
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = posA(t);
+    if ((out_mask >> j) & 1) {
+      dev::mul_rt_poly(r[t], coef[j]);
+      dev::store_chunk(p.orig + (j - opos) * p.orig_shard_stride + off_o, r[t]);
+    }
+  });
+}
+
 // Per pattern and window position x: the decoder's locator constant as a bitsliced
 // multiply matrix.  loc(x) = sum_{e erased, e != x} log(x ^ e) (mod 65535) -- the crate's
 // eval_poly over the window up to one constant factor, which cancels between the input
@@ -1643,6 +1862,15 @@ hipError_t launch_xform_lowrate_decode(unsigned j, const XformParams& p, hipStre
   return hipGetLastError();
 }
 
+// A/B aid: AG_RS_DX_H8=0 keeps per-lane W = 64 decodes on decode_x16
+static bool use_h8() {
+  static const bool on = [] {
+    const char* e = std::getenv("AG_RS_DX_H8");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
   if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -1655,8 +1883,19 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
     else hipLaunchKernelGGL((decode_x_kernel<4>), grid, dim3(256), 0, stream, p);
   } else if (W == 64 && pass == 0) {
     if (p.rows_w != 64) return hipErrorInvalidValue;
-    if (pl) hipLaunchKernelGGL((decode_x16_kernel<true, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
-    else hipLaunchKernelGGL((decode_x16_kernel<false, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
+    if (pl && use_h8()) {
+      // 32-column tiles (the caller's ntiles counts 64-column ones)
+      const uint64_t t32 = (p.total_columns + 31) / 32;
+      if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+      const dim3 g32(static_cast<unsigned>(t32));
+      if (p.low_rate) hipLaunchKernelGGL((decode_h8_kernel<0>), g32, dim3(512), 0, stream, p);
+      else if (p.chunk == 32) hipLaunchKernelGGL((decode_h8_kernel<1>), g32, dim3(512), 0, stream, p);
+      else hipLaunchKernelGGL((decode_h8_kernel<-1>), g32, dim3(512), 0, stream, p);
+    } else if (pl) {
+      hipLaunchKernelGGL((decode_x16_kernel<true, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
+    } else {
+      hipLaunchKernelGGL((decode_x16_kernel<false, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
+    }
   } else if (W == 128 && (pass == 1 || pass == 2)) {
     // the originals must lie in one window half: LowRate k <= 64 (half 0); HighRate chunk 64
     // (half 1)

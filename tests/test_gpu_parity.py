@@ -812,6 +812,42 @@ def test_decode_per_slice_random_patterns(ctx, dev, S, n, mode):
     assert np.array_equal(got, blocks)
 
 
+@pytest.mark.parametrize("k,m", [(32, 32), (32, 64), (32, 33), (40, 16), (48, 8), (20, 40)])
+@pytest.mark.parametrize("S,n", [(1024, 24), (64, 70), (192, 23)])
+@pytest.mark.parametrize("mode", [rs.DECODE_ANY_K, rs.DECODE_EXACT])
+def test_decode_per_lane_window64(ctx, dev, k, m, S, n, mode):
+    """Per-lane W = 64 windows on 32-column tiles (decode_h8): HighRate with the originals in
+    window half 1 (32:32), straddling both halves (40:16, 48:8: no pruned FFT half), and the
+    LowRate sub-window (32:64, 32:33, 20:40: originals in half 0).  S = 64 puts 32 blocks
+    in one tile (the most staged constants); S = 192 tiles that start mid-block.  Random
+    per-block losses keeping k..k+4 shards, against the original data; the class must be
+    window64 for some blocks (the others take the transform, LowRate-chunk, W = 128 or
+    generic paths)."""
+    rng = random.Random(k * 1009 + m * 31 + S + mode)
+    blocks = np.stack([np.frombuffer(o.block_bytes(4400 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    d_o, d_r, op, rp = blocks.copy(), rec.copy(), [], []
+    for b in range(n):
+        # LowRate: survivors inside the 64-point sub-window (recovery 0..31), else W = 128
+        pool = k + m if k > m else k + min(m, 32)
+        keep = set(rng.sample(range(pool), k + rng.randint(0, min(4, pool - k))))
+        if b % 9 == 4:
+            keep |= set(range(k))  # nothing to restore in this block
+        op += [1 if i in keep else 0 for i in range(k)]
+        rp += [1 if k + j in keep else 0 for j in range(m)]
+        for i in range(k):
+            if i not in keep:
+                d_o[b, i] = 0x5A
+        for j in range(m):
+            if k + j not in keep:
+                d_r[b, j] = 0xA5
+    got = gpu_decode(ctx, dev, d_o, d_r, op, rp, mode)
+    assert np.array_equal(got, blocks)
+    classes = rs.last_decode_classes(ctx)
+    if mode == rs.DECODE_ANY_K or k > m:  # the LowRate sub-window is ANY_K only
+        assert classes.get("window64", 0) > 0, classes
+
+
 # --------------------------------------------- shard sizes that are not whole 64-byte chunks
 
 @pytest.mark.parametrize("k,m,S", [(32, 32, 62), (32, 32, 1000), (32, 32, 1022), (32, 64, 1000), (32, 33, 1022),
