@@ -2132,7 +2132,7 @@ int ag_rs_coder_shred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, const ui
 
 namespace {
 int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
-                       int64_t* plen);
+                       int64_t* plen, size_t m);
 }  // namespace
 
 int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
@@ -2153,18 +2153,23 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   // the packing.  ANY_K, or EXACT where no slice holds more than 32 shreds (k shreds fix the
   // codeword, so both decoders agree).  One pattern for the whole batch stays on the host
   // path below (a single transform launch).
-  if (m == kDataShreds && S % 64 == 0 && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
-    std::vector<uint64_t> pres(n);
+  // CodingOnlyShredder's 32:64 (LowRate) takes the same path with the W = 128 window.
+  if ((m == kDataShreds || m == 2 * kDataShreds) && S % 64 == 0 && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
+    const size_t wps = m == kDataShreds ? 1 : 2;  // present words per slice
+    std::vector<uint64_t> pres(wps * n);
     bool uniform = true, surplus = false;
     for (size_t b = 0; b < n; ++b) {
-      pres[b] = pack_flags(dpres + b * kDataShreds, kDataShreds) | (pack_flags(cpres + b * m, m) << 32);
-      uniform = uniform && pres[b] == pres[0];
-      surplus = surplus || __builtin_popcountll(pres[b]) > static_cast<int>(kDataShreds);
+      const uint64_t* q = &pres[wps * b];
+      pres[wps * b] = pack_flags(dpres + b * kDataShreds, kDataShreds) | (pack_flags(cpres + b * m, 32) << 32);
+      if (wps == 2) pres[wps * b + 1] = pack_flags(cpres + b * m + 32, 32);
+      uniform = uniform && std::equal(q, q + wps, pres.data());
+      surplus = surplus ||
+                __builtin_popcountll(q[0]) + (wps == 2 ? __builtin_popcountll(q[1]) : 0) > static_cast<int>(kDataShreds);
     }
     if (!uniform && (mode == AG_RS_DECODE_ANY_K || !surplus)) {
-      if ((st = c->d_present.ensure(n * 8, c->stream))) return st;
-      AG_HIP(hipMemcpyAsync(c->d_present.ptr, pres.data(), n * 8, hipMemcpyHostToDevice, c->stream));
-      return pipe_coder_deshred(c, n, S, cw, cw_stride, c->d_present.as<uint64_t>(), out);  // synchronous
+      if ((st = c->d_present.ensure(wps * n * 8, c->stream))) return st;
+      AG_HIP(hipMemcpyAsync(c->d_present.ptr, pres.data(), wps * n * 8, hipMemcpyHostToDevice, c->stream));
+      return pipe_coder_deshred(c, n, S, cw, cw_stride, c->d_present.as<uint64_t>(), out, m);  // synchronous
     }
   }
   // slices with fewer than 32 shreds: reported, and decoded as "nothing missing" (untouched)
@@ -2622,19 +2627,83 @@ bool pipe_device_coder() {
 // 32-point encode rewrites the coding shreds of the slices that decoded and stripped (store
 // masks per slice; the others keep theirs).  plen[s] as ag_rs_coder_deshred_batch: the
 // payload length, or -NotEnoughShreds / -InvalidPadding.
-int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
-                       int64_t* plen) {
-  constexpr size_t k = kDataShreds, W = 64;
+int pipe_coder_finish(ag_rs_ctx* c, size_t n, const int64_t* strip, const uint8_t* few, int64_t* plen);
+// The same for CodingOnlyShredder's coder (LowRate 32:64, shredder.rs:362-395): every slice
+// decodes in the W = 128 window as the two per-lane decode_x16 passes (the class-8 patterns of
+// decode_device, built on the device by launch_pipe_patterns128), then the strip, and the
+// LowRate re-encode of both 32-shard recovery chunks under the per-slice store masks.
+// present: two words per slice (launch_pipe_patterns128).
+int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
+                               const uint64_t* d_present, int64_t* plen) {
+  constexpr size_t k = kDataShreds, m = 2 * kDataShreds;
   const size_t cps = S / 64;
   int st;
-  if ((st = c->ensure_tables()) || (st = c->d_xmask.ensure(3 * n * 8, c->stream)) ||
-      (st = c->d_rows.ensure(n * W * 4, c->stream)) || (st = c->d_pipe_few.ensure(n, c->stream)) ||
+  if ((st = c->d_x128.ensure(10 * n * 8, c->stream)) || (st = c->d_rows128.ensure(n * 128 * 4, c->stream))) return st;
+  uint64_t* xm = c->d_x128.as<uint64_t>();
+  uint8_t* few = c->d_pipe_few.as<uint8_t>();
+  if (ag::launch_pipe_patterns128(d_present, n, xm, few, c->stream) != hipSuccess ||
+      ag::launch_decode_rows128(xm, static_cast<uint32_t>(n), c->dtables(), c->d_rows128.as<uint32_t>(), c->stream) !=
+          hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  ag::DecodeXParams p{};
+  p.rec = cw + k * S;
+  p.rec_block_stride = cw_stride;
+  p.rec_shard_stride = S;
+  p.orig = cw;
+  p.orig_block_stride = cw_stride;
+  p.orig_shard_stride = S;
+  p.rows = c->d_rows128.as<uint32_t>();
+  p.rows_w = 128;
+  p.k = static_cast<uint32_t>(k);
+  p.m = 32;  // recovery shards per window half (the kernel addresses the rest from p.rec)
+  p.chunk = 32;
+  p.low_rate = 1;
+  p.chunks_per_shard = static_cast<uint32_t>(cps);
+  p.total_columns = static_cast<uint64_t>(n) * cps;
+  p.per_lane = 1;
+  for (int pass = 1; pass <= 2; ++pass) {
+    p.pmask = xm + (pass == 1 ? 6 : 8) * n;
+    if (ag::launch_decode_x(128, pass, p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
+      return AG_RS_ERR_DEVICE;
+  }
+  int64_t* strip = c->d_strip.as<int64_t>();
+  if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(k * S), n, strip, c->stream) != hipSuccess ||
+      ag::launch_pipe_store_masks(few, strip, n, c->d_pipe_mask.as<uint64_t>(), c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  for (unsigned j = 0; j * 32 < m; ++j) {  // one launch per recovery chunk (encode_cols' LowRate loop)
+    ag::XformParams xp{};
+    xp.in = cw;
+    xp.in_block_stride = cw_stride;
+    xp.in_shard_stride = S;
+    xp.out = cw + (k + 32 * j) * S;
+    xp.out_block_stride = cw_stride;
+    xp.out_shard_stride = S;
+    xp.out_mask = c->d_pipe_mask.as<uint64_t>();
+    xp.pattern_per_block = 1;
+    xp.n_in = static_cast<uint32_t>(k);
+    xp.n_out = 32;
+    xp.chunks_per_shard = static_cast<uint32_t>(cps);
+    xp.total_columns = static_cast<uint64_t>(n) * cps;
+    if (ag::launch_xform_lowrate(32, j, xp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
+  return pipe_coder_finish(c, n, strip, few, plen);
+}
+
+int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
+                       int64_t* plen, size_t m) {
+  constexpr size_t k = kDataShreds;
+  const size_t cps = S / 64;
+  int st;
+  if ((st = c->ensure_tables()) || (st = c->d_pipe_few.ensure(n, c->stream)) ||
       (st = c->d_pipe_mask.ensure(8 * n, c->stream)) || (st = c->d_strip.ensure(8 * n, c->stream)))
     return st;
+  uint8_t* few = c->d_pipe_few.as<uint8_t>();
+  if (m == 2 * kDataShreds) return pipe_coder_deshred_lowrate(c, n, S, cw, cw_stride, d_present, plen);
+  constexpr size_t W = 64;
+  if ((st = c->d_xmask.ensure(3 * n * 8, c->stream)) || (st = c->d_rows.ensure(n * W * 4, c->stream))) return st;
   c->xmask_host.clear();  // d_xmask / d_rows no longer hold decode_device's cached patterns
   c->xmask_w = 0;
   uint64_t* xm = c->d_xmask.as<uint64_t>();
-  uint8_t* few = c->d_pipe_few.as<uint8_t>();
   if (ag::launch_pipe_patterns(d_present, n, xm, few, c->stream) != hipSuccess ||
       ag::launch_decode_rows(xm, xm + n, static_cast<uint32_t>(n), static_cast<uint32_t>(W), c->dtables(),
                              c->d_rows.as<uint32_t>(), true, c->stream) != hipSuccess)
@@ -2676,6 +2745,10 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   xp.chunks_per_shard = static_cast<uint32_t>(cps);
   xp.total_columns = static_cast<uint64_t>(n) * cps;
   if (ag::launch_xform(ag::XformKind::kEncode32, xp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  return pipe_coder_finish(c, n, strip, few, plen);
+}
+// plen from the strip results and the too-few flags (synchronous)
+int pipe_coder_finish(ag_rs_ctx* c, size_t n, const int64_t* strip, const uint8_t* few, int64_t* plen) {
   std::vector<uint8_t> hfew(n);
   AG_HIP(hipMemcpyAsync(plen, strip, 8 * n, hipMemcpyDeviceToHost, c->stream));
   AG_HIP(hipMemcpyAsync(hfew.data(), few, n, hipMemcpyDeviceToHost, c->stream));
@@ -2909,7 +2982,7 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   //    all coding shreds, strips the padding); on the device for whole-chunk shreds
   std::vector<int64_t> plen(n);
   if (S % 64 == 0 && pipe_device_coder()) {
-    if ((st = pipe_coder_deshred(c, n, S, codewords, cw_stride, d_present, plen.data()))) return st;
+    if ((st = pipe_coder_deshred(c, n, S, codewords, cw_stride, d_present, plen.data(), kDataShreds))) return st;
   } else {
     std::vector<uint8_t> dp(n * ag::kPipeData), cp(n * (ag::kPipeShreds - ag::kPipeData));
     for (size_t s = 0; s < n; ++s)

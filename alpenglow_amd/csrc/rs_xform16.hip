@@ -47,7 +47,7 @@ __global__ __launch_bounds__(1024, 4) void xform16_kernel(const XformParams p) {
       const uint8_t* base = p.in + sh * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        const uint4 x = ld_piece(base + io.off[q]);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;

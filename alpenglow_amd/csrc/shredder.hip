@@ -144,6 +144,43 @@ __global__ __launch_bounds__(256) void pipe_patterns_kernel(const uint64_t* __re
   few[s] = cnt < kPipeData ? 1 : 0;
 }
 
+// ANY_K survivors of one CodingOnly slice (LowRate 32:64) in the W = 128 window, decode_device's
+// class-8 rule: originals i at i, recovery j at 32 + j (half 0 holds recovery 0..31, half 1
+// recovery 32..63 at 64..95), the present originals then recovery shards in index order up
+// to 32 survivors.  present[2 s] = data bits | coding 0..31 << 32, present[2 s + 1] = coding
+// 32..63.
+__global__ __launch_bounds__(256) void pipe_patterns128_kernel(const uint64_t* __restrict__ present, uint64_t n,
+                                                               uint64_t* __restrict__ xm, uint8_t* __restrict__ few) {
+  const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const uint64_t p0 = present[2 * s], p1 = present[2 * s + 1] & 0xFFFFFFFFull;
+  const uint64_t ob = p0 & 0xFFFFFFFFull;
+  uint64_t rb = (p0 >> 32) | (p1 << 32);  // coding 0..63
+  const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(p0) + __builtin_popcountll(p1));
+  uint64_t e0 = 0, e1 = 0, in0 = 0, in1 = 0, out0 = 0;
+  if (cnt >= kPipeData && ob != 0xFFFFFFFFull) {
+    const uint32_t budget = kPipeData - static_cast<uint32_t>(__builtin_popcountll(ob));
+    while (static_cast<uint32_t>(__builtin_popcountll(rb)) > budget) rb &= ~(uint64_t{1} << (63 - __builtin_clzll(rb)));
+    in0 = ob | ((rb & 0xFFFFFFFFull) << 32);
+    in1 = rb >> 32;
+    out0 = ~ob & 0xFFFFFFFFull;
+    e0 = out0 | (~in0 & ~0xFFFFFFFFull);  // lost / surplus recovery 0..31
+    e1 = ~in1;                            // lost / surplus recovery 32..63, positions past 95
+  }
+  uint64_t* q = xm + 6 * s;  // m6: erased, present, restored as (half 0, half 1) pairs
+  q[0] = e0;
+  q[1] = e1;
+  q[2] = in0;
+  q[3] = in1;
+  q[4] = out0;
+  q[5] = 0;
+  xm[6 * n + 2 * s] = in1;      // pass 1: the other half's survivors
+  xm[6 * n + 2 * s + 1] = out0;
+  xm[8 * n + 2 * s] = in0;      // pass 2: the output half's survivors
+  xm[8 * n + 2 * s + 1] = out0;
+  few[s] = cnt < kPipeData ? 1 : 0;
+}
+
 __global__ __launch_bounds__(256) void pipe_store_mask_kernel(const uint8_t* __restrict__ few,
                                                               const int64_t* __restrict__ strip, uint64_t n,
                                                               uint64_t* __restrict__ mask) {
@@ -204,6 +241,13 @@ hipError_t launch_pipe_patterns(const uint64_t* present, uint64_t nslices, uint6
                                 hipStream_t stream) {
   if (nslices == 0) return hipSuccess;
   hipLaunchKernelGGL(pipe_patterns_kernel, grid256(nslices), dim3(256), 0, stream, present, nslices, xm, few);
+  return hipGetLastError();
+}
+
+hipError_t launch_pipe_patterns128(const uint64_t* present, uint64_t nslices, uint64_t* xm, uint8_t* few,
+                                   hipStream_t stream) {
+  if (nslices == 0) return hipSuccess;
+  hipLaunchKernelGGL(pipe_patterns128_kernel, grid256(nslices), dim3(256), 0, stream, present, nslices, xm, few);
   return hipGetLastError();
 }
 

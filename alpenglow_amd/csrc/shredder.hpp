@@ -93,6 +93,12 @@ hipError_t launch_pipe_merge_lens(const uint32_t* fresh, const uint64_t* present
 // stores); few[s] = 1 for the former (NotEnoughShreds, reed_solomon.rs:144).
 hipError_t launch_pipe_patterns(const uint64_t* present, uint64_t nslices, uint64_t* xm, uint8_t* few,
                                 hipStream_t stream);
+// The same for CodingOnly slices (LowRate 32:64) in the W = 128 window of the two-pass decoder:
+// present[2 s] = data bits | coding 0..31 << 32, present[2 s + 1] = coding 32..63; xm =
+// decode_rows128's m6 [n][6], then the pass-1 and pass-2 (survivors, restored) pairs [n][2]
+// each (rs_api.cpp's class-8 layout).
+hipError_t launch_pipe_patterns128(const uint64_t* present, uint64_t nslices, uint64_t* xm, uint8_t* few,
+                                   hipStream_t stream);
 // mask[s] = ~0 (store every coding shard of the re-encode) when the slice decoded and its
 // padding stripped (few[s] == 0 and strip[s] >= 0), else 0 (the coding shreds stay as they
 // are, like the reference's early returns).

@@ -520,12 +520,18 @@ def coder_deshred(shreds, data_shreds: int, num_coding: int):
     """``ReedSolomonCoder::deshred`` (reed_solomon.rs:140-208) on validated shreds.
     Returns (payload, RawShreds) or raises RSError(NotEnoughShreds | TooMuchData |
     InvalidPadding)."""
-    present = sum(s is not None for s in shreds)
-    if present < DATA_SHREDS:
-        raise RSError("NotEnoughShreds")
     original = {i: shreds[i][1] for i in range(data_shreds) if shreds[i] is not None}
     recovery = {j - data_shreds: shreds[j][1]
                 for j in range(data_shreds, TOTAL_SHREDS) if shreds[j] is not None}
+    return coder_deshred_indexed(original, recovery, num_coding)
+
+
+def coder_deshred_indexed(original: dict, recovery: dict, num_coding: int):
+    """The body of ``ReedSolomonCoder::deshred`` (reed_solomon.rs:144-208) on the shreds'
+    data indices (``data_shred_payloads``) and coding indices (``coding_shred_payloads``):
+    the crate decoder over every given shred, padding strip, re-encode."""
+    if len(original) + len(recovery) < DATA_SHREDS:
+        raise RSError("NotEnoughShreds")
     restored = decode(DATA_SHREDS, num_coding, original, recovery)
     data = []
     payload = bytearray()

@@ -622,11 +622,14 @@ def test_coder_shred_batch_errors(ctx, dev):
 
 @pytest.mark.parametrize("S", [1024, 96])
 @pytest.mark.parametrize("mode", [rs.DECODE_EXACT, rs.DECODE_ANY_K])
-def test_coder_deshred_batch(ctx, dev, S, mode):
+@pytest.mark.parametrize("m", [32, 64])
+def test_coder_deshred_batch(ctx, dev, S, mode, m):
     """Batched deshred vs the oracle's ReedSolomonCoder::deshred: restored payload, all data
-    shards, re-encoded coding shards; NotEnoughShreds / InvalidPadding slices untouched."""
-    rng = random.Random(S + mode)
-    m, n = 32, 9
+    shards, re-encoded coding shards; NotEnoughShreds / InvalidPadding slices untouched.
+    m = 64 is CodingOnlyShredder's coder (LowRate 32:64; at S = 1024 the device-pattern path
+    with the W = 128 window), including slices that keep only coding shreds."""
+    rng = random.Random(S + mode + m)
+    n = 9
     stride = (32 + m) * S
     lens = _payload_lens(rng, S, n)
     cw = np.zeros((n, stride), np.uint8)
@@ -645,17 +648,19 @@ def test_coder_deshred_batch(ctx, dev, S, mode):
     present = []
     for b in range(n):
         if b == 0:
-            keep = set(range(64))
+            keep = set(range(32 + m))
         elif b == 1:
-            keep = set(range(32, 64))           # all data lost
+            keep = set(range(32, 64))           # all data lost (coding 0..31)
+        elif b == 2 and m == 64:
+            keep = set(rng.sample(range(32, 96), 32))  # CodingOnly random arrival: coding shreds only
         elif b == 3:
-            keep = set(rng.sample(range(64), 31))  # not enough
+            keep = set(rng.sample(range(32 + m), 31))  # not enough
         else:
-            keep = set(rng.sample(range(64), rng.randrange(32, 64)))
+            keep = set(rng.sample(range(32 + m), rng.randrange(32, 32 + m)))
         present.append(keep)
     damaged = cw.copy()
     for b in range(n):
-        for i in range(64):
+        for i in range(32 + m):
             if i not in present[b]:
                 damaged[b, i * S:(i + 1) * S] = 0xAB
     dp = [1 if i in present[b] else 0 for b in range(n) for i in range(32)]
@@ -664,9 +669,10 @@ def test_coder_deshred_batch(ctx, dev, S, mode):
     res = rs.coder_deshred_batch(ctx, m, n, S, d_cw, stride, dp, cp, mode)
     host = d_cw.cpu().numpy()
     for b in range(n):
-        shreds = [(i < 32, cw[b, i * S:(i + 1) * S].tobytes()) if i in present[b] else None for i in range(64)]
+        orig_b = {i: cw[b, i * S:(i + 1) * S].tobytes() for i in range(32) if i in present[b]}
+        rec_b = {j: cw[b, (32 + j) * S:(33 + j) * S].tobytes() for j in range(m) if 32 + j in present[b]}
         try:
-            payload, raw = o.coder_deshred(shreds, 32, m)
+            payload, raw = o.coder_deshred_indexed(orig_b, rec_b, m)
         except o.RSError as err:  # wrapper NotEnoughShreds maps to the crate status code
             assert res[b] == {"NotEnoughShreds": "NotEnoughShards"}.get(err.kind, err.kind), (b, res[b])
             assert host[b, 32 * S:].tobytes() == damaged[b, 32 * S:].tobytes()  # coding untouched
