@@ -596,7 +596,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
         const uint8_t* src;
         if constexpr (PL) src = base + (is_rec ? off_r : off_o) + 16 * q;
         else src = base + (is_rec ? io_r.off[q] : io_o.off[q]);
-        const uint4 x = *reinterpret_cast<const uint4*>(src);
+        const uint4 x = ld_piece(src);
         ra[t][4 * q] = x.x;
         ra[t][4 * q + 1] = x.y;
         ra[t][4 * q + 2] = x.z;
@@ -665,9 +665,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
 // IFFT_128 -> derivative -> FFT_128 gives output half o as FFT_64,64o(P u_o ^ u_{1-o}): the
 // size-128 layer's skew factor (index 63) is zero, so the halves meet only there
 // (tests/test_oracle.py pins the identity against the oracle's 128-point decoder).  Pass 1
-// (DIN = the other half, DOUT = the output half): IFFT, no derivative, FFT, output multiply,
-// the partial stored.  Pass 2 (DIN = DOUT = the output half): IFFT, P, FFT, output multiply,
-// XOR-ed into the stored partial (the multiply is linear).  Loads, masks and staged constants
+// (DIN = the other half, DOUT = the output half): IFFT, no derivative, FFT, the partial
+// stored unmultiplied.  Pass 2 (DIN = DOUT = the output half): IFFT, P, FFT, + the stored
+// partial (in planes), output multiply (linear: one product per restored original).  Loads, masks and staged constants
 // are the pass's loaded half (window positions DIN + j); outputs are window positions DOUT + j.
 // Multiplies by the per-position constants are Horner products in the polynomial basis
 // (mul_rt_poly); PL: per-lane constants staged in LDS, else one wave-uniform word.
@@ -704,7 +704,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
   __syncthreads();
   uint64_t in_mask, out_mask;
   const uint32_t* coef = lcoef;  // PL: the lane's staged constants; else the pattern's (global)
-  const uint32_t* coef_out;      // the output half's constants (PASS 1: global, not staged)
+  const uint32_t* coef_out;      // the output half's constants (PASS 1: none, its partial is unmultiplied)
   TileIO io_r, io_o;
   uint64_t off_r = 0, off_o = 0;
   if constexpr (PL) {
@@ -715,7 +715,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
     in_mask = ok ? p.pmask[2 * blk] : 0;
     out_mask = ok ? p.pmask[2 * blk + 1] : 0;
     coef = lcoef + (blk - sb0) * W;  // the lane's block among the staged ones
-    coef_out = PASS == 1 ? p.rows + blk * rw + DOUT : coef;
+    coef_out = coef;  // PASS 1 stores unmultiplied; PASS 2 has DIN == DOUT
     off_r = blk * p.rec_block_stride + col * 64;
     off_o = blk * p.orig_block_stride + col * 64;
   } else {
@@ -751,7 +751,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
         const uint8_t* src;
         if constexpr (PL) src = base + (is_rec ? off_r : off_o) + 16 * q;
         else src = base + (is_rec ? io_r.off[q] : io_o.off[q]);
-        const uint4 x = *reinterpret_cast<const uint4*>(src);
+        const uint4 x = ld_piece(src);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -840,11 +840,25 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
     const uint32_t j = 4 * wave + t;
     if ((out_mask >> j) & 1) {
       uint8_t* dst = p.orig + (DOUT + j - opos) * p.orig_shard_stride;
-      // the output multiply is linear: pass 1 stores its multiplied partial, pass 2 adds its
-      // own to the stored bytes (no extra planes live across the multiply)
-      dev::mul_rt_poly(r[t], coef_out[j]);
-      if constexpr (PL) dev::store_chunk<false, PASS == 2>(dst + off_o, r[t]);
-      else store_shard<PASS == 2>(dst, io_o, io_o.valid, r[t]);
+      // the output multiply is linear: pass 1 stores its unmultiplied partial, pass 2 adds it
+      // in planes and multiplies once
+      if constexpr (PASS == 2) {
+        uint32_t o[16];
+        static_for<4>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          const uint4 x = ld_piece(PL ? dst + off_o + 16 * q : dst + io_o.off[q]);
+          o[4 * q] = x.x;
+          o[4 * q + 1] = x.y;
+          o[4 * q + 2] = x.z;
+          o[4 * q + 3] = x.w;
+        });
+        if constexpr (!PL) swap_halves(o);
+        dev::planes_from_raw(o);
+        dev::xor_planes(r[t], o);
+      }
+      if constexpr (PASS != 1) dev::mul_rt_poly(r[t], coef_out[j]);
+      if constexpr (PL) dev::store_chunk<true>(dst + off_o, r[t]);
+      else store_shard(dst, io_o, io_o.valid, r[t]);
     }
   });
 }
@@ -867,6 +881,10 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
 // (v_permlane32_swap of the pre-derivative slot).  OUTH = the window half (p5) holding the
 // restored originals (1 HighRate chunk 32, 0 the LowRate sub-window, -1 both): after FFT b4
 // the waves whose p5 is the other half send their live slots and retire.
+// PASS 1 / 2: the W = 128 window as decode_x16's two 64-point passes (loaded half DIN, output
+// half DOUT), with the output multiply deferred: pass 1 stores FFT(u_other) unmultiplied,
+// pass 2 adds it to FFT(P u_out) in planes and multiplies once (the multiply is linear), so a
+// restored original costs one runtime product instead of two.
 // =====================================================================================
 template <typename Lay, int B, bool INV, int DELTA, int T, int V, int HPOS>
 __device__ __forceinline__ void h8_bfly(uint32_t* x, uint32_t* y) {
@@ -912,8 +930,10 @@ __device__ __forceinline__ void h8_relayout(Regs4& r) {
   });
 }
 
-template <int OUTH>
+template <int OUTH, int PASS, int DIN, int DOUT>
 __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p) {
+  static_assert(PASS != 0 || (DIN == 0 && DOUT == 0), "the one-pass window starts at 0");
+  static_assert(PASS != 2 || DIN == DOUT, "pass 2 loads its output half");
   using LB = X8Lay<2, 1, 3, 4, 5>;
   using LC = X8Lay<2, 3, 1, 4, 5>;
   using LD = X8Lay<4, 3, 1, 2, 5>;
@@ -931,7 +951,7 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   const uint64_t sb0 = c0 / p.chunks_per_shard;
   {
     const uint32_t nbt = static_cast<uint32_t>(c1 / p.chunks_per_shard - sb0 + 1);  // <= 32
-    for (uint32_t i = threadIdx.x; i < nbt * W; i += blockDim.x) lcoef[i] = p.rows[(sb0 + i / W) * W + i % W];
+    for (uint32_t i = threadIdx.x; i < nbt * W; i += blockDim.x) lcoef[i] = p.rows[(sb0 + i / W) * p.rows_w + DIN + i % W];
   }
   if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
@@ -954,12 +974,13 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
     constexpr int t = decltype(T)::value;
     const uint32_t j = posA(t);
     if ((in_mask >> j) & 1) {
-      const bool is_rec = p.low_rate ? j >= p.chunk : j < p.chunk;
-      const uint8_t* src = is_rec ? p.rec + (j - rpos) * p.rec_shard_stride + off_r
-                                  : p.orig + (j - opos) * p.orig_shard_stride + off_o;
+      const uint32_t g = DIN + j;  // window position
+      const bool is_rec = p.low_rate ? g >= p.chunk : g < p.chunk;
+      const uint8_t* src = is_rec ? p.rec + (g - rpos) * p.rec_shard_stride + off_r
+                                  : p.orig + (g - opos) * p.orig_shard_stride + off_o;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(src + 16 * q);
+        const uint4 x = ld_piece(src + 16 * q);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -977,18 +998,20 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
       dev::mul_rt_poly(r[t], coef[j]);
     }
   });
-  // IFFT_64 (skew delta 0)
-  h8_layer0<true, 0>(wave, h, r);
+  // IFFT_64 (skew delta DIN)
+  h8_layer0<true, DIN>(wave, h, r);
   h8_relayout(r);
-  x8_layer_t<LB, 1, true, 0>(wave, r);
-  x8_layer_t<LB, 2, true, 0>(wave, r);
+  x8_layer_t<LB, 1, true, DIN>(wave, r);
+  x8_layer_t<LB, 2, true, DIN>(wave, r);
   x8_swap<1, 0, 1>(wave, lane, lds, &flags, r);
-  x8_layer_t<LC, 3, true, 0>(wave, r);
+  x8_layer_t<LC, 3, true, DIN>(wave, r);
   x8_swap<0, 1, 2>(wave, lane, lds, &flags, r);
-  x8_layer_t<LD, 4, true, 0>(wave, r);
+  x8_layer_t<LD, 4, true, DIN>(wave, r);
   x8_swap<1, 2, 3>(wave, lane, lds, &flags, r);
-  x8_layer_t<LE, 5, true, 0>(wave, r);
-  // formal derivative in E (slot t: p4 = t & 1, p5 = t >> 1; lane half p0; waves p1 p2 p3)
+  x8_layer_t<LE, 5, true, DIN>(wave, r);
+  // formal derivative in E (slot t: p4 = t & 1, p5 = t >> 1; lane half p0; waves p1 p2 p3);
+  // PASS 2: P = the derivative without its self term; PASS 1: none
+  if constexpr (PASS != 1) {
   __syncthreads();  // every wave's swap reads are done: the exchange buffer is free
   static_for<2>([&](auto Rho) {
     constexpr int rho = decltype(Rho)::value;
@@ -1002,9 +1025,19 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
         hi[q] = __builtin_amdgcn_permlane32_swap(r[t][q], 0u, false, false)[1];
       });
       // slot bits, ascending t: partners t | 1, t | 2 > t still hold pre-derivative values
-      if constexpr (!(t & 1)) dev::xor_planes(r[t], r[t | 1]);
-      if constexpr (!(t & 2)) dev::xor_planes(r[t], r[t | 2]);
-      dev::xor_planes(r[t], hi);
+      if constexpr (PASS == 2) {
+        static_for<16>([&](auto P) {
+          constexpr int q = decltype(P)::value;
+          uint32_t v = hi[q];
+          if constexpr (!(t & 1)) v ^= r[t | 1][q];
+          if constexpr (!(t & 2)) v ^= r[t | 2][q];
+          r[t][q] = v;
+        });
+      } else {
+        if constexpr (!(t & 1)) dev::xor_planes(r[t], r[t | 1]);
+        if constexpr (!(t & 2)) dev::xor_planes(r[t], r[t | 2]);
+        dev::xor_planes(r[t], hi);
+      }
     });
     __syncthreads();
     static_for<3>([&](auto Bb) {
@@ -1016,9 +1049,10 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
     });
     __syncthreads();
   });
-  // FFT_64 (skew delta 0), ending in A
-  x8_layer_t<LE, 5, false, 0>(wave, r);
-  x8_layer_t<LE, 4, false, 0>(wave, r);
+  }
+  // FFT_64 (skew delta DOUT), ending in A
+  x8_layer_t<LE, 5, false, DOUT>(wave, r);
+  x8_layer_t<LE, 4, false, DOUT>(wave, r);
   if constexpr (OUTH < 0) {
     x8_swap<1, 2, 4>(wave, lane, lds, &flags, r);
   } else {
@@ -1047,22 +1081,40 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
     });
     x8_signal(&flags.done[wave], 4, lane);
   }
-  x8_layer_t<LD, 3, false, 0>(wave, r);
+  x8_layer_t<LD, 3, false, DOUT>(wave, r);
   x8_swap<0, 1, 5>(wave, lane, lds, &flags, r);
-  x8_layer_t<LC, 2, false, 0>(wave, r);
+  x8_layer_t<LC, 2, false, DOUT>(wave, r);
   x8_swap<1, 0, 6>(wave, lane, lds, &flags, r);
-  x8_layer_t<LB, 1, false, 0>(wave, r);
+  x8_layer_t<LB, 1, false, DOUT>(wave, r);
   uint32_t mine = 0;
   static_for<4>([&](auto T) { mine |= static_cast<uint32_t>((out_mask >> posA(decltype(T)::value)) & 1); });
   if (__builtin_amdgcn_ballot_w64(mine != 0) == 0) return;  // nothing to restore in this wave
   h8_relayout(r);
-  h8_layer0<false, 0>(wave, h, r);
+  h8_layer0<false, DOUT>(wave, h, r);
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = posA(t);
     if ((out_mask >> j) & 1) {
-      dev::mul_rt_poly(r[t], coef[j]);
-      dev::store_chunk(p.orig + (j - opos) * p.orig_shard_stride + off_o, r[t]);
+      uint8_t* dst = p.orig + (DOUT + j - opos) * p.orig_shard_stride + off_o;
+      if constexpr (PASS == 1) {
+        dev::store_chunk<true>(dst, r[t]);  // the unmultiplied partial
+      } else {
+        if constexpr (PASS == 2) {  // + pass 1's partial, in planes
+          uint32_t o[16];
+          static_for<4>([&](auto Q) {
+            constexpr int q = decltype(Q)::value;
+            const uint4 x = ld_piece(dst + 16 * q);
+            o[4 * q] = x.x;
+            o[4 * q + 1] = x.y;
+            o[4 * q + 2] = x.z;
+            o[4 * q + 3] = x.w;
+          });
+          dev::planes_from_raw(o);
+          dev::xor_planes(r[t], o);
+        }
+        dev::mul_rt_poly(r[t], coef[j]);
+        dev::store_chunk<true>(dst, r[t]);
+      }
     }
   });
 }
@@ -1135,7 +1187,7 @@ __device__ __forceinline__ void mc_load(const XformParams& p, const TileIO& io, 
       const uint8_t* base = p.in + (s0 + t) * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        const uint4 x = ld_piece(base + io.off[q]);
         raw[t][4 * q] = x.x;
         raw[t][4 * q + 1] = x.y;
         raw[t][4 * q + 2] = x.z;
@@ -1227,7 +1279,7 @@ __device__ __forceinline__ void syn_load(const DecodeSynParams& p, const TileIO&
       const uint8_t* base = p.orig + s * p.orig_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
+        const uint4 x = ld_piece(base + io.off[q]);
         raw[t][4 * q] = x.x;
         raw[t][4 * q + 1] = x.y;
         raw[t][4 * q + 2] = x.z;
@@ -1297,7 +1349,7 @@ __global__ __launch_bounds__(256, 2) void decode_syn_kernel(const DecodeSynParam
       uint32_t* sb = raw[0][b];
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(base + rio.off[q]);
+        const uint4 x = ld_piece(base + rio.off[q]);
         sb[4 * q] = x.x;
         sb[4 * q + 1] = x.y;
         sb[4 * q + 2] = x.z;
@@ -1888,9 +1940,9 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
       const uint64_t t32 = (p.total_columns + 31) / 32;
       if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
       const dim3 g32(static_cast<unsigned>(t32));
-      if (p.low_rate) hipLaunchKernelGGL((decode_h8_kernel<0>), g32, dim3(512), 0, stream, p);
-      else if (p.chunk == 32) hipLaunchKernelGGL((decode_h8_kernel<1>), g32, dim3(512), 0, stream, p);
-      else hipLaunchKernelGGL((decode_h8_kernel<-1>), g32, dim3(512), 0, stream, p);
+      if (p.low_rate) hipLaunchKernelGGL((decode_h8_kernel<0, 0, 0, 0>), g32, dim3(512), 0, stream, p);
+      else if (p.chunk == 32) hipLaunchKernelGGL((decode_h8_kernel<1, 0, 0, 0>), g32, dim3(512), 0, stream, p);
+      else hipLaunchKernelGGL((decode_h8_kernel<-1, 0, 0, 0>), g32, dim3(512), 0, stream, p);
     } else if (pl) {
       hipLaunchKernelGGL((decode_x16_kernel<true, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
     } else {
@@ -1900,6 +1952,25 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
     // the originals must lie in one window half: LowRate k <= 64 (half 0); HighRate chunk 64
     // (half 1)
     if (p.rows_w != 128 || (p.low_rate ? p.k > 64 : p.chunk != 64)) return hipErrorInvalidValue;
+    if (pl && use_h8()) {
+      // decode_h8 passes (32-column tiles, deferred output multiply): both passes of a decode
+      // must come from the same kernel family
+      const uint64_t t32 = (p.total_columns + 31) / 32;
+      if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+      const dim3 g32(static_cast<unsigned>(t32));
+      // LowRate: outputs (originals < 32 when k <= 32) in half 0; HighRate: half 1
+      if (p.low_rate && p.k <= 32) {
+        if (pass == 1) hipLaunchKernelGGL((decode_h8_kernel<0, 1, 64, 0>), g32, dim3(512), 0, stream, p);
+        else hipLaunchKernelGGL((decode_h8_kernel<0, 2, 0, 0>), g32, dim3(512), 0, stream, p);
+      } else if (p.low_rate) {
+        if (pass == 1) hipLaunchKernelGGL((decode_h8_kernel<-1, 1, 64, 0>), g32, dim3(512), 0, stream, p);
+        else hipLaunchKernelGGL((decode_h8_kernel<-1, 2, 0, 0>), g32, dim3(512), 0, stream, p);
+      } else {
+        if (pass == 1) hipLaunchKernelGGL((decode_h8_kernel<-1, 1, 0, 64>), g32, dim3(512), 0, stream, p);
+        else hipLaunchKernelGGL((decode_h8_kernel<-1, 2, 64, 64>), g32, dim3(512), 0, stream, p);
+      }
+      return hipGetLastError();
+    }
 #define AG_DX128(PLV, PS, DI, DO) hipLaunchKernelGGL((decode_x16_kernel<PLV, PS, DI, DO>), grid, dim3(1024), 0, stream, p)
     if (p.low_rate) {  // outputs in half 0
       if (pass == 1) { if (pl) AG_DX128(true, 1, 64, 0); else AG_DX128(false, 1, 64, 0); }
