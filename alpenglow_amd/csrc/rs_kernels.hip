@@ -886,50 +886,6 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
 // pass 2 adds it to FFT(P u_out) in planes and multiplies once (the multiply is linear), so a
 // restored original costs one runtime product instead of two.
 // =====================================================================================
-template <typename Lay, int B, bool INV, int DELTA, int T, int V, int HPOS>
-__device__ __forceinline__ void h8_bfly(uint32_t* x, uint32_t* y) {
-  constexpr int w = x8_expand(V, Lay::rel(B));
-  constexpr int S = ((Lay::pos(w, T) | HPOS) & ~((2 << B) - 1)) + (1 << B) + DELTA - 1;
-  if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(x, y);
-}
-// layer 0 in layout A: butterflies on slots (0, 1) and (2, 3); the lane half is p2
-template <bool INV, int DELTA>
-__device__ __forceinline__ void h8_layer0(int wave, int h, Regs4& r) {
-  using LA = X8Lay<0, 1, 3, 4, 5>;
-  static_for<2>([&](auto TT) {
-    constexpr int t = 2 * decltype(TT)::value;
-    if constexpr (INV) dev::xor_planes(r[t + 1], r[t]);
-    auto mul = [&](auto Vc) {
-      constexpr int v = decltype(Vc)::value;
-      if (h) h8_bfly<LA, 0, INV, DELTA, t, v, 4>(r[t], r[t + 1]);
-      else h8_bfly<LA, 0, INV, DELTA, t, v, 0>(r[t], r[t + 1]);
-    };
-    switch (wave) {  // every wave bit lies above bit 0
-      case 0: mul(std::integral_constant<int, 0>{}); break;
-      case 1: mul(std::integral_constant<int, 1>{}); break;
-      case 2: mul(std::integral_constant<int, 2>{}); break;
-      case 3: mul(std::integral_constant<int, 3>{}); break;
-      case 4: mul(std::integral_constant<int, 4>{}); break;
-      case 5: mul(std::integral_constant<int, 5>{}); break;
-      case 6: mul(std::integral_constant<int, 6>{}); break;
-      default: mul(std::integral_constant<int, 7>{}); break;
-    }
-    if constexpr (!INV) dev::xor_planes(r[t + 1], r[t]);
-  });
-}
-// A <-> B: slot bit 0 and the lane half trade places (an involution)
-__device__ __forceinline__ void h8_relayout(Regs4& r) {
-  static_for<2>([&](auto TT) {
-    constexpr int t = 2 * decltype(TT)::value;
-    static_for<16>([&](auto P) {
-      constexpr int q = decltype(P)::value;
-      const auto s = __builtin_amdgcn_permlane32_swap(r[t][q], r[t + 1][q], false, false);
-      r[t][q] = s[0];
-      r[t + 1][q] = s[1];
-    });
-  });
-}
-
 template <int OUTH, int PASS, int DIN, int DOUT>
 __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p) {
   static_assert(PASS != 0 || (DIN == 0 && DOUT == 0), "the one-pass window starts at 0");
@@ -1291,15 +1247,9 @@ __device__ __forceinline__ void syn_load(const DecodeSynParams& p, const TileIO&
   });
 }
 
-#ifndef AG_SYN_RT4
-#define AG_SYN_RT4 1
-#endif
 template <int C>
 __global__ __launch_bounds__(256, 2) void decode_syn_kernel(const DecodeSynParams p) {
   constexpr int NCMAX = kMcMaxK / C;
-#if !AG_SYN_RT4
-  __shared__ uint32_t stab[4][64 * 64];  // per wave: 4 groups x 16 entries x 64 lanes
-#endif
   const int lane = threadIdx.x & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   uint64_t tile = static_cast<uint64_t>(dev::xcd_tile(blockIdx.x, gridDim.x)) * 4 + wave;
@@ -1315,55 +1265,57 @@ __global__ __launch_bounds__(256, 2) void decode_syn_kernel(const DecodeSynParam
   const uint64_t dmask = sp->dmask;
   const uint32_t e = sp->e;
   const TileIO io = tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, p.orig_block_stride);
+  const TileIO rio = tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, p.rec_block_stride);
   const uint32_t nc = (p.k + C - 1) / C;
+  // recovery positions used for the syndromes (wave-uniform)
+  uint32_t used = 0;
+  for (uint32_t b = 0; b < e; ++b) used |= 1u << sp->rec[b];
+  // Stage 0 streams the used received recovery shards R (zero elsewhere) and starts the
+  // accumulator at IFFT_C,0(R); stages 1..nc stream the present originals' chunks as encode_mc.
+  // The final FFT_C,0 then yields re-encoded ^ R = the syndromes at the used positions
+  // (linearity), so no dependent recovery load sits between the stream and the correction.
   uint32_t acc[C][16];
   uint32_t raw[2][C][16];
-  syn_load<C>(p, io, dmask, 0, raw[0]);
-  static_for<NCMAX>([&](auto Cc) {
-    constexpr int c = decltype(Cc)::value;
-    if (c < nc) {
-      if (c + 1 < nc) syn_load<C>(p, io, dmask, (c + 1) * C, raw[(c + 1) & 1]);
-      auto& cur = raw[c & 1];
+  static_for<C>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    if ((used >> t) & 1) {
+      const uint8_t* base = p.rec + t * p.rec_shard_stride;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = ld_piece(base + rio.off[q]);
+        raw[0][t][4 * q] = x.x;
+        raw[0][t][4 * q + 1] = x.y;
+        raw[0][t][4 * q + 2] = x.z;
+        raw[0][t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { raw[0][t][decltype(P)::value] = 0; });
+    }
+  });
+  static_for<NCMAX + 1>([&](auto Sg) {
+    constexpr int sg = decltype(Sg)::value;
+    if (sg <= nc) {
+      if (sg < nc) syn_load<C>(p, io, dmask, sg * C, raw[(sg + 1) & 1]);
+      auto& cur = raw[sg & 1];
       static_for<C>([&](auto T) {
         swap_halves(cur[decltype(T)::value]);
         dev::planes_from_raw(cur[decltype(T)::value]);
       });
-      xform_lane<C, C * (c + 1), true>(cur);
+      if constexpr (sg == 0) {
+        xform_lane<C, 0, true>(cur);
+      } else {
+        xform_lane<C, C * sg, true>(cur);
+      }
       static_for<C>([&](auto T) {
         constexpr int t = decltype(T)::value;
         static_for<16>([&](auto P) {
           constexpr int q = decltype(P)::value;
-          if constexpr (c == 0) acc[t][q] = cur[t][q]; else acc[t][q] ^= cur[t][q];
+          if constexpr (sg == 0) acc[t][q] = cur[t][q]; else acc[t][q] ^= cur[t][q];
         });
       });
     }
   });
-  xform_lane<C, 0, false>(acc);  // re-encoded recovery shards 0..C-1
-  // syndromes S_b (b < e) into raw[0][b]
-  const TileIO rio = tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, p.rec_block_stride);
-  static_for<C>([&](auto B) {
-    constexpr int b = decltype(B)::value;
-    if (b < e) {
-      const uint32_t j = sp->rec[b];  // wave-uniform
-      const uint8_t* base = p.rec + j * p.rec_shard_stride;
-      uint32_t* sb = raw[0][b];
-      static_for<4>([&](auto Q) {
-        constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(base + rio.off[q]);
-        sb[4 * q] = x.x;
-        sb[4 * q + 1] = x.y;
-        sb[4 * q + 2] = x.z;
-        sb[4 * q + 3] = x.w;
-      });
-      swap_halves(sb);
-      dev::planes_from_raw(sb);
-      static_for<C>([&](auto J) {
-        constexpr int jj = decltype(J)::value;
-        if (j == jj) dev::xor_planes(sb, acc[jj]);
-      });
-    }
-  });
-#if AG_SYN_RT4
+  xform_lane<C, 0, false>(acc);  // syndromes S_b at positions rec[b]
   // Four Russians in registers (mul_rt4's scheme): per syndrome b, the 16 XOR combinations
   // of each 4-plane group (44 VALU) serve all e outputs; output plane o of Minv[a][b] S_b is
   // the XOR of 4 entries picked by row o's wave-uniform nibbles (one v_movrels each).
@@ -1374,10 +1326,12 @@ __global__ __launch_bounds__(256, 2) void decode_syn_kernel(const DecodeSynParam
   // (dynamic picks = v_movrels) within its promote-alloca budget; a set per syndrome
   // overflows the budget and lands in scratch
   uint32_t t0[16], t1[16], t2[16], t3[16];
-  static_for<C>([&](auto B) {
-    constexpr int b = decltype(B)::value;
-    if (b < e) {
-      const uint32_t* x = raw[0][b];
+  static_for<C>([&](auto J) {
+    constexpr int j = decltype(J)::value;
+    if ((used >> j) & 1) {
+      uint32_t b = 0;
+      while (b + 1 < e && sp->rec[b] != j) ++b;  // wave-uniform: the syndrome index of position j
+      const uint32_t* x = acc[j];
       auto fill = [&](uint32_t* t, const uint32_t* v) {
         const u32x16 c = syn_table(v);
         static_for<16>([&](auto V) { t[decltype(V)::value] = c[decltype(V)::value]; });
@@ -1404,54 +1358,6 @@ __global__ __launch_bounds__(256, 2) void decode_syn_kernel(const DecodeSynParam
     constexpr int a = decltype(A)::value;
     if (a < e) store_shard(p.orig + sp->out[a] * p.orig_shard_stride, io, io.valid, out[a]);
   });
-#else
-  // Four Russians: per syndrome, the 16 XOR combinations of each 4-plane group go to this
-  // wave's LDS table (entry-major, lane-minor: conflict-free); output plane o of
-  // Minv[a][b] S_b is then 4 table reads at the nibbles of row o (wave-uniform offsets).
-  // Outputs go in pairs so that 2 x 16 accumulators and the syndromes fit the registers.
-  constexpr int NP = C >= 2 ? 2 : 1;
-  uint32_t* tb = stab[wave];
-  static_for<(C + NP - 1) / NP>([&](auto Pp) {
-    constexpr int a0 = NP * decltype(Pp)::value;
-    if (a0 < e) {
-      uint32_t out[NP][16];
-      static_for<NP>([&](auto A) { static_for<16>([&](auto P) { out[decltype(A)::value][decltype(P)::value] = 0; }); });
-      static_for<C>([&](auto B) {
-        constexpr int b = decltype(B)::value;
-        if (b < e) {
-          const uint32_t* x = raw[0][b];
-          static_for<4>([&](auto G) {
-            constexpr int g = decltype(G)::value;
-            const u32x16 t = syn_table(x + 4 * g);
-            static_for<16>([&](auto V) { tb[(16 * g + decltype(V)::value) * 64 + lane] = t[decltype(V)::value]; });
-          });
-          __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-          static_for<NP>([&](auto A) {
-            constexpr int da = decltype(A)::value;
-            if (a0 + da < e) {
-              const uint32_t* rows = sp->rows[a0 + da][b];
-              static_for<16>([&](auto O) {
-                constexpr int o = decltype(O)::value;
-                const uint32_t r = __builtin_amdgcn_readfirstlane(rows[o]);
-                const uint32_t t0 = tb[(r & 15) * 64 + lane], t1 = tb[(16 + ((r >> 4) & 15)) * 64 + lane];
-                const uint32_t t2 = tb[(32 + ((r >> 8) & 15)) * 64 + lane];
-                const uint32_t t3 = tb[(48 + ((r >> 12) & 15)) * 64 + lane];
-                out[da][o] = dev::xor3(out[da][o], t0, t1) ^ dev::xor3(t2, t3, 0u);
-              });
-            }
-          });
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-          __builtin_amdgcn_wave_barrier();
-        }
-      });
-      static_for<NP>([&](auto A) {
-        constexpr int da = decltype(A)::value;
-        if (a0 + da < e) store_shard(p.orig + sp->out[a0 + da] * p.orig_shard_stride, io, io.valid, out[da]);
-      });
-    }
-  });
-#endif
 }
 
 // =====================================================================================

@@ -28,6 +28,9 @@ struct XformParams {
 
 enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };
 
+// In-process A/B selector of kernel variants (tools/ab_xform.py); 0 = the default kernels.
+int xform_variant();
+
 hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream);
 // True when the bitsliced transform exists for this transform size.
 bool xform_supported(unsigned n);

@@ -554,6 +554,54 @@ __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, Flags* f
 #endif
 }
 
+// ---- 32-column tiles with the lane half as a position bit (decode_h8, xform_h8) --------
+// Lane l holds column l & 31 of the tile; h = l >> 5 is position bit 2 in layout A (slots p0
+// p1 | h p2 | waves p3 p4 p5).  A <-> B (h8_relayout) trades slot bit 0 and the lane half.
+// The layer-0 butterfly of layout A; HPOS = the lane half's position bit (4 or 0).
+template <typename Lay, int B, bool INV, int DELTA, int T, int V, int HPOS>
+__device__ __forceinline__ void h8_bfly(uint32_t* x, uint32_t* y) {
+  constexpr int w = x8_expand(V, Lay::rel(B));
+  constexpr int S = ((Lay::pos(w, T) | HPOS) & ~((2 << B) - 1)) + (1 << B) + DELTA - 1;
+  if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(x, y);
+}
+// layer 0 in layout A: butterflies on slots (0, 1) and (2, 3); the lane half is p2
+template <bool INV, int DELTA>
+__device__ __forceinline__ void h8_layer0(int wave, int h, Regs4& r) {
+  using LA = X8Lay<0, 1, 3, 4, 5>;
+  static_for<2>([&](auto TT) {
+    constexpr int t = 2 * decltype(TT)::value;
+    if constexpr (INV) dev::xor_planes(r[t + 1], r[t]);
+    auto mul = [&](auto Vc) {
+      constexpr int v = decltype(Vc)::value;
+      if (h) h8_bfly<LA, 0, INV, DELTA, t, v, 4>(r[t], r[t + 1]);
+      else h8_bfly<LA, 0, INV, DELTA, t, v, 0>(r[t], r[t + 1]);
+    };
+    switch (wave) {  // every wave bit lies above bit 0
+      case 0: mul(std::integral_constant<int, 0>{}); break;
+      case 1: mul(std::integral_constant<int, 1>{}); break;
+      case 2: mul(std::integral_constant<int, 2>{}); break;
+      case 3: mul(std::integral_constant<int, 3>{}); break;
+      case 4: mul(std::integral_constant<int, 4>{}); break;
+      case 5: mul(std::integral_constant<int, 5>{}); break;
+      case 6: mul(std::integral_constant<int, 6>{}); break;
+      default: mul(std::integral_constant<int, 7>{}); break;
+    }
+    if constexpr (!INV) dev::xor_planes(r[t + 1], r[t]);
+  });
+}
+// A <-> B: slot bit 0 and the lane half trade places (an involution)
+__device__ __forceinline__ void h8_relayout(Regs4& r) {
+  static_for<2>([&](auto TT) {
+    constexpr int t = 2 * decltype(TT)::value;
+    static_for<16>([&](auto P) {
+      constexpr int q = decltype(P)::value;
+      const auto s = __builtin_amdgcn_permlane32_swap(r[t][q], r[t + 1][q], false, false);
+      r[t][q] = s[0];
+      r[t + 1][q] = s[1];
+    });
+  });
+}
+
 #ifndef AG_X8_PRIO
 #define AG_X8_PRIO 0
 #endif

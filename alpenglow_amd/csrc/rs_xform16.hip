@@ -104,10 +104,123 @@ __global__ __launch_bounds__(1024, 4) void xform16_kernel(const XformParams p) {
   });
 }
 
+
+// =====================================================================================
+// xform_h8: the same 64-point transform on 32-column tiles with the lane half as a position
+// bit (decode_h8's layouts without the locator products and the derivative): 8 waves x 4
+// slots x 2 lane halves, 64 KiB of swap buffer, so two 512-thread workgroups share a CU and
+// one's loads, swaps and stores overlap the other's arithmetic (xform16 runs one 1024-thread
+// workgroup per CU, its load -> swaps -> store sequence exposed between tiles).  Each lane
+// loads and stores whole 64-byte chunks (its column).  Measured slower than xform16 and kept
+// only as A/B variant 9 (profiles/r03_ab_xform_h8_rejected.txt, 64:64 at 64 KiB - 4 MiB blocks:
+// encode 2.8-3.2 vs 4.3-4.4 TB/s, reconstruct 3.0-3.4 vs 4.2-4.3): a lane's four 16-byte
+// pieces of one chunk are 64 bytes apart in every wave access, where xform16's lane-linear
+// 1 KiB accesses stream; decode_h8 gains from the second workgroup because its runtime
+// products, not its loads, dominate.  Layouts (slot bits | lane half | waves):
+//   A  slots p0 p1 | h p2 | waves p3 p4 p5   loads, IFFT b0; FFT b0, stores
+//   B  slots p2 p1 | h p0 | waves p3 p4 p5   IFFT b1 b2 / FFT b1
+//   C  slots p2 p3 | h p0 | waves p1 p4 p5   IFFT b3 / FFT b2
+//   D  slots p4 p3 | h p0 | waves p1 p2 p5   IFFT b4 / FFT b3
+//   E  slots p4 p5 | h p0 | waves p1 p2 p3   IFFT b5, FFT b5 b4
+// =====================================================================================
+template <int DIN, int DOUT>
+__global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
+  using LB = X8Lay<2, 1, 3, 4, 5>;
+  using LC = X8Lay<2, 3, 1, 4, 5>;
+  using LD = X8Lay<4, 3, 1, 2, 5>;
+  using LE = X8Lay<4, 5, 1, 2, 3>;
+  constexpr int kCols = 32;
+  __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
+  __shared__ X8Flags flags;
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
+  const uint64_t gc = static_cast<uint64_t>(tile) * kCols + (lane & 31);
+  const bool ok = gc < p.total_columns;
+  const uint64_t gcc = ok ? gc : p.total_columns - 1;  // idle lanes re-read the last chunk
+  const uint64_t blk = gcc / p.chunks_per_shard;
+  const uint64_t col = gcc - blk * p.chunks_per_shard;
+  const uint64_t off_in = blk * p.in_block_stride + col * 64;
+  const uint64_t off_out = blk * p.out_block_stride + col * 64;
+  uint64_t mask = ~0ull;
+  if (p.out_mask) mask = p.out_mask[p.pattern_per_block ? blk : 0];
+  if (!ok) mask = 0;
+  Regs4 r;
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = t | (h << 2) | (wave << 3);  // layout A position
+    if (s < p.n_in) {
+      const uint8_t* src = p.in + s * p.in_shard_stride + off_in;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = ld_piece(src + 16 * q);
+        r[t][4 * q] = x.x;
+        r[t][4 * q + 1] = x.y;
+        r[t][4 * q + 2] = x.z;
+        r[t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { r[t][decltype(P)::value] = 0; });
+    }
+  });
+  static_for<4>([&](auto T) { dev::planes_from_raw(r[decltype(T)::value]); });
+  // IFFT_64 (skew delta DIN)
+  h8_layer0<true, DIN>(wave, h, r);
+  h8_relayout(r);
+  x8_layer_t<LB, 1, true, DIN>(wave, r);
+  x8_layer_t<LB, 2, true, DIN>(wave, r);
+  x8_swap<1, 0, 1>(wave, lane, lds, &flags, r);
+  x8_layer_t<LC, 3, true, DIN>(wave, r);
+  x8_swap<0, 1, 2>(wave, lane, lds, &flags, r);
+  x8_layer_t<LD, 4, true, DIN>(wave, r);
+  x8_swap<1, 2, 3>(wave, lane, lds, &flags, r);
+  x8_layer_t<LE, 5, true, DIN>(wave, r);
+  // FFT_64 (skew delta DOUT), ending in A
+  x8_layer_t<LE, 5, false, DOUT>(wave, r);
+  x8_layer_t<LE, 4, false, DOUT>(wave, r);
+  x8_swap<1, 2, 4>(wave, lane, lds, &flags, r);
+  x8_layer_t<LD, 3, false, DOUT>(wave, r);
+  x8_swap<0, 1, 5>(wave, lane, lds, &flags, r);
+  x8_layer_t<LC, 2, false, DOUT>(wave, r);
+  x8_swap<1, 0, 6>(wave, lane, lds, &flags, r);
+  x8_layer_t<LB, 1, false, DOUT>(wave, r);
+  uint32_t need = 0;
+  static_for<4>([&](auto T) {
+    const uint32_t s = decltype(T)::value | (h << 2) | (wave << 3);
+    if (s < p.n_out && ((mask >> s) & 1)) need = 1;
+  });
+  // a wave's partner-swap duties are done: it may retire when it stores nothing
+  if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+  h8_relayout(r);
+  h8_layer0<false, DOUT>(wave, h, r);
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t s = t | (h << 2) | (wave << 3);
+    if (s < p.n_out && ((mask >> s) & 1)) dev::store_chunk<true>(p.out + s * p.out_shard_stride + off_out, r[t]);
+  });
+}
 }  // namespace
+
+constexpr bool kXform64OnH8 = false;
 
 hipError_t launch_xform16(unsigned din, unsigned dout, const XformParams& p, hipStream_t stream) {
   if (p.total_columns == 0) return hipSuccess;
+  // A/B: variant 9 = xform_h8 (32-column tiles, two workgroups per CU), 10 = xform16
+  const bool h8 = xform_variant() == 9 || (xform_variant() != 10 && kXform64OnH8);
+  if (h8) {
+    const uint64_t t32 = (p.total_columns + 31) / 32;
+    if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const dim3 g32(static_cast<unsigned>(t32));
+    if (din == 64 && dout == 0) hipLaunchKernelGGL((xform_h8_kernel<64, 0>), g32, dim3(512), 0, stream, p);
+    else if (din == 0 && dout == 64) hipLaunchKernelGGL((xform_h8_kernel<0, 64>), g32, dim3(512), 0, stream, p);
+    else if (din == 0 && dout == 128) hipLaunchKernelGGL((xform_h8_kernel<0, 128>), g32, dim3(512), 0, stream, p);
+    else if (din == 0 && dout == 192) hipLaunchKernelGGL((xform_h8_kernel<0, 192>), g32, dim3(512), 0, stream, p);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+  }
   const uint64_t tiles = (p.total_columns + kXfLanes - 1) / kXfLanes;
   if (tiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const dim3 grid(static_cast<unsigned>(tiles));
