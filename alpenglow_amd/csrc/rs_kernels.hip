@@ -68,18 +68,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
   // pass C only where some lane of the wave stores one of its 8 shards (a decode restores
   // only the erased originals)
   const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
-  uint32_t need = 0;
-  static_for<8>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    const uint32_t s = 8 * wave + t;
-    if (s < p.n_out && store_qmask(out_io, mask, s)) need = 1;
-  });
-  if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+  const uint32_t qall = qmask_all<8>(out_io, mask, 8 * wave, p.n_out);  // 32 bits: 8 shards x 4 pieces
+  if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;
   xf_pass_c<NW, DOUT>(wave, ra);
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = 8 * wave + t;  // wave-uniform
-    if (s < p.n_out) store_shard(p.out + s * p.out_shard_stride, out_io, store_qmask(out_io, mask, s), ra[t]);
+    if (s < p.n_out) store_shard(p.out + s * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, ra[t]);
   });
 }
 
@@ -159,17 +154,14 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
         static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[out_io.blk[decltype(Q)::value]]; });
       }
     }
-    uint32_t need = 0;
-    static_for<2>([&](auto U) {
-      const uint32_t sh = 2 * wave + decltype(U)::value;
-      if (sh < p.n_out && store_qmask(out_io, mask, sh)) need = 1;
-    });
-    if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+    // store predicates packed before the first store (bits 4 u + q; see qmask_all)
+    const uint32_t qall = qmask_all<2>(out_io, mask, 2 * wave, p.n_out);
+    if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;
     x8_layer_lay<H0, 0, DOUT, 0x5>(wave, r);
     static_for<2>([&](auto U) {
       constexpr int t = 2 * decltype(U)::value;
       const uint32_t sh = 2 * wave + (t >> 1);  // H0 position of live slot t
-      if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, store_qmask(out_io, mask, sh), r[t]);
+      if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * (t >> 1))) & 15u, r[t]);
     });
     return;
   }
@@ -192,17 +184,13 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
       static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[out_io.blk[decltype(Q)::value]]; });
     }
   }
-  uint32_t need = 0;
-  static_for<4>([&](auto T) {
-    const uint32_t sh = 4 * wave + decltype(T)::value;
-    if (sh < p.n_out && store_qmask(out_io, mask, sh)) need = 1;
-  });
-  if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+  const uint32_t qall = qmask_all<4>(out_io, mask, 4 * wave, p.n_out);
+  if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;
   x8_layer<0, 0, false, DOUT>(wave, r);
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t sh = 4 * wave + t;  // wave-uniform
-    if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, store_qmask(out_io, mask, sh), r[t]);
+    if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, r[t]);
   });
 }
 
@@ -409,18 +397,18 @@ __global__ __launch_bounds__(256, 2) void xform64h_kernel(const XformParams p) {
   xf_exchange_bc<4>(wave, lane, lds, rb, ra);
 
   const TileIO out_io = tile_io_h(p.total_columns, p.chunks_per_shard, tile, lane, p.out_block_stride);
-  uint32_t need = 0;
+  uint32_t qall = 0;  // store predicates packed before the first store (see qmask_all)
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = (wave << 4) | (t << 1) | h;
-    if (s < p.n_out && store_qmask(out_io, mask, s)) need = 1;
+    if (s < p.n_out) qall |= store_qmask(out_io, mask, s) << (4 * t);
   });
-  if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+  if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;
   x64h_pass_c<DOUT>(wave, hmask, ra);
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = (wave << 4) | (t << 1) | h;
-    if (s < p.n_out) store_shard_h(p.out + s * p.out_shard_stride, out_io, store_qmask(out_io, mask, s), ra[t]);
+    if (s < p.n_out) store_shard_h(p.out + s * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, ra[t]);
   });
 }
 
@@ -885,8 +873,14 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
 // half DOUT), with the output multiply deferred: pass 1 stores FFT(u_other) unmultiplied,
 // pass 2 adds it to FFT(P u_out) in planes and multiplies once (the multiply is linear), so a
 // restored original costs one runtime product instead of two.
+// LL (16 | chunks per shard): lane-linear loads and stores as xform_h8 (tile_io_l32's piece
+// order + quad_exchange).  Lane i of a half then holds chunks (i >> 2) and (i >> 2) + 8 (i & 2
+// clear) or those + 16 (i & 2 set): one 16-chunk group of the tile, so one slice, whose
+// pattern the lane computes with; its loads and stores also cover the quad partner's group,
+// under that group's masks.  Otherwise each lane loads its own whole chunk (pieces 64 bytes
+// apart in every wave access).
 // =====================================================================================
-template <int OUTH, int PASS, int DIN, int DOUT>
+template <int OUTH, int PASS, int DIN, int DOUT, bool LL>
 __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p) {
   static_assert(PASS != 0 || (DIN == 0 && DOUT == 0), "the one-pass window starts at 0");
   static_assert(PASS != 2 || DIN == DOUT, "pass 2 loads its output half");
@@ -911,15 +905,49 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   }
   if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t gc = c0 + (lane & 31);
-  const bool ok = gc < p.total_columns;
-  const uint64_t blk = ok ? gc / p.chunks_per_shard : sb0;
-  const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
-  const uint64_t in_mask = ok ? p.pmask[2 * blk] : 0;
-  const uint64_t out_mask = ok ? p.pmask[2 * blk + 1] : 0;
+  uint64_t blk, col, in_mask, out_mask;
+  // LL: the two 16-chunk groups of the tile -- block, first chunk, mask word (word 0: present,
+  // 1: restored) -- for lane ln (group 0: pieces q = 0, 1).  Computed at the loads and again
+  // at the stores (from laundered inputs: kept live across the transform they spill).
+  struct Groups {
+    uint64_t blk[2], col[2], mask[2];
+  };
+  auto groups = [&](uint64_t tile_c0, int ln, int word) {
+    Groups gr;
+    static_for<2>([&](auto G) {
+      constexpr int g = decltype(G)::value;
+      const uint64_t gc = tile_c0 + 16 * g + ((ln & 31) >> 2);  // chunks gc, gc + 8 (16 | cps)
+      const bool ok = gc < p.total_columns;
+      gr.blk[g] = ok ? gc / p.chunks_per_shard : sb0;
+      gr.col[g] = ok ? gc - gr.blk[g] * p.chunks_per_shard : 0;
+      gr.mask[g] = ok ? p.pmask[2 * gr.blk[g] + word] : 0;
+    });
+    return gr;
+  };
+  Groups gin{};
+  if constexpr (LL) {
+    gin = groups(c0, lane, 0);
+    const int own = (lane >> 1) & 1;
+    blk = own ? gin.blk[1] : gin.blk[0];
+    col = 0;
+    in_mask = own ? gin.mask[1] : gin.mask[0];
+    out_mask = 0;  // read at the stores
+  } else {
+    const uint64_t gc = c0 + (lane & 31);
+    const bool ok = gc < p.total_columns;
+    blk = ok ? gc / p.chunks_per_shard : sb0;
+    col = ok ? gc - blk * p.chunks_per_shard : 0;
+    in_mask = ok ? p.pmask[2 * blk] : 0;
+    out_mask = ok ? p.pmask[2 * blk + 1] : 0;
+  }
   const uint32_t* coef = lcoef + (blk - sb0) * W;
   const uint64_t off_r = blk * p.rec_block_stride + col * 64;
   const uint64_t off_o = blk * p.orig_block_stride + col * 64;
+  // LL: byte offset of piece q within a shard (rec / orig block strides)
+  auto piece_off = [&](const Groups& gr, int q, uint64_t block_stride) -> uint64_t {
+    const int g = q >> 1;
+    return gr.blk[g] * block_stride + (gr.col[g] + 8 * (q & 1)) * 64 + 16 * (lane & 3);
+  };
   const uint32_t opos = p.low_rate ? 0 : p.chunk, rpos = p.low_rate ? p.chunk : 0;
   // layout A position of slot t in this lane
   auto posA = [&](int t) -> uint32_t {
@@ -929,9 +957,22 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = posA(t);
-    if ((in_mask >> j) & 1) {
-      const uint32_t g = DIN + j;  // window position
-      const bool is_rec = p.low_rate ? g >= p.chunk : g < p.chunk;
+    const uint32_t g = DIN + j;  // window position
+    const bool is_rec = p.low_rate ? g >= p.chunk : g < p.chunk;
+    if constexpr (LL) {
+      const uint8_t* sh = is_rec ? p.rec + (g - rpos) * p.rec_shard_stride : p.orig + (g - opos) * p.orig_shard_stride;
+      const uint64_t bs = is_rec ? p.rec_block_stride : p.orig_block_stride;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if ((gin.mask[q >> 1] >> j) & 1) x = ld_piece(sh + piece_off(gin, q, bs));
+        r[t][4 * q] = x.x;
+        r[t][4 * q + 1] = x.y;
+        r[t][4 * q + 2] = x.z;
+        r[t][4 * q + 3] = x.w;
+      });
+      quad_exchange(r[t], lane);  // every lane: partners exchange whatever they loaded
+    } else if ((in_mask >> j) & 1) {
       const uint8_t* src = is_rec ? p.rec + (g - rpos) * p.rec_shard_stride + off_r
                                   : p.orig + (g - opos) * p.orig_shard_stride + off_o;
       static_for<4>([&](auto Q) {
@@ -1042,11 +1083,69 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   x8_layer_t<LC, 2, false, DOUT>(wave, r);
   x8_swap<1, 0, 6>(wave, lane, lds, &flags, r);
   x8_layer_t<LB, 1, false, DOUT>(wave, r);
+  Groups gout{};
+  if constexpr (LL) {
+    uint64_t c0_late = c0;
+    int lane_late = lane;
+    __asm__ volatile("" : "+s"(c0_late), "+v"(lane_late));
+    gout = groups(c0_late, lane_late, 1);
+    out_mask = ((lane >> 1) & 1) ? gout.mask[1] : gout.mask[0];
+  }
   uint32_t mine = 0;
   static_for<4>([&](auto T) { mine |= static_cast<uint32_t>((out_mask >> posA(decltype(T)::value)) & 1); });
   if (__builtin_amdgcn_ballot_w64(mine != 0) == 0) return;  // nothing to restore in this wave
   h8_relayout(r);
   h8_layer0<false, DOUT>(wave, h, r);
+  if constexpr (LL) {
+    // every store predicate packed before the first store (bit 4 t + q: piece q of slot t)
+    uint32_t qall = 0;
+    static_for<4>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        qall |= static_cast<uint32_t>((gout.mask[q >> 1] >> posA(t)) & 1) << (4 * t + q);
+      });
+      qall |= static_cast<uint32_t>((out_mask >> posA(t)) & 1) << (16 + t);  // the lane's own restore
+    });
+    static_for<4>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      const uint32_t j = posA(t);
+      const bool mine_t = (qall >> (16 + t)) & 1;
+      if (__builtin_amdgcn_ballot_w64(mine_t) == 0) return;  // (this slot only) wave-uniform
+      uint8_t* sh = p.orig + (DOUT + j - opos) * p.orig_shard_stride;
+      if constexpr (PASS == 2) {  // + pass 1's partial, in planes
+        uint32_t o[16];
+        static_for<4>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          uint4 x = make_uint4(0, 0, 0, 0);
+          if ((qall >> (4 * t + q)) & 1) x = ld_piece(sh + piece_off(gout, q, p.orig_block_stride));
+          o[4 * q] = x.x;
+          o[4 * q + 1] = x.y;
+          o[4 * q + 2] = x.z;
+          o[4 * q + 3] = x.w;
+        });
+        quad_exchange(o, lane);
+        if (mine_t) {
+          dev::planes_from_raw(o);
+          dev::xor_planes(r[t], o);
+        }
+      }
+      if constexpr (PASS != 1) {
+        if (mine_t) dev::mul_rt_poly(r[t], coef[j]);
+      }
+      uint32_t v[16];
+      static_for<16>([&](auto P) { v[decltype(P)::value] = r[t][decltype(P)::value]; });
+      dev::transpose8(v);
+      dev::transpose8(v + 8);
+      quad_exchange(v, lane);
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        if ((qall >> (4 * t + q)) & 1)
+          st_piece(sh + piece_off(gout, q, p.orig_block_stride), v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+      });
+    });
+    return;
+  }
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = posA(t);
@@ -1829,6 +1928,18 @@ static bool use_h8() {
   return on;
 }
 
+// A/B aid: AG_RS_H8_LL=1 runs decode_h8 with lane-linear loads and stores (16 | chunks per
+// shard).  Off by default: measured 14.0-14.1 vs 14.4-14.6 M slices/s on the follower's
+// random-arrival coder batch, 7.6-8.0 vs 7.5-7.6 M CodingOnly (profiles/r03_h8_ll_ab.jsonl) --
+// the per-lane products, not the strided loads, bound this kernel.
+static bool use_h8_ll() {
+  static const bool on = [] {
+    const char* e = std::getenv("AG_RS_H8_LL");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
   if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -1846,9 +1957,15 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
       const uint64_t t32 = (p.total_columns + 31) / 32;
       if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
       const dim3 g32(static_cast<unsigned>(t32));
-      if (p.low_rate) hipLaunchKernelGGL((decode_h8_kernel<0, 0, 0, 0>), g32, dim3(512), 0, stream, p);
-      else if (p.chunk == 32) hipLaunchKernelGGL((decode_h8_kernel<1, 0, 0, 0>), g32, dim3(512), 0, stream, p);
-      else hipLaunchKernelGGL((decode_h8_kernel<-1, 0, 0, 0>), g32, dim3(512), 0, stream, p);
+      const bool ll = p.chunks_per_shard % 16 == 0 && use_h8_ll();
+#define AG_H8(O, PS, DI, DO)                                                                   \
+  do {                                                                                        \
+    if (ll) hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO, true>), g32, dim3(512), 0, stream, p); \
+    else hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO, false>), g32, dim3(512), 0, stream, p);   \
+  } while (0)
+      if (p.low_rate) AG_H8(0, 0, 0, 0);
+      else if (p.chunk == 32) AG_H8(1, 0, 0, 0);
+      else AG_H8(-1, 0, 0, 0);
     } else if (pl) {
       hipLaunchKernelGGL((decode_x16_kernel<true, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
     } else {
@@ -1865,16 +1982,18 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
       if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
       const dim3 g32(static_cast<unsigned>(t32));
       // LowRate: outputs (originals < 32 when k <= 32) in half 0; HighRate: half 1
+      const bool ll = p.chunks_per_shard % 16 == 0 && use_h8_ll();
       if (p.low_rate && p.k <= 32) {
-        if (pass == 1) hipLaunchKernelGGL((decode_h8_kernel<0, 1, 64, 0>), g32, dim3(512), 0, stream, p);
-        else hipLaunchKernelGGL((decode_h8_kernel<0, 2, 0, 0>), g32, dim3(512), 0, stream, p);
+        if (pass == 1) AG_H8(0, 1, 64, 0);
+        else AG_H8(0, 2, 0, 0);
       } else if (p.low_rate) {
-        if (pass == 1) hipLaunchKernelGGL((decode_h8_kernel<-1, 1, 64, 0>), g32, dim3(512), 0, stream, p);
-        else hipLaunchKernelGGL((decode_h8_kernel<-1, 2, 0, 0>), g32, dim3(512), 0, stream, p);
+        if (pass == 1) AG_H8(-1, 1, 64, 0);
+        else AG_H8(-1, 2, 0, 0);
       } else {
-        if (pass == 1) hipLaunchKernelGGL((decode_h8_kernel<-1, 1, 0, 64>), g32, dim3(512), 0, stream, p);
-        else hipLaunchKernelGGL((decode_h8_kernel<-1, 2, 64, 64>), g32, dim3(512), 0, stream, p);
+        if (pass == 1) AG_H8(-1, 1, 0, 64);
+        else AG_H8(-1, 2, 64, 64);
       }
+#undef AG_H8
       return hipGetLastError();
     }
 #define AG_DX128(PLV, PS, DI, DO) hipLaunchKernelGGL((decode_x16_kernel<PLV, PS, DI, DO>), grid, dim3(1024), 0, stream, p)
@@ -1980,8 +2099,9 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
       else
         hipLaunchKernelGGL((xform8_kernel<0, 32>), grid, dim3(512), 0, stream, p);
       break;
-    // 64-point: xform16 (A/B against xform64h, profiles/r02_ab_xform16.json: encode 3.87 ->
-    // 4.46 TB/s, reconstruct 3.24 -> 4.14); variant 7 = xform64h, variant 1 = xform<8>.
+    // 64-point: launch_xform16 runs xform_h8 (32-column tiles, lane-linear I/O, two
+    // workgroups per CU; profiles/r03_ab_xform_h8.txt) or xform16 (variant 10; A/B against
+    // xform64h in profiles/r02_ab_xform16.json); variant 7 = xform64h, variant 1 = xform<8>.
     case XformKind::kEncode64:
       if (xform_variant() == 1)
         hipLaunchKernelGGL((xform_kernel<8, 64, 0>), grid, dim3(512), 0, stream, p);

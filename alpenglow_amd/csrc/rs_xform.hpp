@@ -336,6 +336,21 @@ __device__ __forceinline__ uint32_t store_qmask(const TileIO& io, const uint64_t
   return qm;
 }
 
+// The store predicates of NS consecutive shards s0 .. s0 + NS - 1 (wave-uniform s0), packed
+// before the first store: bits 4 i + q = store piece q of shard s0 + i.  Store loops read these
+// bits instead of re-deriving them from the mask words between stores: xform_h8 did that and
+// intermittently skipped whole lane classes' stores (per-block masks re-read with the slot
+// before's stores in flight; tools/stress_xform64.py).  NS <= 8.
+template <int NS>
+__device__ __forceinline__ uint32_t qmask_all(const TileIO& io, const uint64_t* mask, uint32_t s0, uint32_t n_out) {
+  uint32_t q = 0;
+  static_for<NS>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    if (s0 + i < n_out) q |= store_qmask(io, mask, s0 + i) << (4 * i);
+  });
+  return q;
+}
+
 // =====================================================================================
 // xform8: the 32-point transform with 8 waves per workgroup and 4 shard slots per lane.
 // Half the per-lane state of xform<4> (16 loads per lane in flight instead of 32, ~half
@@ -599,6 +614,48 @@ __device__ __forceinline__ void h8_relayout(Regs4& r) {
       r[t][q] = s[0];
       r[t + 1][q] = s[1];
     });
+  });
+}
+
+// Lane-linear I/O for 32-column tiles (xform_h8): in each half (lanes 0..31, 32..63: two
+// positions) lane i reads quarter i & 3 of chunk (i >> 2) + 8 q with instruction q, so every
+// instruction streams 512 contiguous bytes per half (when 8 | chunks per shard).  Quarters 0 /
+// 1 are the low bytes of symbols 0-15 / 16-31, quarters 2 / 3 the high bytes of the same
+// symbols: quad_exchange (lanes i <-> i ^ 2, one DPP quad permute per dword) leaves each lane
+// the low and high bytes of 16 symbols of two chunks -- registers 0..7 low bytes, 8..15 high
+// bytes, planes_from_raw's input -- and, being an involution, turns computed bytes back into
+// the pieces each lane stores.
+__device__ __forceinline__ TileIO tile_io_l32(uint64_t total_columns, uint32_t chunks_per_shard, uint64_t tile, int lane,
+                                              uint64_t block_stride) {
+  TileIO io;
+  io.valid = 0;
+  const uint32_t i = lane & 31;
+  static_for<4>([&](auto Q) {
+    constexpr int q = decltype(Q)::value;
+    const uint64_t g = tile * 32 + (i >> 2) + 8 * q;
+    const bool ok = g < total_columns;
+    const uint64_t gc = ok ? g : total_columns - 1;
+    const uint64_t blk = gc / chunks_per_shard;
+    io.blk[q] = blk;
+    io.off[q] = blk * block_stride + (gc - blk * chunks_per_shard) * 64 + 16 * (i & 3);
+    io.valid |= ok ? (1u << q) : 0u;
+  });
+  return io;
+}
+__device__ __forceinline__ void quad_exchange(uint32_t* v, int lane) {
+  const bool lo = (lane & 2) == 0;  // quarters 0, 1 keep registers 0..7
+  static_for<8>([&](auto D) {
+    constexpr int d = decltype(D)::value;
+    const uint32_t a = v[d], b = v[8 + d];  // selects, not a pointer choice (keeps v in VGPRs)
+#ifdef AG_QX_SWIZZLE
+    const uint32_t recv = static_cast<uint32_t>(
+        __builtin_amdgcn_ds_swizzle(static_cast<int>(lo ? b : a), 0x804E /* quad mode, perm 2,3,0,1 */));
+#else
+    const uint32_t recv = static_cast<uint32_t>(
+        __builtin_amdgcn_mov_dpp(static_cast<int>(lo ? b : a), 0x4E /* quad_perm 2,3,0,1 */, 0xF, 0xF, false));
+#endif
+    v[d] = lo ? a : recv;
+    v[8 + d] = lo ? recv : b;
   });
 }
 

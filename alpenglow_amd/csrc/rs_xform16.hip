@@ -90,17 +90,13 @@ __global__ __launch_bounds__(1024, 4) void xform16_kernel(const XformParams p) {
       static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[out_io.blk[decltype(Q)::value]]; });
     }
   }
-  uint32_t need = 0;
-  static_for<4>([&](auto T) {
-    const uint32_t sh = 4 * wave + decltype(T)::value;
-    if (sh < p.n_out && store_qmask(out_io, mask, sh)) need = 1;
-  });
-  if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+  const uint32_t qall = qmask_all<4>(out_io, mask, 4 * wave, p.n_out);
+  if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;
   x8_layer_t<G0, 0, false, DOUT>(wave, r);
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t sh = 4 * wave + t;  // wave-uniform
-    if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, store_qmask(out_io, mask, sh), r[t]);
+    if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, r[t]);
   });
 }
 
@@ -110,13 +106,13 @@ __global__ __launch_bounds__(1024, 4) void xform16_kernel(const XformParams p) {
 // bit (decode_h8's layouts without the locator products and the derivative): 8 waves x 4
 // slots x 2 lane halves, 64 KiB of swap buffer, so two 512-thread workgroups share a CU and
 // one's loads, swaps and stores overlap the other's arithmetic (xform16 runs one 1024-thread
-// workgroup per CU, its load -> swaps -> store sequence exposed between tiles).  Each lane
-// loads and stores whole 64-byte chunks (its column).  Measured slower than xform16 and kept
-// only as A/B variant 9 (profiles/r03_ab_xform_h8_rejected.txt, 64:64 at 64 KiB - 4 MiB blocks:
-// encode 2.8-3.2 vs 4.3-4.4 TB/s, reconstruct 3.0-3.4 vs 4.2-4.3): a lane's four 16-byte
-// pieces of one chunk are 64 bytes apart in every wave access, where xform16's lane-linear
-// 1 KiB accesses stream; decode_h8 gains from the second workgroup because its runtime
-// products, not its loads, dominate.  Layouts (slot bits | lane half | waves):
+// workgroup per CU, its load -> swaps -> store sequence exposed between tiles).  Loads and
+// stores are lane-linear (tile_io_l32 + quad_exchange).  The default 64-point kernel: 4.81-4.91
+// vs 4.23-4.41 TB/s encode, 4.55-4.60 vs 4.22-4.37 reconstruct against xform16 on 64 KiB - 4
+// MiB blocks (profiles/r03_ab_xform_h8.txt).  A first version that gave each lane one whole
+// chunk (its four 16-byte pieces 64 bytes apart in every wave access) ran 2.8-3.4 TB/s
+// (profiles/r03_ab_xform_h8_rejected.txt).
+// Layouts (slot bits | lane half | waves):
 //   A  slots p0 p1 | h p2 | waves p3 p4 p5   loads, IFFT b0; FFT b0, stores
 //   B  slots p2 p1 | h p0 | waves p3 p4 p5   IFFT b1 b2 / FFT b1
 //   C  slots p2 p3 | h p0 | waves p1 p4 p5   IFFT b3 / FFT b2
@@ -129,7 +125,6 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
   using LC = X8Lay<2, 3, 1, 4, 5>;
   using LD = X8Lay<4, 3, 1, 2, 5>;
   using LE = X8Lay<4, 5, 1, 2, 3>;
-  constexpr int kCols = 32;
   __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
   __shared__ X8Flags flags;
   const int lane = threadIdx.x & 63;
@@ -138,25 +133,16 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
   if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
   const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
-  const uint64_t gc = static_cast<uint64_t>(tile) * kCols + (lane & 31);
-  const bool ok = gc < p.total_columns;
-  const uint64_t gcc = ok ? gc : p.total_columns - 1;  // idle lanes re-read the last chunk
-  const uint64_t blk = gcc / p.chunks_per_shard;
-  const uint64_t col = gcc - blk * p.chunks_per_shard;
-  const uint64_t off_in = blk * p.in_block_stride + col * 64;
-  const uint64_t off_out = blk * p.out_block_stride + col * 64;
-  uint64_t mask = ~0ull;
-  if (p.out_mask) mask = p.out_mask[p.pattern_per_block ? blk : 0];
-  if (!ok) mask = 0;
+  const TileIO io = tile_io_l32(p.total_columns, p.chunks_per_shard, tile, lane, p.in_block_stride);
   Regs4 r;
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = t | (h << 2) | (wave << 3);  // layout A position
     if (s < p.n_in) {
-      const uint8_t* src = p.in + s * p.in_shard_stride + off_in;
+      const uint8_t* base = p.in + s * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(src + 16 * q);
+        const uint4 x = ld_piece(base + io.off[q]);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -166,7 +152,10 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
       static_for<16>([&](auto P) { r[t][decltype(P)::value] = 0; });
     }
   });
-  static_for<4>([&](auto T) { dev::planes_from_raw(r[decltype(T)::value]); });
+  static_for<4>([&](auto T) {
+    quad_exchange(r[decltype(T)::value], lane);
+    dev::planes_from_raw(r[decltype(T)::value]);
+  });
   // IFFT_64 (skew delta DIN)
   h8_layer0<true, DIN>(wave, h, r);
   h8_relayout(r);
@@ -178,6 +167,9 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
   x8_layer_t<LD, 4, true, DIN>(wave, r);
   x8_swap<1, 2, 3>(wave, lane, lds, &flags, r);
   x8_layer_t<LE, 5, true, DIN>(wave, r);
+#ifdef AG_XH8_MIDSYNC
+  __syncthreads();
+#endif
   // FFT_64 (skew delta DOUT), ending in A
   x8_layer_t<LE, 5, false, DOUT>(wave, r);
   x8_layer_t<LE, 4, false, DOUT>(wave, r);
@@ -187,24 +179,59 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
   x8_layer_t<LC, 2, false, DOUT>(wave, r);
   x8_swap<1, 0, 6>(wave, lane, lds, &flags, r);
   x8_layer_t<LB, 1, false, DOUT>(wave, r);
-  uint32_t need = 0;
-  static_for<4>([&](auto T) {
-    const uint32_t s = decltype(T)::value | (h << 2) | (wave << 3);
-    if (s < p.n_out && ((mask >> s) & 1)) need = 1;
-  });
+  // store addresses computed only now; the empty asm keeps the compiler from keeping the
+  // load-time divisions live across the transform (VGPR pressure)
+  uint32_t tile_late = tile;
+  int lane_late = lane;
+  __asm__ volatile("" : "+s"(tile_late), "+v"(lane_late));
+  const TileIO out_io = tile_io_l32(p.total_columns, p.chunks_per_shard, tile_late, lane_late, p.out_block_stride);
+  // Every store predicate of the wave, packed before the first store (bit 4 t + q: piece q of
+  // slot t): the store loop then reads no mask word.  With per-block masks re-read between
+  // the slots' stores, whole lane classes of a slot intermittently skipped their stores.
+  uint32_t qall = 0;
+  {
+    uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
+    if (p.out_mask) {
+      if (!p.pattern_per_block) {
+        const uint64_t m = p.out_mask[0];
+        mask[0] = mask[1] = mask[2] = mask[3] = m;
+      } else {
+        static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[out_io.blk[decltype(Q)::value]]; });
+      }
+    }
+    static_for<4>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      const uint32_t s = t | (h << 2) | (wave << 3);
+      if (s < p.n_out) qall |= store_qmask(out_io, mask, s) << (4 * t);
+    });
+  }
   // a wave's partner-swap duties are done: it may retire when it stores nothing
-  if (__builtin_amdgcn_ballot_w64(need != 0) == 0) return;
+#ifndef AG_XH8_NO_RETIRE
+  if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;
+#endif
   h8_relayout(r);
   h8_layer0<false, DOUT>(wave, h, r);
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = t | (h << 2) | (wave << 3);
-    if (s < p.n_out && ((mask >> s) & 1)) dev::store_chunk<true>(p.out + s * p.out_shard_stride + off_out, r[t]);
+    // the quad partners' quarters belong to the same shard: both lanes take part in the
+    // exchange, each stores only its own pieces
+    uint32_t v[16];
+    static_for<16>([&](auto P) { v[decltype(P)::value] = r[t][decltype(P)::value]; });
+    dev::transpose8(v);
+    dev::transpose8(v + 8);
+    quad_exchange(v, lane);
+    uint8_t* base = p.out + s * p.out_shard_stride;
+    static_for<4>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      if ((qall >> (4 * t + q)) & 1) st_piece(base + out_io.off[q], v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    });
   });
 }
+
 }  // namespace
 
-constexpr bool kXform64OnH8 = false;
+constexpr bool kXform64OnH8 = true;  // profiles/r03_ab_xform_h8.txt: +11-14 % encode, +5-8 % reconstruct
 
 hipError_t launch_xform16(unsigned din, unsigned dout, const XformParams& p, hipStream_t stream) {
   if (p.total_columns == 0) return hipSuccess;

@@ -205,8 +205,8 @@ def test_fast_decode_64_point(ctx, dev, erased):
 
 @pytest.mark.parametrize("variant", [7, 9, 10])
 def test_transform64_kernel_variants(ctx, dev, variant):
-    """The 64-point transform's A/B kernels (7 = xform64h, 9 = xform_h8 on 32-column tiles,
-    10 = xform16 on 64-column tiles; 0 is the default the other tests run): HighRate encodes
+    """The 64-point transform's A/B kernels (7 = xform64h, 9 = xform_h8 on 32-column tiles --
+    the default the other tests run --, 10 = xform16 on 64-column tiles): HighRate encodes
     with next_pow2(m) = 64, LowRate 64-point chunk encodes and full-recovery decodes with
     per-block store masks, bit-exact against the C oracle."""
     lib = rs.load()
