@@ -2135,6 +2135,46 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
                        int64_t* plen, size_t m);
 }  // namespace
 
+namespace {
+// ag_rs_coder_deshred_batch when every slice has the same present shreds (pattern = slice 0's).
+int coder_deshred_uniform(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
+                          const uint8_t* dpres, const uint8_t* cpres, int mode, int64_t* out) {
+  const size_t nd = count_flags(dpres, kDataShreds), nc = count_flags(cpres, m);
+  if (nd + nc < kDataShreds) {  // reed_solomon.rs:144: nothing decoded, coding untouched
+    for (size_t b = 0; b < n; ++b) out[b] = -AG_RS_ERR_NOT_ENOUGH_SHARDS;
+    return AG_RS_OK;
+  }
+  uint8_t* rec = cw + kDataShreds * S;
+  int st = decode_device(c, kDataShreds, m, S, n, cw, cw_stride, rec, cw_stride, dpres, cpres, 1, mode);
+  if (st) return st;
+  if ((st = c->d_strip.ensure(n * 8, c->stream))) return st;
+  if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(kDataShreds * S), n, c->d_strip.as<int64_t>(),
+                             c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  AG_HIP(hipMemcpyAsync(out, c->d_strip.ptr, n * 8, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipStreamSynchronize(c->stream));
+  for (size_t b = 0; b < n; ++b)
+    if (out[b] < 0) out[b] = -AG_RS_ERR_INVALID_PADDING;
+  // re-encode (encode_coding_from_data) the runs of slices that stripped; skipped when the
+  // present shreds are exactly the 32 coding shreds (the re-encode reproduces them)
+  if (m == kDataShreds && nd == 0 && nc == m) return AG_RS_OK;
+  for (size_t b = 0; b < n;) {
+    if (out[b] < 0) {
+      ++b;
+      continue;
+    }
+    size_t e = b;
+    while (e < n && out[e] >= 0) ++e;
+    if ((st = encode_device(c, kDataShreds, m, S, e - b, cw + b * cw_stride, cw_stride, rec + b * cw_stride,
+                            cw_stride)))
+      return st;
+    b = e;
+  }
+  AG_HIP(hipStreamSynchronize(c->stream));
+  return AG_RS_OK;
+}
+}  // namespace
+
 int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
                               const uint8_t* dpres, const uint8_t* cpres, int mode, int64_t* out) {
   if (!c || (n && (!cw || !dpres || !cpres || !out))) return AG_RS_ERR_INVALID_ARGUMENT;
@@ -2146,6 +2186,12 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   if (n == 0) return AG_RS_OK;
   int st = c->enter();
   if (st) return st;
+  // One pattern for the whole batch (a repair batch; the reference bench's shape): one
+  // pattern word on the host, no per-slice bookkeeping past the strip results.
+  bool uniform = true;
+  for (size_t b = 1; b < n && uniform; ++b)
+    uniform = std::memcmp(dpres, dpres + b * kDataShreds, kDataShreds) == 0 && std::memcmp(cpres, cpres + b * m, m) == 0;
+  if (uniform) return coder_deshred_uniform(c, m, n, S, cw, cw_stride, dpres, cpres, mode, out);
   // Per-slice patterns of RegularShredder's 32:32 on whole-chunk shreds (the follower's
   // random arrival): one 64-bit present mask per slice goes to the device, and the window
   // patterns, locator constants, per-lane decode, padding strip and re-encode run there
