@@ -138,18 +138,14 @@ __device__ __forceinline__ void mul_rt_poly(uint32_t* x, uint32_t coef) {
 // x <- c x for a wave-uniform runtime constant c (polynomial basis, as mul_rt_poly): the same
 // Horner scheme with the coefficient bits tested on the scalar unit, so a clear bit costs no
 // vector work (~45 XORs of doublings + 16 per set bit + the two basis changes, against
-// mul_rt_poly's 16 masked XORs per bit).  Starts at the highest set bit.
+// mul_rt_poly's 16 masked XORs per bit).
 __device__ __forceinline__ void mul_rt_poly_u(uint32_t* x, uint32_t coef) {
-  const uint32_t c = __builtin_amdgcn_readfirstlane(coef) & 0xFFFFu;
-  if (c == 0) {
-    static_for<16>([&](auto P) { x[decltype(P)::value] = 0; });
-    return;
-  }
+  const uint32_t c = __builtin_amdgcn_readfirstlane(coef);
   uint32_t X[16], acc[16];
   basis_apply<0>(x, X);
-  static_for<16>([&](auto P) { acc[decltype(P)::value] = X[decltype(P)::value]; });
-  const int top = 31 - __builtin_clz(c);
-  for (int i = top - 1; i >= 0; --i) {  // wave-uniform trip count and branches
+  static_for<16>([&](auto P) { acc[decltype(P)::value] = ((c >> 15) & 1) ? X[decltype(P)::value] : 0u; });
+  static_for<15>([&](auto I) {  // unrolled: every index static (a runtime loop sent x to scratch)
+    constexpr int i = 14 - decltype(I)::value;
     const uint32_t t = acc[15];
     static_for<15>([&](auto P) {
       constexpr int q = 15 - decltype(P)::value;  // 15 .. 1
@@ -160,7 +156,7 @@ __device__ __forceinline__ void mul_rt_poly_u(uint32_t* x, uint32_t coef) {
     acc[3] ^= t;
     acc[5] ^= t;
     if ((c >> i) & 1) static_for<16>([&](auto P) { acc[decltype(P)::value] ^= X[decltype(P)::value]; });
-  }
+  });
   basis_apply<1>(acc, x);
 }
 

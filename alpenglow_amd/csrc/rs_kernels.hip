@@ -880,8 +880,14 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
 // under that group's masks.  Otherwise each lane loads its own whole chunk (pieces 64 bytes
 // apart in every wave access).
 // =====================================================================================
-template <int OUTH, int PASS, int DIN, int DOUT, bool LL>
+// IO = 2 (UNI, 32 | chunks per shard): one pattern per tile (tiles never straddle blocks: the
+// batch's single pattern, or per-block patterns through block_ids) with lane-linear I/O.  The
+// constants and masks are wave-uniform per lane half, so a slot's product runs on the scalar-
+// branch Horner under the half's exec mask when one half needs it, on the per-lane Horner when
+// both do, and not at all when neither does.
+template <int OUTH, int PASS, int DIN, int DOUT, int IO>
 __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p) {
+  constexpr bool LL = IO >= 1, UNI = IO == 2;
   static_assert(PASS != 0 || (DIN == 0 && DOUT == 0), "the one-pass window starts at 0");
   static_assert(PASS != 2 || DIN == DOUT, "pass 2 loads its output half");
   using LB = X8Lay<2, 1, 3, 4, 5>;
@@ -896,13 +902,24 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   const int h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
-  const uint64_t c0 = static_cast<uint64_t>(tile) * kCols;
+  uint64_t vtile = tile, pat = 0;  // UNI: the tile's place in the batch and its pattern
+  if constexpr (UNI) {
+    if (p.per_block) {
+      const uint64_t bi = tile / p.tiles_per_block;
+      const uint64_t bk = p.block_ids ? p.block_ids[bi] : bi;
+      vtile = bk * p.tiles_per_block + (tile - bi * p.tiles_per_block);
+      pat = bk;
+    }
+  }
+  const uint64_t c0 = vtile * kCols;
   const uint64_t c1 = c0 + kCols - 1 < p.total_columns ? c0 + kCols - 1 : p.total_columns - 1;
   const uint64_t sb0 = c0 / p.chunks_per_shard;
-  {
+  if constexpr (!UNI) {
     const uint32_t nbt = static_cast<uint32_t>(c1 / p.chunks_per_shard - sb0 + 1);  // <= 32
     for (uint32_t i = threadIdx.x; i < nbt * W; i += blockDim.x) lcoef[i] = p.rows[(sb0 + i / W) * p.rows_w + DIN + i % W];
   }
+  const uint32_t* coefu = p.rows + pat * p.rows_w + DIN;  // UNI: the pattern's constants (uniform)
+  const uint64_t umask_in = UNI ? p.pmask[2 * pat] : 0, umask_out = UNI ? p.pmask[2 * pat + 1] : 0;
   if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
   uint64_t blk, col, in_mask, out_mask;
@@ -920,7 +937,8 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
       const bool ok = gc < p.total_columns;
       gr.blk[g] = ok ? gc / p.chunks_per_shard : sb0;
       gr.col[g] = ok ? gc - gr.blk[g] * p.chunks_per_shard : 0;
-      gr.mask[g] = ok ? p.pmask[2 * gr.blk[g] + word] : 0;
+      if constexpr (UNI) gr.mask[g] = ok ? (word ? umask_out : umask_in) : 0;
+      else gr.mask[g] = ok ? p.pmask[2 * gr.blk[g] + word] : 0;
     });
     return gr;
   };
@@ -940,7 +958,7 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
     in_mask = ok ? p.pmask[2 * blk] : 0;
     out_mask = ok ? p.pmask[2 * blk + 1] : 0;
   }
-  const uint32_t* coef = lcoef + (blk - sb0) * W;
+  const uint32_t* coef = UNI ? coefu : lcoef + (blk - sb0) * W;
   const uint64_t off_r = blk * p.rec_block_stride + col * 64;
   const uint64_t off_o = blk * p.orig_block_stride + col * 64;
   // LL: byte offset of piece q within a shard (rec / orig block strides)
@@ -952,6 +970,19 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   // layout A position of slot t in this lane
   auto posA = [&](int t) -> uint32_t {
     return static_cast<uint32_t>((t & 1) | ((t >> 1) << 1) | (h << 2) | (wave << 3));
+  };
+  // UNI: slot t's product for the halves whose bit of mask m is set (m, the constants and the
+  // choice are wave-uniform)
+  auto mul_u = [&](uint32_t* x, int t, uint64_t m) __attribute__((always_inline)) {  // inlined: a
+    // called closure would put the kernel's locals in scratch
+    const uint32_t j0 = static_cast<uint32_t>(t | (wave << 3)), j1 = j0 | 4u;
+    const bool n0 = (m >> j0) & 1, n1 = (m >> j1) & 1;
+    const uint32_t c0 = __builtin_amdgcn_readfirstlane(coefu[j0]), c1 = __builtin_amdgcn_readfirstlane(coefu[j1]);
+    if (n0 && n1) {
+      dev::mul_rt_poly(x, h ? c1 : c0);
+    } else if (n0 || n1) {
+      if ((h != 0) == n1) dev::mul_rt_poly_u(x, n1 ? c1 : c0);  // the one half that needs it
+    }
   };
   Regs4 r;
   static_for<4>([&](auto T) {
@@ -990,7 +1021,13 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = posA(t);
-    if ((in_mask >> j) & 1) {
+    if constexpr (UNI) {
+      const uint32_t j0 = static_cast<uint32_t>(t | (wave << 3));
+      if (((umask_in >> j0) | (umask_in >> (j0 | 4u))) & 1) {  // wave-uniform
+        dev::planes_from_raw(r[t]);  // absent halves hold zeros
+        mul_u(r[t], t, umask_in);
+      }
+    } else if ((in_mask >> j) & 1) {
       dev::planes_from_raw(r[t]);
       dev::mul_rt_poly(r[t], coef[j]);
     }
@@ -1131,7 +1168,9 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
         }
       }
       if constexpr (PASS != 1) {
-        if (mine_t) dev::mul_rt_poly(r[t], coef[j]);
+        if (mine_t) {
+          if constexpr (UNI) mul_u(r[t], t, umask_out); else dev::mul_rt_poly(r[t], coef[j]);
+        }
       }
       uint32_t v[16];
       static_for<16>([&](auto P) { v[decltype(P)::value] = r[t][decltype(P)::value]; });
@@ -1928,16 +1967,29 @@ static bool use_h8() {
   return on;
 }
 
-// A/B aid: AG_RS_H8_LL=1 runs decode_h8 with lane-linear loads and stores (16 | chunks per
-// shard).  Off by default: measured 14.0-14.1 vs 14.4-14.6 M slices/s on the follower's
-// random-arrival coder batch, 7.6-8.0 vs 7.5-7.6 M CodingOnly (profiles/r03_h8_ll_ab.jsonl) --
-// the per-lane products, not the strided loads, bound this kernel.
-static bool use_h8_ll() {
+// A/B aid: AG_RS_H8U=1 runs one-pattern-per-tile W = 64 decodes on decode_h8 (UNI) instead
+// of decode_x16.
+static bool use_h8u() {
   static const bool on = [] {
-    const char* e = std::getenv("AG_RS_H8_LL");
+    const char* e = std::getenv("AG_RS_H8U");
     return e && e[0] == '1';
   }();
   return on;
+}
+
+// decode_h8 with IO 0 (per-lane patterns, whole-chunk lanes) or 2 (one pattern per tile,
+// lane-linear); 32-column tiles.  The lane-linear per-lane mode (IO 1) measured slower than
+// IO 0 on the follower's batches (14.0-14.1 vs 14.4-14.6 M slices/s, CodingOnly 7.6-8.0 vs
+// 7.5-7.6, profiles/r03_h8_ll_ab.jsonl) and is not launched.
+template <int O, int PS, int DI, int DO>
+static void launch_h8(bool uni, dim3 g, const DecodeXParams& pp, hipStream_t stream) {
+  if constexpr (PS == 0) {  // UNI passes 1 / 2 spill (pass 2: the partial's planes); not built
+    if (uni) {
+      hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO, 2>), g, dim3(512), 0, stream, pp);
+      return;
+    }
+  }
+  hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO, 0>), g, dim3(512), 0, stream, pp);
 }
 
 hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
@@ -1950,19 +2002,26 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
   if (W == 32 && pass == 0) {
     if (pl) hipLaunchKernelGGL((decode_x_kernel<4, true>), grid, dim3(256), 0, stream, p);
     else hipLaunchKernelGGL((decode_x_kernel<4>), grid, dim3(256), 0, stream, p);
-  } else if (W == 64 && pass == 0) {
+    return hipGetLastError();
+  }
+  // decode_h8: per-lane patterns (the caller's ntiles counts 64-column ones: 32-column tiles
+  // over every column), or one pattern per tile on 32-column tiles inside blocks (UNI; per
+  // block: the listed blocks' tiles)
+  const bool uni = W == 64 && !pl && use_h8u() && p.chunks_per_shard % 32 == 0 &&
+                   (!p.per_block || p.chunks_per_shard % 64 == 0);
+  const bool h8 = (pl && use_h8()) || uni;
+  DecodeXParams ph = p;
+  uint64_t t32 = (p.total_columns + 31) / 32;
+  if (uni && p.per_block) {
+    ph.tiles_per_block = p.chunks_per_shard / 32;
+    t32 = ntiles * 2;  // two 32-column tiles per 64-column one, block by block
+  }
+  if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const dim3 g32(static_cast<unsigned>(t32));
+#define AG_H8(O, PS, DI, DO) launch_h8<O, PS, DI, DO>(uni, g32, ph, stream)
+  if (W == 64 && pass == 0) {
     if (p.rows_w != 64) return hipErrorInvalidValue;
-    if (pl && use_h8()) {
-      // 32-column tiles (the caller's ntiles counts 64-column ones)
-      const uint64_t t32 = (p.total_columns + 31) / 32;
-      if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
-      const dim3 g32(static_cast<unsigned>(t32));
-      const bool ll = p.chunks_per_shard % 16 == 0 && use_h8_ll();
-#define AG_H8(O, PS, DI, DO)                                                                   \
-  do {                                                                                        \
-    if (ll) hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO, true>), g32, dim3(512), 0, stream, p); \
-    else hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO, false>), g32, dim3(512), 0, stream, p);   \
-  } while (0)
+    if (h8) {
       if (p.low_rate) AG_H8(0, 0, 0, 0);
       else if (p.chunk == 32) AG_H8(1, 0, 0, 0);
       else AG_H8(-1, 0, 0, 0);
@@ -1975,14 +2034,10 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
     // the originals must lie in one window half: LowRate k <= 64 (half 0); HighRate chunk 64
     // (half 1)
     if (p.rows_w != 128 || (p.low_rate ? p.k > 64 : p.chunk != 64)) return hipErrorInvalidValue;
-    if (pl && use_h8()) {
+    if (h8) {
       // decode_h8 passes (32-column tiles, deferred output multiply): both passes of a decode
       // must come from the same kernel family
-      const uint64_t t32 = (p.total_columns + 31) / 32;
-      if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
-      const dim3 g32(static_cast<unsigned>(t32));
       // LowRate: outputs (originals < 32 when k <= 32) in half 0; HighRate: half 1
-      const bool ll = p.chunks_per_shard % 16 == 0 && use_h8_ll();
       if (p.low_rate && p.k <= 32) {
         if (pass == 1) AG_H8(0, 1, 64, 0);
         else AG_H8(0, 2, 0, 0);
