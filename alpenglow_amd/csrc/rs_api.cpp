@@ -846,7 +846,9 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
     p.chunks_per_shard = static_cast<uint32_t>(S / 64);
     p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
     // all restored originals among shards 0..15: the output-pruned 32-point transform
-    p.out_low_half = npts == 32 && std::all_of(mask.begin(), mask.end(), [](uint64_t w) { return (w >> 16) == 0; });
+    // (64-point: every restored original among shards 0..31, xform_h8's pruned FFT)
+    p.out_low_half = (npts == 32 && std::all_of(mask.begin(), mask.end(), [](uint64_t w) { return (w >> 16) == 0; })) ||
+                     (npts == 64 && std::all_of(mask.begin(), mask.end(), [](uint64_t w) { return (w >> 32) == 0; }));
     const auto kind = npts == 32 ? ag::XformKind::kDecode32 : ag::XformKind::kDecode64;
     if (ag::launch_xform(kind, p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   }

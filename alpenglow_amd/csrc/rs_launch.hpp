@@ -23,7 +23,7 @@ struct XformParams {
   uint32_t n_out;              // shards 0..n_out-1 may be stored
   uint32_t chunks_per_shard;   // shard_bytes / 64
   uint64_t total_columns;         // nblocks * chunks_per_shard
-  uint32_t out_low_half;          // 32-point decode: every stored shard is < 16 (pruned FFT)
+  uint32_t out_low_half;          // decode: every stored shard is < N / 2 (pruned FFT)
 };
 
 enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };

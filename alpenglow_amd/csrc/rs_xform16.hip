@@ -119,7 +119,10 @@ __global__ __launch_bounds__(1024, 4) void xform16_kernel(const XformParams p) {
 //   D  slots p4 p3 | h p0 | waves p1 p2 p5   IFFT b4 / FFT b3
 //   E  slots p4 p5 | h p0 | waves p1 p2 p3   IFFT b5, FFT b5 b4
 // =====================================================================================
-template <int DIN, int DOUT>
+// HALF: every stored shard is < 32 (position bit 5 clear; a reconstruct whose erased originals
+// all lie in shards 0..31): after FFT layer 4 the waves whose slots would hold p5 = 1 hand
+// over their live slots and retire (decode_h8's OUTH pruning).
+template <int DIN, int DOUT, bool HALF = false>
 __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
   using LB = X8Lay<2, 1, 3, 4, 5>;
   using LC = X8Lay<2, 3, 1, 4, 5>;
@@ -173,7 +176,34 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
   // FFT_64 (skew delta DOUT), ending in A
   x8_layer_t<LE, 5, false, DOUT>(wave, r);
   x8_layer_t<LE, 4, false, DOUT>(wave, r);
-  x8_swap<1, 2, 4>(wave, lane, lds, &flags, r);
+  if constexpr (!HALF) {
+    x8_swap<1, 2, 4>(wave, lane, lds, &flags, r);
+  } else {
+    // E -> D: slot bit 1 (p5) <-> wave bit 2 (p3).  After it a wave's slots all have p5 = its
+    // wave bit 2; the waves of the p5 = 1 half only send the slots their live partner needs.
+    const int partner = wave ^ 4;
+    if ((wave >> 2) & 1) {
+      x8_wait_ge(&flags.done[partner], 3);
+      static_for<4>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        if constexpr (((t >> 1) & 1) == 0) {
+          lds_put(lds, 2 * partner + (t & 1), lane, r[t]);
+          __asm__ volatile("; xh8 put %0" ::"n"(t));
+        }
+      });
+      x8_signal(&flags.ready[wave], 4, lane);
+      return;
+    }
+    x8_wait_ge(&flags.ready[partner], 4);
+    static_for<4>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      if constexpr (((t >> 1) & 1) != 0) {
+        lds_get(lds, 2 * wave + (t & 1), lane, r[t]);
+        __asm__ volatile("; xh8 get %0" ::"n"(t));
+      }
+    });
+    x8_signal(&flags.done[wave], 4, lane);
+  }
   x8_layer_t<LD, 3, false, DOUT>(wave, r);
   x8_swap<0, 1, 5>(wave, lane, lds, &flags, r);
   x8_layer_t<LC, 2, false, DOUT>(wave, r);
@@ -242,6 +272,8 @@ hipError_t launch_xform16(unsigned din, unsigned dout, const XformParams& p, hip
     if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
     const dim3 g32(static_cast<unsigned>(t32));
     if (din == 64 && dout == 0) hipLaunchKernelGGL((xform_h8_kernel<64, 0>), g32, dim3(512), 0, stream, p);
+    else if (din == 0 && dout == 64 && p.out_low_half && xform_variant() != 5)
+      hipLaunchKernelGGL((xform_h8_kernel<0, 64, true>), g32, dim3(512), 0, stream, p);
     else if (din == 0 && dout == 64) hipLaunchKernelGGL((xform_h8_kernel<0, 64>), g32, dim3(512), 0, stream, p);
     else if (din == 0 && dout == 128) hipLaunchKernelGGL((xform_h8_kernel<0, 128>), g32, dim3(512), 0, stream, p);
     else if (din == 0 && dout == 192) hipLaunchKernelGGL((xform_h8_kernel<0, 192>), g32, dim3(512), 0, stream, p);

@@ -235,19 +235,20 @@ def test_transform64_kernel_variants(ctx, dev, variant):
         lib.ag_rs_internal_set_xform_variant(0)
 
 
-@pytest.mark.parametrize("k,S", [(32, 2048), (64, 2048), (64, 1024)])
-def test_repeated_per_block_mask_reconstructs(ctx, dev, k, S):
+@pytest.mark.parametrize("k,S,low", [(32, 2048, False), (64, 2048, False), (64, 1024, False), (64, 2048, True)])
+def test_repeated_per_block_mask_reconstructs(ctx, dev, k, S, low):
     """Full-recovery reconstructs with a random store mask per block, repeated: an earlier
     64-point kernel skipped whole lane classes' stores in 14-45 % of such calls (timing
     dependent), which single calls rarely caught."""
     m, n = k, 64
-    rng = random.Random(k * 7 + S)
+    rng = random.Random(k * 7 + S + low)
     blocks = np.stack([np.frombuffer(o.block_bytes(4200 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
     d_rec = to_dev(ro_c.encode_blocks(blocks, m, threads=8).reshape(n, m * S), dev)
+    span = k // 2 if low else k  # low: every erasure in the lower half (the pruned-FFT kernels)
     for it in range(12):
         opa = np.ones((n, k), np.uint8)
         for b in range(n):
-            opa[b, rng.sample(range(k), rng.randrange(1, k))] = 0
+            opa[b, rng.sample(range(span), rng.randrange(1, span))] = 0
         damaged = blocks.copy()
         damaged[opa == 0] = 0x5A
         d_o = to_dev(damaged.reshape(n, k * S), dev)
