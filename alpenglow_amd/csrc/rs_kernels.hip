@@ -885,6 +885,9 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
 // constants and masks are wave-uniform per lane half, so a slot's product runs on the scalar-
 // branch Horner under the half's exec mask when one half needs it, on the per-lane Horner when
 // both do, and not at all when neither does.
+#ifndef AG_H8_PAIRDER
+#define AG_H8_PAIRDER 1
+#endif
 template <int OUTH, int PASS, int DIN, int DOUT, int IO>
 __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p) {
   constexpr bool LL = IO >= 1, UNI = IO == 2;
@@ -1044,12 +1047,34 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   x8_swap<1, 2, 3>(wave, lane, lds, &flags, r);
   x8_layer_t<LE, 5, true, DIN>(wave, r);
   // formal derivative in E (slot t: p4 = t & 1, p5 = t >> 1; lane half p0; waves p1 p2 p3);
-  // PASS 2: P = the derivative without its self term; PASS 1: none
+  // PASS 2: P = the derivative without its self term; PASS 1: none.  Each wave publishes its
+  // two pre-derivative slots of round rho in its own region (its swap inbox); the waves with
+  // a wave bit b clear add the region of their partner w | 2^b.  AG_H8_PAIRDER: the regions
+  // are handed over by the epoch flags of the swaps (ready = published, done = this wave's
+  // reads finished; a region is rewritten once every reader of its last epoch is done)
+  // instead of workgroup barriers.  Epochs: swaps 1-3, derivative rounds 4-5, swaps 6-8.
+  constexpr int D = (PASS != 1 && AG_H8_PAIRDER) ? 2 : 0;  // FFT swap epochs 4 + D ..
+  // the readers of region x in a derivative round: x with one of its set wave bits cleared
+  auto wait_readers = [&](int x, uint32_t e) __attribute__((always_inline)) {
+    static_for<3>([&](auto Bb) {
+      constexpr int b = decltype(Bb)::value;
+      if ((x >> b) & 1) x8_wait_ge(&flags.done[x & ~(1 << b)], e);
+    });
+  };
   if constexpr (PASS != 1) {
+#if !AG_H8_PAIRDER
   __syncthreads();  // every wave's swap reads are done: the exchange buffer is free
+#endif
   static_for<2>([&](auto Rho) {
     constexpr int rho = decltype(Rho)::value;
+#if AG_H8_PAIRDER
+    constexpr uint32_t e = 4 + rho;
+    if constexpr (rho == 1) wait_readers(wave, e - 1);  // round 0's readers of this region
+#endif
     static_for<2>([&](auto U) { lds_put(lds, 2 * wave + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+#if AG_H8_PAIRDER
+    x8_signal(&flags.ready[wave], e, lane);
+#endif
     static_for<2>([&](auto U) {
       constexpr int t = 2 * rho + decltype(U)::value;
       // p0 term: the lower half (p0 clear) adds the upper half's pre-derivative value
@@ -1073,28 +1098,39 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
         dev::xor_planes(r[t], hi);
       }
     });
+#if !AG_H8_PAIRDER
     __syncthreads();
+#endif
     static_for<3>([&](auto Bb) {
       constexpr int b = decltype(Bb)::value;
       if (!((wave >> b) & 1)) {
         const int pw = wave | (1 << b);
+#if AG_H8_PAIRDER
+        x8_wait_ge(&flags.ready[pw], e);
+#endif
         static_for<2>([&](auto U) { lds_get_xor(lds, 2 * pw + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
       }
     });
+#if AG_H8_PAIRDER
+    x8_signal(&flags.done[wave], e, lane);
+#else
     __syncthreads();
+#endif
   });
   }
-  // FFT_64 (skew delta DOUT), ending in A
+  // FFT_64 (skew delta DOUT), ending in A.  The first swap writes the partner's region: its
+  // last derivative round's readers must be done with it.
   x8_layer_t<LE, 5, false, DOUT>(wave, r);
   x8_layer_t<LE, 4, false, DOUT>(wave, r);
+  if constexpr (D != 0) wait_readers(wave ^ 4, 5);
   if constexpr (OUTH < 0) {
-    x8_swap<1, 2, 4>(wave, lane, lds, &flags, r);
+    x8_swap<1, 2, 4 + D>(wave, lane, lds, &flags, r);
   } else {
     // E -> D: slot bit 1 (p5) <-> wave bit 2 (p3).  After it a wave's slots all have p5 =
     // its wave bit 2; the other half's waves only send the slots the live partner needs.
     const int partner = wave ^ 4;
     if (((wave >> 2) & 1) != OUTH) {
-      x8_wait_ge(&flags.done[partner], 3);
+      x8_wait_ge(&flags.done[partner], 3 + D);
       static_for<4>([&](auto T) {
         constexpr int t = decltype(T)::value;
         if constexpr (((t >> 1) & 1) == (OUTH > 0 ? 1 : 0)) {
@@ -1102,10 +1138,10 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
           __asm__ volatile("; h8 put %0" ::"n"(t));
         }
       });
-      x8_signal(&flags.ready[wave], 4, lane);
+      x8_signal(&flags.ready[wave], 4 + D, lane);
       return;
     }
-    x8_wait_ge(&flags.ready[partner], 4);
+    x8_wait_ge(&flags.ready[partner], 4 + D);
     static_for<4>([&](auto T) {
       constexpr int t = decltype(T)::value;
       if constexpr (((t >> 1) & 1) != (OUTH > 0 ? 1 : 0)) {
@@ -1113,12 +1149,12 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
         __asm__ volatile("; h8 get %0" ::"n"(t));
       }
     });
-    x8_signal(&flags.done[wave], 4, lane);
+    x8_signal(&flags.done[wave], 4 + D, lane);
   }
   x8_layer_t<LD, 3, false, DOUT>(wave, r);
-  x8_swap<0, 1, 5>(wave, lane, lds, &flags, r);
+  x8_swap<0, 1, 5 + D>(wave, lane, lds, &flags, r);
   x8_layer_t<LC, 2, false, DOUT>(wave, r);
-  x8_swap<1, 0, 6>(wave, lane, lds, &flags, r);
+  x8_swap<1, 0, 6 + D>(wave, lane, lds, &flags, r);
   x8_layer_t<LB, 1, false, DOUT>(wave, r);
   Groups gout{};
   if constexpr (LL) {
