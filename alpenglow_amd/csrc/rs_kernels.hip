@@ -1820,12 +1820,13 @@ __device__ __forceinline__ void store16_a2(uint8_t* dst, uint4 v) {
 // sizes are even, so the crate-layout side is at least 2-byte aligned when its strides
 // are even); the tail chunk and odd strides go byte by byte.
 __global__ __launch_bounds__(256) void restride_kernel(const RestrideParams p) {
-  // grid: x = 16-byte pieces of one block (per_block <= 2^31), y = blocks of this launch
+  // one thread per 16-byte piece of the padded layout, flattened over (block, shard, piece):
+  // small tails (4 pieces per shard) fill whole workgroups
   const uint32_t per_shard = p.Sp / 16, per_block = per_shard * p.nshards;
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= per_block) return;
-  const uint64_t b = blockIdx.y + static_cast<uint64_t>(blockIdx.z) * 65535;
+  const uint64_t gid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const uint64_t b = gid / per_block;
   if (b >= p.nblocks) return;
+  const uint32_t r = static_cast<uint32_t>(gid - b * per_block);
   const uint32_t sh = r / per_shard, u = r - sh * per_shard;
   const uint32_t q = 16 * u;
   const bool whole = q + 16 <= 64 * (p.S >> 6);
@@ -1877,10 +1878,22 @@ __global__ __launch_bounds__(256) void restride_kernel(const RestrideParams p) {
     if (whole && (reinterpret_cast<uintptr_t>(dst) & 1) == 0) {
       store16_a2(dst + q, v);
     } else {
+      // a tail piece is one run of L <= 16 contiguous destination bytes (the low or high
+      // half of the tail symbols): dword stores when the run is dword-aligned and whole
       const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-      for (int i = 0; i < 16; ++i) {
-        const int64_t o = restride_src(q + i, p.S);
-        if (o >= 0) dst[o] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+      const uint32_t tb = 64 * (p.S >> 6), h = (p.S & 63) >> 1, wq = q - tb;
+      const uint32_t off = wq & 31, start = tb + (wq < 32 ? 0 : h) + off;
+      const uint32_t L = whole ? 16u : (off < h ? min(16u, h - off) : 0u);
+      if (!whole && ((reinterpret_cast<uintptr_t>(dst + start) | L) & 3) == 0) {
+        uint32_t* d4 = reinterpret_cast<uint32_t*>(dst + start);
+#pragma unroll
+        for (uint32_t j = 0; j < 4; ++j)
+          if (4 * j < L) d4[j] = w[j];
+      } else {
+        for (int i = 0; i < 16; ++i) {
+          const int64_t o = restride_src(q + i, p.S);
+          if (o >= 0) dst[o] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+        }
       }
     }
   }
@@ -2268,10 +2281,9 @@ hipError_t launch_restride(const uint8_t* src, uint64_t src_block_stride, uint64
   p.mask_per_block = mask_per_block ? 1u : 0u;
   const uint64_t per_block = static_cast<uint64_t>(nshards) * (p.Sp / 16);
   if (per_block == 0 || nblocks == 0) return hipSuccess;
-  if (per_block > 0x7FFFFFFFull || nblocks > 65535ull * 65535ull) return hipErrorInvalidValue;
-  const dim3 grid(static_cast<unsigned>((per_block + 255) / 256), static_cast<unsigned>(std::min<uint64_t>(nblocks, 65535)),
-                  static_cast<unsigned>((nblocks + 65534) / 65535));
-  hipLaunchKernelGGL(restride_kernel, grid, dim3(256), 0, stream, p);
+  const uint64_t groups = (per_block * nblocks + 255) / 256;
+  if (per_block > 0x7FFFFFFFull || groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(restride_kernel, dim3(static_cast<unsigned>(groups)), dim3(256), 0, stream, p);
   return hipGetLastError();
 }
 
