@@ -1899,6 +1899,43 @@ __global__ __launch_bounds__(256) void restride_kernel(const RestrideParams p) {
   }
 }
 
+// Unpack of tail-only shards (0 < S < 64: one padded chunk per shard) to an even destination.
+// The workgroup stages its 64 chunks in LDS; then the four threads of a shard write the S
+// destination bytes as aligned dwords, with half-dwords at the two ends.  The per-piece path
+// above falls back to byte stores for every run that starts off a dword: 3 of the 4 runs of
+// a 62-byte tail.
+__global__ __launch_bounds__(256) void unpack_tail_kernel(const RestrideParams p) {
+  __shared__ uint4 chunk[256];
+  const uint32_t t = threadIdx.x, u = t & 3;
+  const uint64_t g = (static_cast<uint64_t>(blockIdx.x) * 256 + t) >> 2;  // (block, shard)
+  const uint64_t b = g / p.nshards;
+  const uint32_t sh = static_cast<uint32_t>(g - b * p.nshards);
+  const bool sel = b < p.nblocks && (!p.mask || ((p.mask[p.mask_per_block ? b : 0] >> sh) & 1));
+  if (sel)
+    chunk[t] = *reinterpret_cast<const uint4*>(p.src + b * p.src_block_stride + sh * p.src_shard_stride + 16 * u);
+  __syncthreads();
+  if (!sel) return;
+  const uint8_t* c = reinterpret_cast<const uint8_t*>(chunk + (t & ~3u));
+  const int32_t T = static_cast<int32_t>(p.S), h = T >> 1;
+  uint8_t* a = p.dst + b * p.dst_block_stride + sh * p.dst_shard_stride;
+  const int32_t lead = static_cast<int32_t>(reinterpret_cast<uintptr_t>(a) & 3);  // 0 or 2
+  uint8_t* a0 = a - lead;
+  const int32_t nd = (lead + T + 3) >> 2;
+  for (int32_t j = static_cast<int32_t>(u); j < nd; j += 4) {
+    const int32_t i0 = 4 * j - lead;  // destination byte of the dword's first byte
+    uint32_t x = 0;
+#pragma unroll
+    for (int32_t s = 0; s < 4; ++s) {
+      // destination byte i: the low symbol bytes (padded 0..h-1), then the high (32..)
+      const int32_t i = i0 + s;
+      if (i >= 0 && i < T) x |= static_cast<uint32_t>(c[i < h ? i : 32 + i - h]) << (8 * s);
+    }
+    if (i0 >= 0 && i0 + 4 <= T) *reinterpret_cast<uint32_t*>(a0 + 4 * j) = x;
+    else if (i0 < 0) *reinterpret_cast<uint16_t*>(a0 + 4 * j + 2) = static_cast<uint16_t>(x >> 16);
+    else *reinterpret_cast<uint16_t*>(a0 + 4 * j) = static_cast<uint16_t>(x);
+  }
+}
+
 // Per slice: payload length after stripping the bit padding (trailing zeros, then a 0x80
 // marker), or -1 when the padding is invalid.  One workgroup per slice.
 // Padding strip (reed_solomon.rs:191-203): the last non-zero byte of the data region must
@@ -2283,6 +2320,16 @@ hipError_t launch_restride(const uint8_t* src, uint64_t src_block_stride, uint64
   if (per_block == 0 || nblocks == 0) return hipSuccess;
   const uint64_t groups = (per_block * nblocks + 255) / 256;
   if (per_block > 0x7FFFFFFFull || groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  // tail-only unpack to an even destination (S even: the sizes are whole symbols)
+  static const bool lds_tail = [] {
+    const char* e = std::getenv("AG_RS_TAIL_PIECES");  // A/B: 1 = the per-piece path
+    return !(e && e[0] == '1');
+  }();
+  if (lds_tail && unpack && S > 0 && S < 64 && S % 2 == 0 &&
+      ((reinterpret_cast<uintptr_t>(dst) | dst_block_stride | dst_shard_stride) & 1) == 0) {
+    hipLaunchKernelGGL(unpack_tail_kernel, dim3(static_cast<unsigned>(groups)), dim3(256), 0, stream, p);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(restride_kernel, dim3(static_cast<unsigned>(groups)), dim3(256), 0, stream, p);
   return hipGetLastError();
 }
