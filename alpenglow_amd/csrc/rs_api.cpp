@@ -174,6 +174,7 @@ struct ag_rs_ctx {
   DevBuf one_in, one_out;                 // crate-API single codeword
   PinBuf one_pin;                         // its pinned host staging
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
+  std::vector<uint64_t> stage_mask_host;  // last restride masks uploaded to stage_mask
   std::vector<uint64_t> xmask_host;       // last general-decode masks (d_xmask), W = xmask_w
   size_t xmask_w = 0;
   bool xmask_poly = false;                // d_rows holds polynomial-basis constants (per-lane)
@@ -656,9 +657,18 @@ int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t Sv, size_t sstride
     mask[npat + p] = pack_flags(opres + p * k, k);
     mask[2 * npat + p] = rmask ? pack_flags(rpres + p * m, m) : 0;
   }
-  int st = c->stage_mask.ensure(3 * npat * 8, c->stream);
-  if (st) return st;
-  AG_HIP(hipMemcpyAsync(c->stage_mask.ptr, mask.data(), 3 * npat * 8, hipMemcpyHostToDevice, c->stream));
+  // upload only when the masks changed (steady-state batches reuse them, no sync)
+  int st;
+  if (mask != c->stage_mask_host) {
+    AG_HIP(hipStreamSynchronize(c->stream));  // queued restrides / a pending upload may read the old masks
+    if ((st = c->stage_mask.ensure(3 * npat * 8, c->stream))) return st;
+    c->stage_mask_host = std::move(mask);
+    if (hipMemcpyAsync(c->stage_mask.ptr, c->stage_mask_host.data(), 3 * npat * 8, hipMemcpyHostToDevice,
+                       c->stream) != hipSuccess) {
+      c->stage_mask_host.clear();  // never matches a mask set (3 * npat >= 3 words)
+      return AG_RS_ERR_DEVICE;
+    }
+  }
   const uint64_t* d_omask = c->stage_mask.as<uint64_t>() + npat;
   const uint64_t* d_rmask = rmask ? c->stage_mask.as<uint64_t>() + 2 * npat : nullptr;
   const size_t group = std::max<size_t>(1, kRestrideGroupBytes / per_block);
@@ -681,7 +691,6 @@ int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t Sv, size_t sstride
                             c->stream) != hipSuccess)
       return AG_RS_ERR_DEVICE;
   }
-  AG_HIP(hipStreamSynchronize(c->stream));  // the host mask vector goes out of scope
   return AG_RS_OK;
 }
 
