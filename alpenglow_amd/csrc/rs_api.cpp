@@ -1015,7 +1015,11 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
       // the crate's decoder
       if (mode == AG_RS_DECODE_ANY_K) {
         const size_t budget = k - static_cast<size_t>(__builtin_popcountll(ob));
-        while (static_cast<size_t>(__builtin_popcountll(rb)) > budget) rb &= ~(uint64_t{1} << (63 - __builtin_clzll(rb)));
+        // keep the lowest `budget` set bits (one pass over the kept bits: a popcount per
+        // dropped bit cost ~40 ns per pattern, 5 ms per 131 072-pattern call)
+        uint64_t keep = 0;
+        for (size_t i = 0; i < budget && rb; ++i, rb &= rb - 1) keep |= rb & (~rb + 1);
+        rb = keep;
       }
       const uint64_t cmask = (uint64_t{1} << xchunk) - 1;  // xchunk <= 32
       uint64_t in, out, e;
