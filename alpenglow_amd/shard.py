@@ -40,6 +40,15 @@ def gather_over_ranks(value: float, dist=None, device=None) -> list:
     return [float(x.item()) for x in out]
 
 
+def verify_over_ranks(ok, dist=None, device=None) -> list:
+    """Every rank's verification verdict, in rank order: True (verified), False (a check
+    failed) or None (not verified).  All ranks receive the whole list, so each can exit
+    non-zero when any rank failed (bench.py: a wrong result on GPU 5 must not exit 0)."""
+    code = -1.0 if ok is None else (1.0 if ok else 0.0)
+    flags = gather_over_ranks(code, dist, device)
+    return [None if f < 0 else bool(f) for f in flags]
+
+
 # ---- the bench's per-rank plan (bench.py; tested under gloo in tests/test_dist.py) ----
 
 SEED_BASE = 0x5EED_A19E_0000_0000  # SURVEY.md §8(d): block b is seeded SEED_BASE + b

@@ -69,6 +69,7 @@ def parse():
                     help="launcher / rank plumbing only (gloo, no GPU call, no kernel): the timed "
                          "steps are empty and the line reports no throughput (tests/test_dist.py)")
     ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--dry-verify-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -112,41 +113,88 @@ def _spawn_ranks(args) -> int:
     return status
 
 
-def _dry_main(args, world: int, rank: int):
-    """The multi-rank harness without a device: gloo group, rank plan, barrier-bracketed
-    empty steps, max-over-ranks wall time, gathered per-rank walls, one JSON line."""
+def _init_rank(args, world: int, rank: int, local: int):
+    """Bind this rank's device, then join the process group (shared by the device and the
+    --dry-device branches).  The device is bound before init_process_group and passed as
+    its device_id, so RCCL's communicator is created on this rank's GPU, never on GPU 0.
+    Returns (dist or None, device or None)."""
     import torch.distributed as dist
 
+    dev = None
+    if not args.dry_device:
+        import torch
+
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
+    if world == 1:
+        return None, dev
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    if args.dry_device:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+    if dist.get_world_size() != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has "
+                         f"{dist.get_world_size()} rank(s)")
+    return dist, dev
+
+
+def _finish(args, d, dev, rank: int, line, ok) -> int:
+    """Shared tail of both branches: every rank's verify verdict is gathered onto every
+    rank (a rank whose blocks came out wrong must not let the job exit 0), rank 0 prints
+    its line with the per-rank verdicts, and every rank returns the exit status: 4 when
+    any rank failed its verification, else 0."""
+    from alpenglow_amd.shard import verify_over_ranks
+
+    flags = verify_over_ranks(ok, d, dev)
+    failed = [r for r, f in enumerate(flags) if f is False]
+    if rank == 0:
+        if line.get("verify") is not None or any(f is not None for f in flags):
+            line["verify"] = dict(line.get("verify") or {}, per_rank=flags, all_ranks_ok=not failed)
+        print(json.dumps(line), flush=True)
+    if failed and rank == 0:
+        print(f"bench.py: verification failed on rank(s) {failed}", file=sys.stderr, flush=True)
+    return 4 if failed else 0
+
+
+def _dry_main(args, world: int, rank: int, local: int) -> int:
+    """The multi-rank harness without a device: gloo group, rank plan, barrier-bracketed
+    empty steps, max-over-ranks wall time, gathered per-rank walls, the verify aggregation
+    and exit status of the device branch (_finish), one JSON line."""
     from alpenglow_amd.shard import RankPlan, gather_over_ranks, max_over_ranks
 
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+    d, _ = _init_rank(args, world, rank, local)
     if rank == args.dry_fail_rank:
         raise SystemExit(3)
     plan = RankPlan(rank, world, args.nblocks, args.stream_blocks)
-    if world > 1:
-        dist.barrier()
+    if d:
+        d.barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         pass
-    if world > 1:
-        dist.barrier()
+    if d:
+        d.barrier()
     wall = time.perf_counter() - t0
-    d = dist if world > 1 else None
     wall_max = max_over_ranks(wall, d)
     walls = gather_over_ranks(wall, d)
     firsts = gather_over_ranks(plan.first, d)
+    # a rank's "verification" here is only the flag the test asks for (--dry-verify-fail-rank)
+    ok = None if args.no_verify else rank != args.dry_verify_fail_rank
+    line = None
     if rank == 0:
-        print(json.dumps({
+        line = {
             "metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": wall_max * 1e3 / max(args.steps, 1), "higher_is_better": True,
             "scaling": plan.scaling, "vs_baseline": None, "dry_device": True,
             "ranks": {"backend": "gloo" if world > 1 else None, "world_size": world, "wall_s": walls,
                       "first_block": [int(f) for f in firsts], "blocks_per_rank": plan.nblocks},
             "config": {"workload": _workload(args, world, plan.nblocks)},
-        }), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
+            "verify": None,
+        }
+    status = _finish(args, d, None, rank, line, ok)
+    if d:
+        d.destroy_process_group()
+    return status
 
 
 METRIC = "GiB/s device-resident RS shred encode+reconstruct, batched 1 MiB blocks"
@@ -177,17 +225,12 @@ def main():
     if world != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if args.dry_device:
-        return _dry_main(args, world, rank)
+        sys.exit(_dry_main(args, world, rank, local))
     import torch
-    import torch.distributed as dist
 
     from alpenglow_amd import rs
 
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    dist, dev = _init_rank(args, world, rank, local)
 
     from alpenglow_amd.shard import RankPlan, erasure_patterns, gather_over_ranks, max_over_ranks
 
@@ -204,8 +247,6 @@ def main():
     cw_stride = (k + m) * S
 
     ctx = rs.Context(local)
-    if os.environ.get("AG_XFORM_VARIANT"):  # A/B aid (tools/ab_xform.py variants); 0 = default
-        rs.load().ag_rs_internal_set_xform_variant(int(os.environ["AG_XFORM_VARIANT"]))
     stream = torch.cuda.Stream(dev)  # explicit stream: torch work, kernels and events share it
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
@@ -227,7 +268,7 @@ def main():
 
     def barrier():
         torch.cuda.synchronize()
-        if world > 1:
+        if dist:
             dist.barrier()
         torch.cuda.synchronize()
 
@@ -260,13 +301,13 @@ def main():
     enc_ms = sum(ev[s][0].elapsed_time(ev[s][1]) for s in range(args.steps)) / args.steps
     dec_ms = sum(ev[s][1].elapsed_time(ev[s][2]) for s in range(args.steps)) / args.steps
 
-    wall_max = max_over_ranks(wall, dist if world > 1 else None, dev)
-    walls = gather_over_ranks(wall, dist if world > 1 else None, dev)
+    wall_max = max_over_ranks(wall, dist, dev)
+    walls = gather_over_ranks(wall, dist, dev)
     ms_per_step = wall_max * 1e3 / args.steps
 
     # full-size property check: zero the erased shards, reconstruct, compare with a fresh
     # regeneration of the data; and a 2-block bit-exact spot check of the parity vs oracle
-    verify = None
+    verify, ok = None, None
     if not args.no_verify:
         # zero every shred the decoder is told is absent (erased data AND lost coding), so a
         # decoder that read an absent shred could not pass
@@ -282,6 +323,7 @@ def main():
         del ref
         encode()  # restore the zeroed coding shreds for the CPU baseline's parity comparison
         verify = {"reconstruct_restores_all_blocks": ok_rec}
+        ok = ok_rec
 
     line = None
     if rank == 0:
@@ -312,8 +354,8 @@ def main():
             "vs_baseline": None,
             "dtype": "u8 (GF(2^16) symbols, bitsliced u32 planes)",
             "data": "synthetic (splitmix64 random blocks, device-generated)",
-            "ranks": {"backend": "nccl (RCCL)" if world > 1 else None,
-                      "world_size": dist.get_world_size() if world > 1 else 1,
+            "ranks": {"backend": "nccl (RCCL)" if dist else None,
+                      "world_size": dist.get_world_size() if dist else 1,
                       "wall_s": walls, "blocks_per_rank": n},
             "config": {"workload": _workload(args, world, n, e, lc),
                        "blocks_per_gpu": n, "block_bytes": B, "shard_bytes": S,
@@ -329,20 +371,21 @@ def main():
                                    / HBM_PEAK_GBPS) if (enc_ms + dec_ms) else None,
             "verify": verify,
         }
-    if world > 1:
-        dist.barrier()
     # CPU baseline (rank 0, N = 1 only) on a bounded sample of the same blocks
     if rank == 0:
         if world == 1 and not args.no_cpu_baseline:
             line["cpu_baseline"] = _cpu_baseline(args, cw, k, m, S, e)
+            ok = ok is not False and line["cpu_baseline"]["gpu_parity_matches_cpu"]
         else:
             line["cpu_baseline"] = None
         if args.pcie and world == 1:
             line["pcie_inclusive"] = _pcie(args, ctx, cw, k, m, S, e, torch, dev)
-        print(json.dumps(line), flush=True)
+            ok = ok is not False and line["pcie_inclusive"]["matches_device_result"]
+    status = _finish(args, dist, dev, rank, line, ok)
     ctx.close()
-    if world > 1:
+    if dist:
         dist.destroy_process_group()
+    sys.exit(status)
 
 
 def _settle(step, stream, torch, max_steps=200, min_steps=3, tol=0.01, window=4):

@@ -162,6 +162,37 @@ def test_bench_launcher_world2(extra, firsts):
     assert line["n_gpus"] == 2 and line["ranks"]["world_size"] == 2 and line["ranks"]["backend"] == "gloo"
     assert len(line["ranks"]["wall_s"]) == 2 and line["ranks"]["first_block"] == firsts
     assert line["scaling"] == ("strong" if extra else "weak")
+    assert line["verify"]["per_rank"] == [True, True] and line["verify"]["all_ranks_ok"] is True
+
+
+@pytest.mark.parametrize("bad", [0, 1])
+def test_bench_verify_aggregated_over_ranks(bad):
+    """A rank whose verification fails (rank 1 here stands for GPUs 1-7, whose own checks
+    rank 0 never sees) makes the whole job exit non-zero, and rank 0's line names it: the
+    flags are all-gathered by the same _finish the device branch runs."""
+    r = _bench("--gpus", "2", "--dry-device", "--steps", "1", "--dry-verify-fail-rank", str(bad))
+    assert r.returncode == 4, (r.returncode, r.stderr)
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    v = json.loads(lines[0])["verify"]
+    assert v["all_ranks_ok"] is False
+    assert v["per_rank"] == [i != bad for i in range(2)]
+    assert f"verification failed on rank(s) [{bad}]" in r.stderr
+
+
+def test_bench_no_verify_reports_unverified():
+    r = _bench("--gpus", "2", "--dry-device", "--steps", "1", "--no-verify")
+    assert r.returncode == 0, r.stderr
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert line["verify"] is None
+
+
+def test_verify_over_ranks_single():
+    from alpenglow_amd.shard import verify_over_ranks
+
+    assert verify_over_ranks(True) == [True]
+    assert verify_over_ranks(False) == [False]
+    assert verify_over_ranks(None) == [None]
 
 
 def test_bench_launcher_fails_loudly():
