@@ -27,8 +27,8 @@ ARCH = "gfx950"
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc" if os.path.exists("/opt/rocm/bin/hipcc") else "hipcc")
 CXX = os.environ.get("CXX_HOST", "g++")
 
-SOURCES = ["rs_kernels.hip", "rs_xform16.hip", "rs_decode_c.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hip", "slice.hip", "shredder.hip", "rs_api.cpp", "gf16.cpp"]
-HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_xform.hpp", "rs_launch.hpp", "rs_consts.inc", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp", "slice.hpp", "shredder.hpp"]
+SOURCES = ["rs_kernels.hip", "rs_xform64.hip", "rs_decode_c.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hip", "slice.hip", "shredder.hip", "rs_api.cpp", "rs_patterns.cpp", "gf16.cpp"]
+HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_xform.hpp", "rs_launch.hpp", "rs_consts.inc", "rs_patterns.hpp", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp", "slice.hpp", "shredder.hpp"]
 # -fno-slp-vectorize: the SLP vectoriser packs the bitsliced XOR networks into <2 x i32>
 # ops, which lengthens live ranges (measured +40 VGPRs on the transform kernel).
 # -amdgpu-promote-alloca-to-vector-limit: keeps the four-Russians tables of decode_x and
@@ -95,7 +95,7 @@ def build(force: bool = False) -> str:
         obj = os.path.join(OBJDIR, s + ".o")
         objs.append(obj)
         deps = [os.path.join(CSRC, h) for h in _deps(s)] + [os.path.join(INCLUDE, "alpenglow_rs.h")]
-        limit = 2048 if s in ("rs_kernels.hip", "rs_xform16.hip", "rs_decode_c.hip") else 512
+        limit = 2048 if s in ("rs_kernels.hip", "rs_xform64.hip", "rs_decode_c.hip") else 512
         cmd = [HIPCC, *HIP_FLAGS, "-mllvm", f"-amdgpu-promote-alloca-to-vector-limit={limit}", "-c", src, "-o", obj]
         # the stamp holds the full compile command: a flag change (AG_RS_EXTRA_HIPFLAGS
         # diagnostics, the promote-alloca limit) rebuilds the object even when no file changed

@@ -35,7 +35,7 @@ __global__ __launch_bounds__(64) void ed_init_kernel(int32_t* table) {
 }
 
 // WPE: waves per SIMD the register budget is sized for (1: 313 VGPRs, no spills; 2: 256
-// VGPRs, 48 spilled; 3: 168, 220 spilled) -- AG_ED_VERIFY_WPE selects one at run time for A/B.
+// VGPRs, 48 spilled; 3: 168, 220 spilled); 2 is launched (kVerifyWpe).
 template <int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE, WPE))) void ed_verify_kernel(
     const EdVerifyParams p) {
@@ -120,13 +120,7 @@ hipError_t launch_ed25519_init(int32_t* base_table, hipStream_t stream) {
 hipError_t launch_ed25519_verify(const EdVerifyParams& p, hipStream_t stream) {
   if (p.n == 0) return hipSuccess;
   if ((p.n + 63) / 64 > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  static const int wpe = [] {
-    const char* e = std::getenv("AG_ED_VERIFY_WPE");
-    return e ? std::atoi(e) : kVerifyWpe;
-  }();
-  if (wpe == 3) hipLaunchKernelGGL(ed_verify_kernel<3>, grid_for(p.n, 64), dim3(64), 0, stream, p);
-  else if (wpe == 2) hipLaunchKernelGGL(ed_verify_kernel<2>, grid_for(p.n, 64), dim3(64), 0, stream, p);
-  else hipLaunchKernelGGL(ed_verify_kernel<1>, grid_for(p.n, 64), dim3(64), 0, stream, p);
+  hipLaunchKernelGGL(ed_verify_kernel<kVerifyWpe>, grid_for(p.n, 64), dim3(64), 0, stream, p);
   return hipGetLastError();
 }
 

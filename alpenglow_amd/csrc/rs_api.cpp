@@ -27,9 +27,18 @@
 #include "wire.hpp"
 #include "merkle.hpp"
 #include "rs_launch.hpp"
+#include "rs_patterns.hpp"
 #include "shredder.hpp"
 
+using ag::build_corr_pattern;
+using ag::build_syn_pattern;
+using ag::corr_fits;
+using ag::count_flags;
+using ag::gf_invert;
 using ag::next_pow2;
+using ag::pack_flags;
+using ag::window128_masks;
+using ag::window64_masks;
 
 namespace {
 
@@ -149,7 +158,8 @@ struct ag_rs_ctx {
   DevBuf d_flags, d_loc, d_blocks, d_mask;  // decode bookkeeping
   DevBuf d_xmask, d_rows, d_xblocks;        // bitsliced general decode: masks, matrices
   DevBuf d_x128, d_rows128;                 // W = 128 two-pass decode: masks, constants
-  uint64_t last_classes[16] = {};           // patterns per decoder class of the last decode
+  uint64_t last_classes[16] = {};           // patterns per decoder class of the last decode call
+  int decode_depth = 0;                     // decode_device nesting (tail restrides decode inside)
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
   DevBuf d_corr, d_corrk, d_corrblocks;     // correction decoder: patterns, K picks, block ids
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
@@ -180,6 +190,8 @@ struct ag_rs_ctx {
   bool xmask_poly = false;                // d_rows holds polynomial-basis constants (per-lane)
   std::vector<uint8_t> syn_key;             // (k, m, present flags) of the patterns in d_syn
   std::vector<uint8_t> corr_key;            // (k, m, present flags) of the patterns in d_corr
+  std::vector<uint64_t> x128_host;          // last W = 128 masks uploaded to d_x128
+  std::vector<uint32_t> x128_ids;           // their per-block ids (d_xblocks)
 
   int enter() { return hipSetDevice(device) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE; }
 
@@ -264,232 +276,6 @@ constexpr size_t kGenericScratchBytes = size_t{512} << 20;
 
 // Restrided shard buffer (shard sizes that are not whole 64-byte chunks), per group.
 constexpr size_t kRestrideGroupBytes = size_t{2048} << 20;
-
-// Syndrome-decoder pattern (decode_syn_kernel): restore the erased originals from the
-// first e present recovery shards.  Returns false if the e x e system is singular (cannot
-// happen for an MDS code; the caller then takes another decoder).
-bool build_syn_pattern(size_t k, size_t m, const uint8_t* opres, const uint8_t* rpres, const uint16_t* G,
-                       ag::SynPattern* sp) {
-  const ag::Gf16Tables& t = ag::gf16_tables();
-  std::memset(sp, 0, sizeof *sp);
-  size_t e = 0, r = 0;
-  for (size_t i = 0; i < k; ++i) {
-    if (opres[i]) sp->dmask |= uint64_t{1} << i;
-    else if (e < 4) sp->out[e++] = static_cast<uint8_t>(i);
-    else return false;
-  }
-  for (size_t j = 0; j < m && r < e; ++j)
-    if (rpres[j]) sp->rec[r++] = static_cast<uint8_t>(j);
-  if (r < e) return false;
-  sp->e = static_cast<uint32_t>(e);
-  // A[b][a] = G[rec[b]][out[a]]; Gauss-Jordan inverse over GF(2^16)
-  uint16_t A[4][8] = {};
-  for (size_t b = 0; b < e; ++b) {
-    for (size_t a = 0; a < e; ++a) A[b][a] = G[sp->rec[b] * k + sp->out[a]];
-    A[b][e + b] = 1;
-  }
-  for (size_t col = 0; col < e; ++col) {
-    size_t piv = col;
-    while (piv < e && A[piv][col] == 0) ++piv;
-    if (piv == e) return false;
-    if (piv != col)
-      for (size_t x = 0; x < 2 * e; ++x) std::swap(A[piv][x], A[col][x]);
-    const uint16_t inv = ag::gf_inv(t, A[col][col]);
-    for (size_t x = 0; x < 2 * e; ++x) A[col][x] = ag::gf_mul_elem(t, A[col][x], inv);
-    for (size_t row = 0; row < e; ++row) {
-      if (row == col || A[row][col] == 0) continue;
-      const uint16_t f = A[row][col];
-      for (size_t x = 0; x < 2 * e; ++x) A[row][x] ^= ag::gf_mul_elem(t, f, A[col][x]);
-    }
-  }
-  // Minv[a][b] = A[a][e + b]; bitsliced matrix rows[o] bit i = bit o of (Minv * 2^i)
-  for (size_t a = 0; a < e; ++a)
-    for (size_t b = 0; b < e; ++b)
-      for (unsigned i = 0; i < 16; ++i) {
-        const uint16_t prod = ag::gf_mul_elem(t, A[a][e + b], static_cast<uint16_t>(1u << i));
-        for (unsigned o = 0; o < 16; ++o) sp->rows[a][b][o] |= ((prod >> o) & 1u) << i;
-      }
-  return true;
-}
-
-// In-place Gauss-Jordan inverse of an n x n matrix over GF(2^16) (row-major, stride n).
-// Returns false if singular.
-bool gf_invert(size_t n, uint16_t* A) {
-  const ag::Gf16Tables& t = ag::gf16_tables();
-  std::vector<uint16_t> M(n * 2 * n, 0);
-  for (size_t r = 0; r < n; ++r) {
-    for (size_t c = 0; c < n; ++c) M[r * 2 * n + c] = A[r * n + c];
-    M[r * 2 * n + n + r] = 1;
-  }
-  for (size_t col = 0; col < n; ++col) {
-    size_t piv = col;
-    while (piv < n && M[piv * 2 * n + col] == 0) ++piv;
-    if (piv == n) return false;
-    if (piv != col)
-      for (size_t x = 0; x < 2 * n; ++x) std::swap(M[piv * 2 * n + x], M[col * 2 * n + x]);
-    const uint16_t inv = ag::gf_inv(t, M[col * 2 * n + col]);
-    for (size_t x = 0; x < 2 * n; ++x) M[col * 2 * n + x] = ag::gf_mul_elem(t, M[col * 2 * n + x], inv);
-    for (size_t row = 0; row < n; ++row) {
-      const uint16_t f = M[row * 2 * n + col];
-      if (row == col || f == 0) continue;
-      for (size_t x = 0; x < 2 * n; ++x) M[row * 2 * n + x] ^= ag::gf_mul_elem(t, f, M[col * 2 * n + x]);
-    }
-  }
-  for (size_t r = 0; r < n; ++r)
-    for (size_t c = 0; c < n; ++c) A[r * n + c] = M[r * 2 * n + n + c];
-  return true;
-}
-
-// X = the 32-point full-recovery transform as a matrix (d_i = XOR_j X[i][j] * r_j): the
-// inverse of the 32:32 HighRate encoder.  A k < 32 code is the 32:32 code with originals
-// k..31 zero, so the same X serves every k <= 32 with m = 32.
-const uint16_t* full_window_x32() {
-  static const std::vector<uint16_t> X = [] {
-    std::vector<uint16_t> G(32 * 32);
-    ag::hr_generator(32, 32, G.data());
-    if (!gf_invert(32, G.data())) G.clear();  // cannot happen: the encoder is invertible
-    return G;
-  }();
-  return X.empty() ? nullptr : X.data();
-}
-
-// Correction-decoder pattern (decode_c_kernel): HighRate k <= 32, m = 32, lost recovery
-// shards L (1 <= |L| <= kCorrMaxSyn).  Syndrome points: virtual zeros k..31 first (no
-// load), then present originals in index order.  False if the pattern does not fit (the
-// caller takes another decoder).
-// decode_c's balanced correction (rs_decode_c.hip), decided per pattern: layout H0 gives wave
-// w the positions 2w, 16 + 2w, 2w + 1, 17 + 2w (slots 0..3).  Every wave keeps at most
-// quota = ceil(|E| / 8) of its own restored originals (lowest slots first); the surplus, in
-// ascending position order, is dealt to the waves below quota (ascending wave order), which
-// accumulate it in their free slots (ascending slot order) and return the sums through LDS
-// slot = the output's donation rank.
-void corr_assign(ag::CorrPattern* cp) {
-  auto pos = [](uint32_t w, uint32_t t) { return (t & 1 ? 16u : 0u) + 2 * w + (t >> 1); };
-  const uint64_t em = cp->emask;
-  const uint32_t ne = static_cast<uint32_t>(__builtin_popcountll(em & 0xFFFFFFFFull));
-  const uint32_t quota = (ne + 7) >> 3;
-  auto rank = [&](uint64_t m, uint32_t a) {
-    return static_cast<uint32_t>(__builtin_popcountll(m & ((uint64_t{1} << a) - 1)));
-  };
-  uint32_t own[8], donated[8], cap[8];
-  uint64_t dmask = 0;
-  for (uint32_t w = 0; w < 8; ++w) {
-    own[w] = 0;
-    for (uint32_t t = 0; t < 4; ++t)
-      if ((em >> pos(w, t)) & 1) own[w] |= 1u << t;
-    uint32_t m = own[w];
-    for (uint32_t q = 0; q < quota && m; ++q) m &= m - 1;
-    donated[w] = m;
-    for (uint32_t t = 0; t < 4; ++t)
-      if ((m >> t) & 1) dmask |= uint64_t{1} << pos(w, t);
-    const uint32_t c = static_cast<uint32_t>(__builtin_popcount(own[w]));
-    cap[w] = c < quota ? quota - c : 0;
-  }
-  const uint32_t nd = static_cast<uint32_t>(__builtin_popcountll(dmask));
-  uint64_t rem = dmask;
-  uint32_t d = 0;
-  for (uint32_t w = 0; w < 8; ++w) {
-    uint32_t act = 0, foreign = 0;
-    for (uint32_t t = 0; t < 4; ++t) {
-      uint32_t a = 64, lds = 0;
-      if (((own[w] & ~donated[w]) >> t) & 1) {
-        a = pos(w, t);
-      } else if ((donated[w] >> t) & 1) {
-        lds = rank(dmask, pos(w, t));
-      } else if (!((own[w] >> t) & 1) && cap[w] && d < nd) {
-        a = static_cast<uint32_t>(__builtin_ctzll(rem));
-        rem &= rem - 1;
-        lds = d++;
-        --cap[w];
-        foreign |= 1u << t;
-      }
-      uint32_t kofs = 0;
-      if (a < 64) {
-        act |= 1u << t;
-        kofs = ag::kCorrPairWords * rank(em, a) * cp->ns;
-      }
-      cp->wslot[w][t] = kofs | (lds << 20);
-    }
-    cp->wsum[w] = act | (own[w] << 4) | (donated[w] << 8) | (foreign << 12) | ((nd ? 1u : 0u) << 16);
-  }
-}
-
-bool build_corr_pattern(size_t k, const uint8_t* opres, const uint8_t* rpres, ag::CorrPattern* cp,
-                        std::vector<uint32_t>& pool) {
-  const uint16_t* X = full_window_x32();
-  if (!X || k > 32) return false;
-  const ag::Gf16Tables& t = ag::gf16_tables();
-  std::memset(cp, 0, sizeof *cp);
-  uint8_t E[32], L[32], D[32];
-  size_t ne = 0, nl = 0, nd = 0;
-  for (size_t j = 0; j < 32; ++j) {
-    if (rpres[j]) cp->rmask |= uint64_t{1} << j;
-    else L[nl++] = static_cast<uint8_t>(j);
-  }
-  for (size_t i = 0; i < k; ++i)
-    if (!opres[i]) {
-      cp->emask |= uint64_t{1} << i;
-      E[ne++] = static_cast<uint8_t>(i);
-    }
-  if (nl == 0 || nl > static_cast<size_t>(ag::kCorrMaxSyn) || ne == 0 || ne * nl > ag::kCorrMaxPairs) return false;
-  for (size_t i = k; i < 32 && nd < nl; ++i) D[nd++] = static_cast<uint8_t>(i);
-  for (size_t i = 0; i < k && nd < nl; ++i)
-    if (opres[i]) D[nd++] = static_cast<uint8_t>(i);
-  if (nd < nl) return false;  // fewer than k survivors
-  for (size_t b = 0; b < nd; ++b) cp->smask |= uint64_t{1} << D[b];
-  // the syndrome rank b of point D[b] must follow position order (the kernel ranks by popcount)
-  std::sort(D, D + nd);
-  cp->ne = static_cast<uint32_t>(ne);
-  cp->ns = static_cast<uint32_t>(nl);
-  corr_assign(cp);
-  // N = X[D, L], K = X[E, L] N^-1
-  std::vector<uint16_t> N(nl * nl), K(ne * nl, 0);
-  for (size_t b = 0; b < nl; ++b)
-    for (size_t c = 0; c < nl; ++c) N[b * nl + c] = X[D[b] * 32 + L[c]];
-  if (!gf_invert(nl, N.data())) return false;
-  for (size_t a = 0; a < ne; ++a)
-    for (size_t b = 0; b < nl; ++b) {
-      uint16_t acc = 0;
-      for (size_t c = 0; c < nl; ++c) acc ^= ag::gf_mul_elem(t, X[E[a] * 32 + L[c]], N[c * nl + b]);
-      K[a * nl + b] = acc;
-    }
-  // table picks: per pair, group pair gp and output plane o, the two nibbles of row o
-  // (input planes 8gp..8gp+3, 8gp+4..8gp+7); row o bit i = bit o of K * 2^i
-  cp->kofs = pool.size();
-  pool.resize(pool.size() + ne * nl * ag::kCorrPairWords);
-  uint32_t* dst = pool.data() + cp->kofs;
-  for (size_t a = 0; a < ne; ++a)
-    for (size_t b = 0; b < nl; ++b, dst += ag::kCorrPairWords) {
-      uint32_t rows[16] = {};
-      const uint16_t v = K[a * nl + b];
-      for (unsigned i = 0; i < 16; ++i) {
-        const uint16_t prod = ag::gf_mul_elem(t, v, static_cast<uint16_t>(1u << i));
-        for (unsigned o = 0; o < 16; ++o) rows[o] |= ((prod >> o) & 1u) << i;
-      }
-      for (unsigned gp = 0; gp < 2; ++gp)
-        for (unsigned o = 0; o < 16; ++o) {
-          dst[32 * gp + 2 * o] = (rows[o] >> (8 * gp)) & 15u;
-          dst[32 * gp + 2 * o + 1] = (rows[o] >> (8 * gp + 4)) & 15u;
-        }
-    }
-  return true;
-}
-
-// The correction decoder takes a 32:m=32 pattern when 1 <= |L| <= kCorrMaxSyn recovery
-// shards are lost and some original is erased (no = present originals, nr = present
-// recovery shards; no + nr >= k is checked first).
-bool corr_fits(size_t k, size_t no, size_t nr) {
-  const size_t nl = 32 - nr, ne = k - no;
-  return nl >= 1 && nl <= static_cast<size_t>(ag::kCorrMaxSyn) && ne >= 1 && ne * nl <= ag::kCorrMaxPairs;
-}
-// AG_RS_NO_CORR=1 routes those patterns to decode_x instead (A/B timing).
-bool corr_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("AG_RS_NO_CORR");
-    return !(e && e[0] == '1');
-  }();
-  return on;
-}
 
 int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
                   size_t ostride, uint8_t* rec, size_t rstride);
@@ -612,28 +398,6 @@ int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
   return encode_cols(c, k, m, S, S, nblocks, orig, ostride, rec, rstride);
 }
 
-// Host flag arrays (0 / nonzero bytes, one per shard) -> bit masks, 8 flags per step:
-// the per-pattern bookkeeping of a 65 536-slice batch stays well under a millisecond.
-inline uint64_t pack_flags(const uint8_t* f, size_t n) {  // n <= 64
-  uint64_t bits = 0;
-  size_t i = 0;
-  for (; i + 8 <= n; i += 8) {
-    uint64_t x;
-    std::memcpy(&x, f + i, 8);
-    // high bit of each byte <- byte != 0, then gather the 8 high bits (multiply trick)
-    const uint64_t nz = ((((x & 0x7F7F7F7F7F7F7F7Full) + 0x7F7F7F7F7F7F7F7Full) | x) & 0x8080808080808080ull) >> 7;
-    bits |= ((nz * 0x0102040810204080ull) >> 56) << i;
-  }
-  for (; i < n; ++i) bits |= uint64_t{f[i] != 0} << i;
-  return bits;
-}
-inline size_t count_flags(const uint8_t* f, size_t n) {
-  if (n <= 64) return static_cast<size_t>(__builtin_popcountll(pack_flags(f, n)));
-  size_t c = 0;
-  for (size_t i = 0; i < n; ++i) c += f[i] != 0;
-  return c;
-}
-
 int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
                   const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
                   int mode);
@@ -700,9 +464,25 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
                 size_t ostride, const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres,
                 size_t npat, int mode);
 
+int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
+                       const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
+                       int mode);
+
+// last_classes counts every pattern of the outermost call: the whole-chunk decode and the
+// tail restride's inner decode of a shard size with S % 64 != 0 add up (reset once per call)
 int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
                   const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
                   int mode) {
+  if (c->decode_depth == 0) std::fill(std::begin(c->last_classes), std::end(c->last_classes), uint64_t{0});
+  ++c->decode_depth;
+  const int st = decode_device_body(c, k, m, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
+  --c->decode_depth;
+  return st;
+}
+
+int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
+                       const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
+                       int mode) {
   if (nblocks == 0) return AG_RS_OK;
   const bool odd = odd_layout(orig, rec, ostride, rstride);
   if (k <= 64 && (S % 64 != 0 || odd) && S % 2 == 0) {
@@ -776,8 +556,7 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
   // decode_c: the 32-point full-window geometries (HighRate, m = 32, k <= 32) with lost
   // recovery shards; any k survivors, same tiling rule
   const bool corr_geo = mode == AG_RS_DECODE_ANY_K && hr == 1 && m == 32 && k <= 32 && S % 64 == 0 && aligned &&
-                        (npat == 1 || cps % 64 == 0) && static_cast<uint64_t>(nblocks) * cps < (uint64_t{1} << 31) &&
-                        corr_enabled();
+                        (npat == 1 || cps % 64 == 0) && static_cast<uint64_t>(nblocks) * cps < (uint64_t{1} << 31);
   // W = 128 windows as two 64-point passes (decode_x16 PASS 1 / 2): the originals in one
   // window half -- HighRate with next_pow2(m) = 64 (originals at 64..127), LowRate with
   // next_pow2(k) <= 64 and next_pow2(k) + m in (64, 128] (originals at 0..k-1).  Any k
@@ -825,7 +604,6 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
       any_generic = true;
     }
   }
-  std::fill(std::begin(c->last_classes), std::end(c->last_classes), uint64_t{0});
   for (size_t p = 0; p < npat; ++p) ++c->last_classes[cls[p]];
   int st;
   if (any_fast) {
@@ -1005,33 +783,9 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
     std::vector<uint64_t> xm(3 * npat, 0);
     for (size_t p = 0; p < npat; ++p) {
       if (cls[p] != 3) continue;
-      // window positions: HighRate recovery j < xchunk, original i at xchunk + i (xchunk + k
-      // <= 64); LowRate original i at i, recovery j at xchunk + j (j < xm_rec)
-      const uint64_t ob = pack_flags(opres + p * k, k), kmask = (uint64_t{1} << k) - 1;
-      uint64_t rb = pack_flags(rpres + p * m, xm_rec);
-      // ANY_K: exactly k survivors -- the present originals, then recovery shards in index
-      // order; surplus recovery shards count as erased (MDS: any k survivors determine the
-      // originals), so only k input multiplies remain.  EXACT: every present shard, as
-      // the crate's decoder
-      if (mode == AG_RS_DECODE_ANY_K) {
-        const size_t budget = k - static_cast<size_t>(__builtin_popcountll(ob));
-        // keep the lowest `budget` set bits (one pass over the kept bits: a popcount per
-        // dropped bit cost ~40 ns per pattern, 5 ms per 131 072-pattern call)
-        uint64_t keep = 0;
-        for (size_t i = 0; i < budget && rb; ++i, rb &= rb - 1) keep |= rb & (~rb + 1);
-        rb = keep;
-      }
-      const uint64_t cmask = (uint64_t{1} << xchunk) - 1;  // xchunk <= 32
-      uint64_t in, out, e;
-      if (hr == 1) {
-        in = rb | (ob << xchunk);
-        out = (~ob & kmask) << xchunk;
-        e = (~rb & cmask) | out;  // lost / surplus recovery, virtual points m..chunk-1
-      } else {
-        in = ob | (rb << xchunk);
-        out = ~ob & kmask;       // the zero padding k..31 is neither loaded nor erased
-        e = out | ((~rb & cmask) << xchunk);  // lost / surplus recovery, positions past m
-      }
+      uint64_t e, in, out;
+      window64_masks(hr == 1, k, m, xchunk, xm_rec, opres + p * k, rpres + p * m, mode == AG_RS_DECODE_ANY_K, &e, &in,
+                     &out);
       xm[p] = e;
       xm[npat + 2 * p] = in;
       xm[npat + 2 * p + 1] = out;
@@ -1098,50 +852,7 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
     std::vector<uint64_t> xm(10 * npat, 0);
     for (size_t p = 0; p < npat; ++p) {
       if (cls[p] != 8) continue;
-      const uint64_t ob = pack_flags(opres + p * k, k), kmask = k >= 64 ? ~uint64_t{0} : (uint64_t{1} << k) - 1;
-      uint64_t rb[2] = {pack_flags(rpres + p * m, std::min<size_t>(m, 64)), m > 64 ? pack_flags(rpres + p * m + 64, m - 64) : 0};
-      // exactly k survivors: the present originals, then recovery shards in index order
-      size_t budget = k - static_cast<size_t>(__builtin_popcountll(ob));
-      for (int w = 0; w < 2; ++w) {
-        uint64_t keep = 0;
-        for (uint64_t b = rb[w]; b && budget; b &= b - 1, --budget) keep |= b & (~b + 1);
-        rb[w] = keep;
-      }
-      uint64_t in[2], out[2], e[2];
-      if (hr == 1) {  // recovery j at j (j < m <= 64), original i at 64 + i
-        in[0] = rb[0];
-        in[1] = ob;
-        out[0] = 0;
-        out[1] = ~ob & kmask;
-        e[0] = ~rb[0];  // lost / surplus recovery and the virtual points m..63
-        e[1] = out[1];  // positions 64 + k.. are the encoder's zeros, not erasures
-      } else {  // original i at i, zero padding k..c-1, recovery j at c + j, erasures from c + m
-        uint64_t rw[2] = {0, 0}, valid[2] = {0, 0};  // recovery positions in the window
-        for (size_t j = 0; j < m; ++j) {
-          const size_t g = c128 + j;
-          if ((rb[j >> 6] >> (j & 63)) & 1) rw[g >> 6] |= uint64_t{1} << (g & 63);
-          valid[g >> 6] |= uint64_t{1} << (g & 63);
-        }
-        const uint64_t cm = c128 >= 64 ? ~uint64_t{0} : (uint64_t{1} << c128) - 1;  // originals + padding
-        in[0] = ob | rw[0];
-        in[1] = rw[1];
-        out[0] = ~ob & kmask;
-        out[1] = 0;
-        e[0] = out[0] | (~rw[0] & ~cm);  // lost / surplus recovery, positions past c + m
-        e[1] = ~rw[1];
-        (void)valid;
-      }
-      uint64_t* q = &xm[10 * p];
-      q[0] = e[0];
-      q[1] = e[1];
-      q[2] = in[0];
-      q[3] = in[1];
-      q[4] = out[0];
-      q[5] = out[1];
-      q[6] = in[1 - oh];  // pass 1: the other half's inputs
-      q[7] = out[oh];
-      q[8] = in[oh];      // pass 2: the output half's inputs
-      q[9] = out[oh];
+      window128_masks(hr == 1, k, m, c128, opres + p * k, rpres + p * m, &xm[10 * p]);
     }
     // device: m6 [npat][6], pass-1 pairs [npat][2], pass-2 pairs [npat][2]
     std::vector<uint64_t> dev(10 * npat);
@@ -1152,14 +863,23 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
       dev[8 * npat + 2 * p] = xm[10 * p + 8];
       dev[8 * npat + 2 * p + 1] = xm[10 * p + 9];
     }
-    AG_HIP(hipStreamSynchronize(c->stream));  // a previous upload may still be pending
-    if ((st = c->d_x128.ensure(dev.size() * 8, c->stream)) || (st = c->d_rows128.ensure(npat * 128 * 4, c->stream)))
-      return st;
-    AG_HIP(hipMemcpy(c->d_x128.ptr, dev.data(), dev.size() * 8, hipMemcpyHostToDevice));
+    // upload (and rebuild the constants) only when the masks changed; the copy is ordered on
+    // the stream and reads the context's own host vector, so nothing waits for it
+    if (dev != c->x128_host) {
+      AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read x128_host
+      if ((st = c->d_x128.ensure(dev.size() * 8, c->stream)) || (st = c->d_rows128.ensure(npat * 128 * 4, c->stream)))
+        return st;
+      c->x128_host = std::move(dev);
+      if (hipMemcpyAsync(c->d_x128.ptr, c->x128_host.data(), c->x128_host.size() * 8, hipMemcpyHostToDevice,
+                         c->stream) != hipSuccess) {
+        c->x128_host.clear();
+        return AG_RS_ERR_DEVICE;
+      }
+      if (ag::launch_decode_rows128(c->d_x128.as<uint64_t>(), static_cast<uint32_t>(npat), c->dtables(),
+                                    c->d_rows128.as<uint32_t>(), c->stream) != hipSuccess)
+        return AG_RS_ERR_DEVICE;
+    }
     const uint64_t* d6 = c->d_x128.as<uint64_t>();
-    if (ag::launch_decode_rows128(d6, static_cast<uint32_t>(npat), c->dtables(), c->d_rows128.as<uint32_t>(),
-                                  c->stream) != hipSuccess)
-      return AG_RS_ERR_DEVICE;
     ag::DecodeXParams p{};
     p.rec = rec;
     p.rec_block_stride = rstride;
@@ -1188,8 +908,11 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
       for (size_t b = 0; b < nblocks; ++b)
         if (cls[b] == 8) ids.push_back(static_cast<uint32_t>(b));
       if (ids.size() != nblocks) {
+        AG_HIP(hipStreamSynchronize(c->stream));  // a pending id upload may still read x128_ids
         if ((st = c->d_xblocks.ensure(ids.size() * 4, c->stream))) return st;
-        AG_HIP(hipMemcpy(c->d_xblocks.ptr, ids.data(), ids.size() * 4, hipMemcpyHostToDevice));
+        c->x128_ids = std::move(ids);
+        AG_HIP(hipMemcpyAsync(c->d_xblocks.ptr, c->x128_ids.data(), c->x128_ids.size() * 4, hipMemcpyHostToDevice,
+                              c->stream));
         p.block_ids = c->d_xblocks.as<uint32_t>();
       }
       ntiles = static_cast<uint64_t>(ids.size()) * p.tiles_per_block;
@@ -1201,7 +924,6 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
       p.pmask = d6 + (pass == 1 ? 6 : 8) * npat;
       if (ag::launch_decode_x(128, pass, p, ntiles, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
     }
-    AG_HIP(hipStreamSynchronize(c->stream));  // host vectors above are read by the copies
   }
   if (!any_generic) return AG_RS_OK;
 
@@ -1346,16 +1068,29 @@ int ag_rs_ctx_create(int device, ag_rs_ctx** out) {
 
 void ag_rs_ctx_destroy(ag_rs_ctx* c) { delete c; }
 
+// A stream switch first drains the old stream (its queued kernels may still read the cached
+// pattern uploads and scratch) and forgets the upload caches, whose copies were ordered on it.
+static int switch_stream(ag_rs_ctx* c, hipStream_t s) {
+  if (s == c->stream) return AG_RS_OK;
+  if (c->enter() || hipStreamSynchronize(c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  c->stream = s;
+  c->mask_host.clear();
+  c->stage_mask_host.clear();
+  c->xmask_host.clear();
+  c->x128_host.clear();
+  c->syn_key.clear();
+  c->corr_key.clear();
+  return AG_RS_OK;
+}
+
 int ag_rs_ctx_set_stream(ag_rs_ctx* c, void* s) {
   if (!c) return AG_RS_ERR_INVALID_ARGUMENT;
-  c->stream = static_cast<hipStream_t>(s);
-  return AG_RS_OK;
+  return switch_stream(c, static_cast<hipStream_t>(s));
 }
 
 int ag_rs_ctx_reset_stream(ag_rs_ctx* c) {
   if (!c) return AG_RS_ERR_INVALID_ARGUMENT;
-  c->stream = c->own_stream;
-  return AG_RS_OK;
+  return switch_stream(c, c->own_stream);
 }
 
 void* ag_rs_ctx_stream(ag_rs_ctx* c) { return c ? static_cast<void*>(c->stream) : nullptr; }
@@ -2218,16 +1953,16 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   if ((m == kDataShreds || m == 2 * kDataShreds) && S % 64 == 0 && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
     const size_t wps = m == kDataShreds ? 1 : 2;  // present words per slice
     std::vector<uint64_t> pres(wps * n);
-    bool uniform = true, surplus = false;
+    // (uniform batches returned above)
+    bool surplus = false;
     for (size_t b = 0; b < n; ++b) {
       const uint64_t* q = &pres[wps * b];
       pres[wps * b] = pack_flags(dpres + b * kDataShreds, kDataShreds) | (pack_flags(cpres + b * m, 32) << 32);
       if (wps == 2) pres[wps * b + 1] = pack_flags(cpres + b * m + 32, 32);
-      uniform = uniform && std::equal(q, q + wps, pres.data());
       surplus = surplus ||
                 __builtin_popcountll(q[0]) + (wps == 2 ? __builtin_popcountll(q[1]) : 0) > static_cast<int>(kDataShreds);
     }
-    if (!uniform && (mode == AG_RS_DECODE_ANY_K || !surplus)) {
+    if (mode == AG_RS_DECODE_ANY_K || !surplus) {
       if ((st = c->d_present.ensure(wps * n * 8, c->stream))) return st;
       AG_HIP(hipMemcpyAsync(c->d_present.ptr, pres.data(), wps * n * 8, hipMemcpyHostToDevice, c->stream));
       return pipe_coder_deshred(c, n, S, cw, cw_stride, c->d_present.as<uint64_t>(), out, m);  // synchronous
@@ -2673,14 +2408,6 @@ bool pipe_args_ok(size_t nslices, size_t S, const uint8_t* codewords, const uint
 }  // namespace
 
 namespace {
-// A/B aid: AG_PIPE_HOST_CODER=1 keeps the host-pattern coder path (ag_rs_coder_deshred_batch).
-bool pipe_device_coder() {
-  static const bool dev = [] {
-    const char* e = std::getenv("AG_PIPE_HOST_CODER");
-    return !(e && e[0] == '1');
-  }();
-  return dev;
-}
 // ReedSolomonCoder::deshred (reed_solomon.rs:140-208, ANY_K) over the kept shreds of every
 // slice without a host round trip, for whole-chunk shreds (S % 64 == 0): the per-slice
 // patterns come from the kept-shred masks on the device (launch_pipe_patterns), the per-lane
@@ -3042,7 +2769,7 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   // 4. ReedSolomonCoder::deshred over the kept shreds (restores the data shreds, re-encodes
   //    all coding shreds, strips the padding); on the device for whole-chunk shreds
   std::vector<int64_t> plen(n);
-  if (S % 64 == 0 && pipe_device_coder()) {
+  if (S % 64 == 0) {
     if ((st = pipe_coder_deshred(c, n, S, codewords, cw_stride, d_present, plen.data(), kDataShreds))) return st;
   } else {
     std::vector<uint8_t> dp(n * ag::kPipeData), cp(n * (ag::kPipeShreds - ag::kPipeData));

@@ -193,13 +193,8 @@ __device__ __forceinline__ void ifft_bfly(uint32_t* x, uint32_t* y) {
 // neighbours (tools/membench/membench4.hip: 32-shard tile copies 5.18 -> 5.49 TB/s at 64
 // chunks per tile, 5.76 -> 6.20 TB/s at 16).  A bijection on [0, g) for any g.
 __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t g) {
-#ifdef AG_NO_XCD_REMAP
-  (void)g;
-  return b;
-#else
   const uint32_t x = b & 7, q = g >> 3, r = g & 7;
   return x * q + (x < r ? x : r) + (b >> 3);
-#endif
 }
 
 // ---- 8x32 bit transpose (3 delta swaps; an involution) ------------------------------

@@ -87,18 +87,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
 //   H1 slots p4 p1 | waves p0 p2 p3   FFT b1
 //   H0 slots p4 p0 | waves p1 p2 p3   FFT b0, store shards 2w, 2w + 1
 template <int DIN, int DOUT, bool HALF = false>
-__global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const XformParams p) {
+__global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
   __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
   __shared__ X8Flags flags;
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-#if AG_X8_PRIO  // A/B: static priority for the second-dispatched half (MI355X_MICROARCH.md)
-  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
-#if AG_X8_PAIRSYNC
   if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
-#endif
   const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
   const TileIO io = tile_io(p, tile, lane, p.in_block_stride);
   Regs4 r;
@@ -195,224 +190,6 @@ __global__ __launch_bounds__(512, AG_X8_WAVES_PER_EU) void xform8_kernel(const X
 }
 
 // =====================================================================================
-// xform64h: 64-point transform with two workgroups per CU.  4 waves; a tile is 32
-// columns; lane half h (lane >> 5) is position bit 0 in passes A and C:
-//   pass A/C  position (w << 4) | (t << 1) | h : layers dist 2, 4, 8 in-lane; dist 1
-//             pairs the two lane halves (v_permlane32_swap gives every lane both x and
-//             y, both halves run the butterfly, each keeps its own output)
-//   pass B    position h | (w << 1) | (t << 3) : layers dist 16, 32 in-lane
-// The A<->B slot mapping is the 32-point kernel's, lane-local, so the LDS exchanges are
-// shared with xform<4>.  Skew constants never depend on h: the dist-1 group start is the
-// even position of the pair.
-// =====================================================================================
-
-// butterfly whose skew index is BASE + 16 * wave
-template <int BASE, bool INV>
-__device__ __forceinline__ void bfly_w16(int wave, uint32_t* x, uint32_t* y) {
-  switch (wave) {
-    case 0: bfly<BASE, INV>(x, y); break;
-    case 1: bfly<BASE + 16, INV>(x, y); break;
-    case 2: bfly<BASE + 32, INV>(x, y); break;
-    default: bfly<BASE + 48, INV>(x, y); break;
-  }
-}
-
-// dist-1 butterfly across lane halves: half 0 holds x, half 1 holds y (same register).
-template <int S, bool INV>
-__device__ __forceinline__ void cross_bfly(uint32_t* r, uint32_t hmask) {
-  uint32_t X[16], Y[16];
-  static_for<16>([&](auto P) {
-    constexpr int q = decltype(P)::value;
-    const auto sw = __builtin_amdgcn_permlane32_swap(r[q], r[q], false, false);
-    X[q] = sw[0];  // lanes of both halves: x
-    Y[q] = sw[1];  // y
-  });
-  if constexpr (INV) {
-    dev::xor_planes(Y, X);
-    if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(X, Y);
-  } else {
-    if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(X, Y);
-    dev::xor_planes(Y, X);
-  }
-  static_for<16>([&](auto P) {
-    constexpr int q = decltype(P)::value;
-    r[q] = dev::bfi(hmask, Y[q], X[q]);
-  });
-}
-template <int BASE, bool INV>
-__device__ __forceinline__ void cross_bfly_w16(int wave, uint32_t* r, uint32_t hmask) {
-  switch (wave) {
-    case 0: cross_bfly<BASE, INV>(r, hmask); break;
-    case 1: cross_bfly<BASE + 16, INV>(r, hmask); break;
-    case 2: cross_bfly<BASE + 32, INV>(r, hmask); break;
-    default: cross_bfly<BASE + 48, INV>(r, hmask); break;
-  }
-}
-
-// in-lane layers of pass A / C: layer bit b (1..3) <-> slot bit b-1
-template <int B, int DELTA, bool INV>
-__device__ __forceinline__ void x64h_inlane_layer(int wave, Regs8& r) {
-  constexpr int d = 1 << B, tb = B - 1;
-  static_for<4>([&](auto I) {
-    constexpr int i = decltype(I)::value;
-    constexpr int t = ((i >> tb) << (tb + 1)) | (i & ((1 << tb) - 1));
-    constexpr int g = (2 * t) & ~(2 * d - 1);
-    bfly_w16<g + d + DELTA - 1, INV>(wave, r[t], r[t + (1 << tb)]);
-  });
-}
-template <int DIN>
-__device__ __forceinline__ void x64h_pass_a(int wave, uint32_t hmask, Regs8& r) {
-  static_for<8>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    cross_bfly_w16<2 * t + DIN, true>(wave, r[t], hmask);
-  });
-  x64h_inlane_layer<1, DIN, true>(wave, r);
-  x64h_inlane_layer<2, DIN, true>(wave, r);
-  x64h_inlane_layer<3, DIN, true>(wave, r);
-}
-template <int DOUT>
-__device__ __forceinline__ void x64h_pass_c(int wave, uint32_t hmask, Regs8& r) {
-  x64h_inlane_layer<3, DOUT, false>(wave, r);
-  x64h_inlane_layer<2, DOUT, false>(wave, r);
-  x64h_inlane_layer<1, DOUT, false>(wave, r);
-  static_for<8>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    cross_bfly_w16<2 * t + DOUT, false>(wave, r[t], hmask);
-  });
-}
-// pass B: slot t <-> position bits 3..5; layers bit 4 (slot bit 1), bit 5 (slot bit 2)
-template <int DIN>
-__device__ __forceinline__ void x64h_pass_b_ifft(Regs8& r) {
-  static_for<4>([&](auto I) {
-    constexpr int t = ((decltype(I)::value >> 1) << 2) | (decltype(I)::value & 1);
-    dev::ifft_bfly<32 * (t >> 2) + 16 + DIN - 1>(r[t], r[t + 2]);
-  });
-  static_for<4>([&](auto I) {
-    constexpr int t = decltype(I)::value;
-    dev::ifft_bfly<32 + DIN - 1>(r[t], r[t + 4]);
-  });
-}
-template <int DOUT>
-__device__ __forceinline__ void x64h_pass_b_fft(Regs8& r) {
-  static_for<4>([&](auto I) {
-    constexpr int t = decltype(I)::value;
-    dev::fft_bfly<32 + DOUT - 1>(r[t], r[t + 4]);
-  });
-  static_for<4>([&](auto I) {
-    constexpr int t = ((decltype(I)::value >> 1) << 2) | (decltype(I)::value & 1);
-    dev::fft_bfly<32 * (t >> 2) + 16 + DOUT - 1>(r[t], r[t + 2]);
-  });
-}
-
-// Half-wave tile I/O: a tile is 32 chunks; instruction q covers chunks 8q .. 8q+7 of the
-// tile per lane half (512 B lane-linear); half-lane c = 16a + b takes quarter (b & 1) of
-// chunk 8q + (b >> 1), low bytes for a = 0, high bytes for a = 1.  v_permlane16_swap then
-// pairs low and high bytes (lanes b and b + 16 of a half): a = 0 keeps chunks q = 0, 1,
-// a = 1 chunks q = 2, 3.
-__device__ __forceinline__ TileIO tile_io_h(uint64_t total_columns, uint32_t chunks_per_shard, uint64_t tile,
-                                            int lane, uint64_t block_stride) {
-  TileIO io;
-  io.valid = 0;
-  const int c = lane & 31, a = c >> 4, b = c & 15;
-  static_for<4>([&](auto Q) {
-    constexpr int q = decltype(Q)::value;
-    const uint64_t g = tile * 32 + 8 * q + (b >> 1);
-    const bool ok = g < total_columns;
-    const uint64_t gc = ok ? g : total_columns - 1;
-    const uint64_t blk = gc / chunks_per_shard;
-    io.blk[q] = blk;
-    io.off[q] = blk * block_stride + (gc - blk * chunks_per_shard) * 64 + 32 * a + 16 * (b & 1);
-    io.valid |= ok ? (1u << q) : 0u;
-  });
-  return io;
-}
-__device__ __forceinline__ void swap_rows16(uint32_t* v) {
-  static_for<8>([&](auto K) {
-    constexpr int k = decltype(K)::value;
-    const auto r = __builtin_amdgcn_permlane16_swap(v[k], v[k + 8], false, false);
-    v[k] = r[0];
-    v[k + 8] = r[1];
-  });
-}
-__device__ __forceinline__ void store_shard_h(uint8_t* __restrict__ base, const TileIO& io, uint32_t qmask,
-                                              const uint32_t* planes) {
-  uint32_t v[16];
-  static_for<16>([&](auto P) { v[decltype(P)::value] = planes[decltype(P)::value]; });
-  dev::transpose8(v);
-  dev::transpose8(v + 8);
-  swap_rows16(v);
-  static_for<4>([&](auto Q) {
-    constexpr int q = decltype(Q)::value;
-    if (qmask & (1u << q))
-      *reinterpret_cast<uint4*>(base + io.off[q]) = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-  });
-}
-
-template <int DIN, int DOUT>
-__global__ __launch_bounds__(256, 2) void xform64h_kernel(const XformParams p) {
-  __shared__ uint4 lds[16 * 4 * kXfLanes];
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t h = lane >> 5;
-  const uint32_t hmask = 0u - h;
-  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
-  const TileIO io = tile_io_h(p.total_columns, p.chunks_per_shard, tile, lane, p.in_block_stride);
-  Regs8 ra;
-  static_for<8>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    const uint32_t s = (wave << 4) | (t << 1) | h;  // this lane's shard (differs per half)
-    if (s < p.n_in) {
-      const uint8_t* base = p.in + s * p.in_shard_stride;
-      static_for<4>([&](auto Q) {
-        constexpr int q = decltype(Q)::value;
-        const uint4 x = *reinterpret_cast<const uint4*>(base + io.off[q]);
-        ra[t][4 * q] = x.x;
-        ra[t][4 * q + 1] = x.y;
-        ra[t][4 * q + 2] = x.z;
-        ra[t][4 * q + 3] = x.w;
-      });
-    } else {
-      static_for<16>([&](auto P) { ra[t][decltype(P)::value] = 0; });
-    }
-  });
-  uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
-  if (p.out_mask) {
-    if (!p.pattern_per_block) {
-      const uint64_t m = p.out_mask[0];
-      mask[0] = mask[1] = mask[2] = mask[3] = m;
-    } else {
-      const TileIO oi = tile_io_h(p.total_columns, p.chunks_per_shard, tile, lane, p.out_block_stride);
-      static_for<4>([&](auto Q) { mask[decltype(Q)::value] = p.out_mask[oi.blk[decltype(Q)::value]]; });
-    }
-  }
-  static_for<8>([&](auto T) {
-    swap_rows16(ra[decltype(T)::value]);
-    dev::planes_from_raw(ra[decltype(T)::value]);
-  });
-  x64h_pass_a<DIN>(wave, hmask, ra);
-  Regs8 rb;
-  xf_exchange_ab<4>(wave, lane, lds, ra, rb);
-  x64h_pass_b_ifft<DIN>(rb);
-  x64h_pass_b_fft<DOUT>(rb);
-  xf_exchange_bc<4>(wave, lane, lds, rb, ra);
-
-  const TileIO out_io = tile_io_h(p.total_columns, p.chunks_per_shard, tile, lane, p.out_block_stride);
-  uint32_t qall = 0;  // store predicates packed before the first store (see qmask_all)
-  static_for<8>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    const uint32_t s = (wave << 4) | (t << 1) | h;
-    if (s < p.n_out) qall |= store_qmask(out_io, mask, s) << (4 * t);
-  });
-  if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;
-  x64h_pass_c<DOUT>(wave, hmask, ra);
-  static_for<8>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    const uint32_t s = (wave << 4) | (t << 1) | h;
-    if (s < p.n_out) store_shard_h(p.out + s * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, ra[t]);
-  });
-}
-
-// =====================================================================================
 // decode_x<NW>: the crate's HighRate decoder for any erasure
 // pattern, bitsliced, over a W = 8*NW point window (W = next_pow2(chunk + k) in {32, 64}):
 //   pass A : load present positions (recovery j < chunk, original chunk + i), multiply by
@@ -426,28 +203,11 @@ __global__ __launch_bounds__(256, 2) void xform64h_kernel(const XformParams p) {
 // pattern for the batch, or tiles that never straddle blocks).
 // =====================================================================================
 
-// x <- M x for a runtime 16x16 GF(2) matrix, rows[o] bit i = M[o][i] (wave-uniform rows:
-// the row words and the 0/~0 masks live in SGPRs; 256 v_bitop3 per 32-symbol plane set).
-__device__ __forceinline__ void mul_rt(uint32_t* x, const uint32_t* __restrict__ rows) {
-  uint32_t y[16];
-  static_for<16>([&](auto O) {
-    constexpr int o = decltype(O)::value;
-    const uint32_t r = __builtin_amdgcn_readfirstlane(rows[o]);
-    uint32_t acc = 0;
-    static_for<16>([&](auto I) {
-      constexpr int i = decltype(I)::value;
-      const uint32_t msk = static_cast<uint32_t>(static_cast<int32_t>(r << (31 - i)) >> 31);
-      acc = __builtin_amdgcn_bitop3_b32(acc, x[i], msk, 0x78);  // acc ^ (x & msk)
-    });
-    y[o] = acc;
-  });
-  static_for<16>([&](auto O) { x[decltype(O)::value] = y[decltype(O)::value]; });
-}
-
-// The same product by four Russians: per group of 4 input planes, the 16 XOR combinations
-// (11 XORs); output plane o is then the XOR of 4 combinations picked by the row's nibbles.
-// The nibbles are wave-uniform, so each pick is one v_movrels (M0 index) instead of 4
-// bitop3s: 44 + 16 * 5 VALU per multiply instead of 256 (+ the mask extraction).
+// x <- M x for a runtime 16x16 GF(2) matrix (rows[o] bit i = M[o][i], wave-uniform rows) by
+// four Russians: per group of 4 input planes, the 16 XOR combinations (11 XORs); output plane
+// o is then the XOR of 4 combinations picked by the row's nibbles.  The nibbles are
+// wave-uniform, so each pick is one v_movrels (M0 index) instead of 4 bitop3s: 44 + 16 * 5
+// VALU per multiply instead of 256 masked XORs (+ the mask extraction).
 __device__ __forceinline__ void mul_rt4(uint32_t* x, const uint32_t* __restrict__ rows) {
   uint32_t t0[16], t1[16], t2[16], t3[16];
   auto build = [&](uint32_t* t, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
@@ -477,17 +237,6 @@ __device__ __forceinline__ void mul_rt4(uint32_t* x, const uint32_t* __restrict_
     const uint32_t r = __builtin_amdgcn_readfirstlane(rows[o]);
     x[o] = dev::xor3(t0[r & 15], t1[(r >> 4) & 15], t2[(r >> 8) & 15]) ^ t3[(r >> 12) & 15];
   });
-}
-
-#ifndef AG_DX_MUL4
-#define AG_DX_MUL4 1
-#endif
-__device__ __forceinline__ void mul_rt_dx(uint32_t* x, const uint32_t* __restrict__ rows) {
-#if AG_DX_MUL4
-  mul_rt4(x, rows);
-#else
-  mul_rt(x, rows);
-#endif
 }
 
 __device__ __forceinline__ void lds_get_xor(const uint4* lds, int slot, int lane, uint32_t* v) {
@@ -600,7 +349,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
     if ((in_mask >> j) & 1) {
       if constexpr (!PL) swap_halves(ra[t]);
       dev::planes_from_raw(ra[t]);
-      if constexpr (PL) dev::mul_rt_poly(ra[t], rows[j]); else mul_rt_dx(ra[t], rows + j * 16);
+      if constexpr (PL) dev::mul_rt_poly(ra[t], rows[j]); else mul_rt4(ra[t], rows + j * 16);
     }
   });
   xf_pass_a<NW, 0>(wave, ra);
@@ -626,7 +375,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
         dev::mul_rt_poly(ra[t], rows[j]);
         dev::store_chunk(dst + off_o, ra[t]);
       } else {
-        mul_rt_dx(ra[t], rows + j * 16);
+        mul_rt4(ra[t], rows + j * 16);
         store_shard(dst, io_o, io_o.valid, ra[t]);
       }
     }
@@ -634,7 +383,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
 }
 
 // =====================================================================================
-// decode_x16<PL, PASS, DIN, DOUT>: the window decoder (decode_x's algorithm) on xform16's
+// decode_x16<PASS, DIN, DOUT>: the window decoder (decode_x's algorithm) on the 16-wave
 // layout: 16 waves x 4 slots, one 1024-thread workgroup per CU at 4 waves/SIMD (decode_x<8>
 // keeps 8 slots per lane at 216 VGPRs: 2 waves/SIMD, latency-bound).
 // Positions by layout (X8Lay: slot bits | wave bits):
@@ -655,12 +404,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
 // (tests/test_oracle.py pins the identity against the oracle's 128-point decoder).  Pass 1
 // (DIN = the other half, DOUT = the output half): IFFT, no derivative, FFT, the partial
 // stored unmultiplied.  Pass 2 (DIN = DOUT = the output half): IFFT, P, FFT, + the stored
-// partial (in planes), output multiply (linear: one product per restored original).  Loads, masks and staged constants
-// are the pass's loaded half (window positions DIN + j); outputs are window positions DOUT + j.
-// Multiplies by the per-position constants are Horner products in the polynomial basis
-// (mul_rt_poly); PL: per-lane constants staged in LDS, else one wave-uniform word.
+// partial (in planes), output multiply (linear: one product per restored original).  Loads
+// and masks are the pass's loaded half (window positions DIN + j); outputs are window
+// positions DOUT + j.  One pattern per tile (tiles never straddle blocks): the constants are
+// wave-uniform words, multiplied by the Horner scheme in the polynomial basis (mul_rt_poly).
+// Per-lane patterns run on decode_h8.
 // =====================================================================================
-template <bool PL, int PASS, int DIN, int DOUT>
+template <int PASS, int DIN, int DOUT>
 __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams p) {
   using G0 = X8Lay<0, 1, 2, 3, 4, 5>;
   using G1 = X8Lay<2, 1, 0, 3, 4, 5>;
@@ -669,77 +419,39 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
   using G4 = X8Lay<4, 5, 0, 1, 2, 3>;
   static_assert(PASS != 0 || (DIN == 0 && DOUT == 0), "the one-pass window starts at 0");
   static_assert(PASS != 2 || DIN == DOUT, "pass 2 loads its output half");
-  constexpr int W = 64;  // positions per pass
   __shared__ uint4 lds[32 * 4 * kXfLanes];  // 16 waves x 2 slots x 4 KiB
   __shared__ XFlags<16> flags;
-  // PL: the polynomial-basis constants of the pass's 64 positions for the <= 64 blocks the
-  // tile's columns belong to, staged once by the workgroup instead of a dependent global
-  // load per product
-  __shared__ uint32_t lcoef[PL ? kXfLanes * W : 1];
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
   const uint32_t rw = p.rows_w;  // constants per pattern (64 or 128)
-  uint64_t sb0 = 0;  // PL: first block of the tile
-  if constexpr (PL) {
-    const uint64_t c0 = static_cast<uint64_t>(tile) * kXfLanes;
-    const uint64_t c1 = c0 + kXfLanes - 1 < p.total_columns ? c0 + kXfLanes - 1 : p.total_columns - 1;
-    sb0 = c0 / p.chunks_per_shard;
-    const uint32_t nbt = static_cast<uint32_t>(c1 / p.chunks_per_shard - sb0 + 1);  // <= 64
-    for (uint32_t i = threadIdx.x; i < nbt * W; i += blockDim.x) lcoef[i] = p.rows[(sb0 + i / W) * rw + DIN + i % W];
-  }
   if (threadIdx.x < 32) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
-  uint64_t in_mask, out_mask;
-  const uint32_t* coef = lcoef;  // PL: the lane's staged constants; else the pattern's (global)
-  const uint32_t* coef_out;      // the output half's constants (PASS 1: none, its partial is unmultiplied)
-  TileIO io_r, io_o;
-  uint64_t off_r = 0, off_o = 0;
-  if constexpr (PL) {
-    const uint64_t gc = static_cast<uint64_t>(tile) * kXfLanes + lane;
-    const bool ok = gc < p.total_columns;
-    const uint64_t blk = ok ? gc / p.chunks_per_shard : sb0;
-    const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
-    in_mask = ok ? p.pmask[2 * blk] : 0;
-    out_mask = ok ? p.pmask[2 * blk + 1] : 0;
-    coef = lcoef + (blk - sb0) * W;  // the lane's block among the staged ones
-    coef_out = coef;  // PASS 1 stores unmultiplied; PASS 2 has DIN == DOUT
-    off_r = blk * p.rec_block_stride + col * 64;
-    off_o = blk * p.orig_block_stride + col * 64;
-  } else {
-    uint64_t vtile = tile, pat = 0;
-    if (p.per_block) {
-      const uint64_t bi = tile / p.tiles_per_block;
-      const uint64_t blk = p.block_ids ? p.block_ids[bi] : bi;
-      vtile = blk * p.tiles_per_block + (tile - bi * p.tiles_per_block);
-      pat = blk;
-    }
-    in_mask = p.pmask[2 * pat];
-    out_mask = p.pmask[2 * pat + 1];
-    coef = p.rows + pat * rw + DIN;
-    coef_out = p.rows + pat * rw + DOUT;
-    io_r = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.rec_block_stride);
-    io_o = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.orig_block_stride);
+  uint64_t vtile = tile, pat = 0;
+  if (p.per_block) {
+    const uint64_t bi = tile / p.tiles_per_block;
+    const uint64_t blk = p.block_ids ? p.block_ids[bi] : bi;
+    vtile = blk * p.tiles_per_block + (tile - bi * p.tiles_per_block);
+    pat = blk;
   }
+  const uint64_t in_mask = p.pmask[2 * pat];
+  const uint64_t out_mask = p.pmask[2 * pat + 1];
+  const uint32_t* coef = p.rows + pat * rw + DIN;
+  const uint32_t* coef_out = p.rows + pat * rw + DOUT;
+  const TileIO io_r = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.rec_block_stride);
+  const TileIO io_o = tile_io_g(p.total_columns, p.chunks_per_shard, vtile, lane, p.orig_block_stride);
   const uint32_t opos = p.low_rate ? 0 : p.chunk, rpos = p.low_rate ? p.chunk : 0;
-  // shard base of window position g (recovery shards below the originals in HighRate)
-  auto shard_src = [&](uint32_t g, bool& is_rec) -> const uint8_t* {
-    is_rec = p.low_rate ? g >= p.chunk : g < p.chunk;
-    return is_rec ? p.rec + (g - rpos) * p.rec_shard_stride : p.orig + (g - opos) * p.orig_shard_stride;
-  };
   Regs4 r;
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = 4 * wave + t;  // G0 position in the pass (wave-uniform)
-    if ((in_mask >> j) & 1) {          // PL: per lane
-      bool is_rec;
-      const uint8_t* base = shard_src(DIN + j, is_rec);
+    if ((in_mask >> j) & 1) {
+      const uint32_t g = DIN + j;  // window position (recovery shards below the originals in HighRate)
+      const bool is_rec = p.low_rate ? g >= p.chunk : g < p.chunk;
+      const uint8_t* base = is_rec ? p.rec + (g - rpos) * p.rec_shard_stride : p.orig + (g - opos) * p.orig_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint8_t* src;
-        if constexpr (PL) src = base + (is_rec ? off_r : off_o) + 16 * q;
-        else src = base + (is_rec ? io_r.off[q] : io_o.off[q]);
-        const uint4 x = ld_piece(src);
+        const uint4 x = ld_piece(base + (is_rec ? io_r.off[q] : io_o.off[q]));
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -753,7 +465,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
     constexpr int t = decltype(T)::value;
     const uint32_t j = 4 * wave + t;
     if ((in_mask >> j) & 1) {
-      if constexpr (!PL) swap_halves(r[t]);
+      swap_halves(r[t]);
       dev::planes_from_raw(r[t]);
       dev::mul_rt_poly(r[t], coef[j]);
     }
@@ -816,37 +528,34 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
   x8_swap<1, 1, 7>(wave, lane, lds, &flags, r);
   x8_layer_t<G1, 1, false, DOUT>(wave, r);
   x8_swap<0, 0, 8>(wave, lane, lds, &flags, r);
-  const uint32_t mine = static_cast<uint32_t>(out_mask >> (4 * wave)) & 0xF;
-  if constexpr (PL) {
-    if (__builtin_amdgcn_ballot_w64(mine != 0) == 0) return;  // nothing to restore in this wave
-  } else {
-    if (mine == 0) return;
-  }
+  const uint32_t mine = static_cast<uint32_t>(out_mask >> (4 * wave)) & 0xF;  // wave-uniform
+  if (mine == 0) return;
   x8_layer_t<G0, 0, false, DOUT>(wave, r);
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = 4 * wave + t;
-    if ((out_mask >> j) & 1) {
+    if ((mine >> t) & 1) {
       uint8_t* dst = p.orig + (DOUT + j - opos) * p.orig_shard_stride;
-      // the output multiply is linear: pass 1 stores its unmultiplied partial, pass 2 adds it
-      // in planes and multiplies once
       if constexpr (PASS == 2) {
+        // + pass 1's partial, in planes (the youngest memory operation when waited on, as in
+        // decode_h8)
         uint32_t o[16];
         static_for<4>([&](auto Q) {
           constexpr int q = decltype(Q)::value;
-          const uint4 x = ld_piece(PL ? dst + off_o + 16 * q : dst + io_o.off[q]);
+          const uint4 x = ld_piece(dst + io_o.off[q]);
           o[4 * q] = x.x;
           o[4 * q + 1] = x.y;
           o[4 * q + 2] = x.z;
           o[4 * q + 3] = x.w;
         });
-        if constexpr (!PL) swap_halves(o);
+        swap_halves(o);
         dev::planes_from_raw(o);
         dev::xor_planes(r[t], o);
       }
+      // the output multiply is linear: pass 1 stores its unmultiplied partial, pass 2 has
+      // added it in planes and multiplies once
       if constexpr (PASS != 1) dev::mul_rt_poly(r[t], coef_out[j]);
-      if constexpr (PL) dev::store_chunk<true>(dst + off_o, r[t]);
-      else store_shard(dst, io_o, io_o.valid, r[t]);
+      store_shard(dst, io_o, io_o.valid, r[t]);
     }
   });
 }
@@ -873,24 +582,14 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
 // half DOUT), with the output multiply deferred: pass 1 stores FFT(u_other) unmultiplied,
 // pass 2 adds it to FFT(P u_out) in planes and multiplies once (the multiply is linear), so a
 // restored original costs one runtime product instead of two.
-// LL (16 | chunks per shard): lane-linear loads and stores as xform_h8 (tile_io_l32's piece
-// order + quad_exchange).  Lane i of a half then holds chunks (i >> 2) and (i >> 2) + 8 (i & 2
-// clear) or those + 16 (i & 2 set): one 16-chunk group of the tile, so one slice, whose
-// pattern the lane computes with; its loads and stores also cover the quad partner's group,
-// under that group's masks.  Otherwise each lane loads its own whole chunk (pieces 64 bytes
-// apart in every wave access).
-// =====================================================================================
-// IO = 2 (UNI, 32 | chunks per shard): one pattern per tile (tiles never straddle blocks: the
-// batch's single pattern, or per-block patterns through block_ids) with lane-linear I/O.  The
-// constants and masks are wave-uniform per lane half, so a slot's product runs on the scalar-
-// branch Horner under the half's exec mask when one half needs it, on the per-lane Horner when
-// both do, and not at all when neither does.
-#ifndef AG_H8_PAIRDER
-#define AG_H8_PAIRDER 1
-#endif
-template <int OUTH, int PASS, int DIN, int DOUT, int IO>
+// Each lane loads its own whole chunk (four 16-byte pieces of one chunk).  A lane-linear
+// option (xform_h8's piece order + quad_exchange) measured slower on the follower's batches
+// (14.0-14.1 vs 14.4-14.6 M slices/s, profiles/r03_h8_ll_ab.jsonl) and was removed.
+// The derivative's regions are handed over by the swaps' epoch flags (no workgroup barriers):
+// ready = published, done = this wave's reads finished; a region is rewritten once every
+// reader of its last epoch is done.  Epochs: swaps 1-3, derivative rounds 4-5, swaps 6-8.
+template <int OUTH, int PASS, int DIN, int DOUT>
 __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p) {
-  constexpr bool LL = IO >= 1, UNI = IO == 2;
   static_assert(PASS != 0 || (DIN == 0 && DOUT == 0), "the one-pass window starts at 0");
   static_assert(PASS != 2 || DIN == DOUT, "pass 2 loads its output half");
   using LB = X8Lay<2, 1, 3, 4, 5>;
@@ -905,87 +604,28 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   const int h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
-  uint64_t vtile = tile, pat = 0;  // UNI: the tile's place in the batch and its pattern
-  if constexpr (UNI) {
-    if (p.per_block) {
-      const uint64_t bi = tile / p.tiles_per_block;
-      const uint64_t bk = p.block_ids ? p.block_ids[bi] : bi;
-      vtile = bk * p.tiles_per_block + (tile - bi * p.tiles_per_block);
-      pat = bk;
-    }
-  }
-  const uint64_t c0 = vtile * kCols;
+  const uint64_t c0 = static_cast<uint64_t>(tile) * kCols;
   const uint64_t c1 = c0 + kCols - 1 < p.total_columns ? c0 + kCols - 1 : p.total_columns - 1;
   const uint64_t sb0 = c0 / p.chunks_per_shard;
-  if constexpr (!UNI) {
+  {
     const uint32_t nbt = static_cast<uint32_t>(c1 / p.chunks_per_shard - sb0 + 1);  // <= 32
     for (uint32_t i = threadIdx.x; i < nbt * W; i += blockDim.x) lcoef[i] = p.rows[(sb0 + i / W) * p.rows_w + DIN + i % W];
   }
-  const uint32_t* coefu = p.rows + pat * p.rows_w + DIN;  // UNI: the pattern's constants (uniform)
-  const uint64_t umask_in = UNI ? p.pmask[2 * pat] : 0, umask_out = UNI ? p.pmask[2 * pat + 1] : 0;
   if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
-  uint64_t blk, col, in_mask, out_mask;
-  // LL: the two 16-chunk groups of the tile -- block, first chunk, mask word (word 0: present,
-  // 1: restored) -- for lane ln (group 0: pieces q = 0, 1).  Computed at the loads and again
-  // at the stores (from laundered inputs: kept live across the transform they spill).
-  struct Groups {
-    uint64_t blk[2], col[2], mask[2];
-  };
-  auto groups = [&](uint64_t tile_c0, int ln, int word) {
-    Groups gr;
-    static_for<2>([&](auto G) {
-      constexpr int g = decltype(G)::value;
-      const uint64_t gc = tile_c0 + 16 * g + ((ln & 31) >> 2);  // chunks gc, gc + 8 (16 | cps)
-      const bool ok = gc < p.total_columns;
-      gr.blk[g] = ok ? gc / p.chunks_per_shard : sb0;
-      gr.col[g] = ok ? gc - gr.blk[g] * p.chunks_per_shard : 0;
-      if constexpr (UNI) gr.mask[g] = ok ? (word ? umask_out : umask_in) : 0;
-      else gr.mask[g] = ok ? p.pmask[2 * gr.blk[g] + word] : 0;
-    });
-    return gr;
-  };
-  Groups gin{};
-  if constexpr (LL) {
-    gin = groups(c0, lane, 0);
-    const int own = (lane >> 1) & 1;
-    blk = own ? gin.blk[1] : gin.blk[0];
-    col = 0;
-    in_mask = own ? gin.mask[1] : gin.mask[0];
-    out_mask = 0;  // read at the stores
-  } else {
-    const uint64_t gc = c0 + (lane & 31);
-    const bool ok = gc < p.total_columns;
-    blk = ok ? gc / p.chunks_per_shard : sb0;
-    col = ok ? gc - blk * p.chunks_per_shard : 0;
-    in_mask = ok ? p.pmask[2 * blk] : 0;
-    out_mask = ok ? p.pmask[2 * blk + 1] : 0;
-  }
-  const uint32_t* coef = UNI ? coefu : lcoef + (blk - sb0) * W;
+  const uint64_t gc = c0 + (lane & 31);
+  const bool ok = gc < p.total_columns;
+  const uint64_t blk = ok ? gc / p.chunks_per_shard : sb0;
+  const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
+  const uint64_t in_mask = ok ? p.pmask[2 * blk] : 0;
+  const uint64_t out_mask = ok ? p.pmask[2 * blk + 1] : 0;
+  const uint32_t* coef = lcoef + (blk - sb0) * W;
   const uint64_t off_r = blk * p.rec_block_stride + col * 64;
   const uint64_t off_o = blk * p.orig_block_stride + col * 64;
-  // LL: byte offset of piece q within a shard (rec / orig block strides)
-  auto piece_off = [&](const Groups& gr, int q, uint64_t block_stride) -> uint64_t {
-    const int g = q >> 1;
-    return gr.blk[g] * block_stride + (gr.col[g] + 8 * (q & 1)) * 64 + 16 * (lane & 3);
-  };
   const uint32_t opos = p.low_rate ? 0 : p.chunk, rpos = p.low_rate ? p.chunk : 0;
   // layout A position of slot t in this lane
   auto posA = [&](int t) -> uint32_t {
     return static_cast<uint32_t>((t & 1) | ((t >> 1) << 1) | (h << 2) | (wave << 3));
-  };
-  // UNI: slot t's product for the halves whose bit of mask m is set (m, the constants and the
-  // choice are wave-uniform)
-  auto mul_u = [&](uint32_t* x, int t, uint64_t m) __attribute__((always_inline)) {  // inlined: a
-    // called closure would put the kernel's locals in scratch
-    const uint32_t j0 = static_cast<uint32_t>(t | (wave << 3)), j1 = j0 | 4u;
-    const bool n0 = (m >> j0) & 1, n1 = (m >> j1) & 1;
-    const uint32_t c0 = __builtin_amdgcn_readfirstlane(coefu[j0]), c1 = __builtin_amdgcn_readfirstlane(coefu[j1]);
-    if (n0 && n1) {
-      dev::mul_rt_poly(x, h ? c1 : c0);
-    } else if (n0 || n1) {
-      if ((h != 0) == n1) dev::mul_rt_poly_u(x, n1 ? c1 : c0);  // the one half that needs it
-    }
   };
   Regs4 r;
   static_for<4>([&](auto T) {
@@ -993,20 +633,7 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
     const uint32_t j = posA(t);
     const uint32_t g = DIN + j;  // window position
     const bool is_rec = p.low_rate ? g >= p.chunk : g < p.chunk;
-    if constexpr (LL) {
-      const uint8_t* sh = is_rec ? p.rec + (g - rpos) * p.rec_shard_stride : p.orig + (g - opos) * p.orig_shard_stride;
-      const uint64_t bs = is_rec ? p.rec_block_stride : p.orig_block_stride;
-      static_for<4>([&](auto Q) {
-        constexpr int q = decltype(Q)::value;
-        uint4 x = make_uint4(0, 0, 0, 0);
-        if ((gin.mask[q >> 1] >> j) & 1) x = ld_piece(sh + piece_off(gin, q, bs));
-        r[t][4 * q] = x.x;
-        r[t][4 * q + 1] = x.y;
-        r[t][4 * q + 2] = x.z;
-        r[t][4 * q + 3] = x.w;
-      });
-      quad_exchange(r[t], lane);  // every lane: partners exchange whatever they loaded
-    } else if ((in_mask >> j) & 1) {
+    if ((in_mask >> j) & 1) {
       const uint8_t* src = is_rec ? p.rec + (g - rpos) * p.rec_shard_stride + off_r
                                   : p.orig + (g - opos) * p.orig_shard_stride + off_o;
       static_for<4>([&](auto Q) {
@@ -1024,13 +651,7 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t j = posA(t);
-    if constexpr (UNI) {
-      const uint32_t j0 = static_cast<uint32_t>(t | (wave << 3));
-      if (((umask_in >> j0) | (umask_in >> (j0 | 4u))) & 1) {  // wave-uniform
-        dev::planes_from_raw(r[t]);  // absent halves hold zeros
-        mul_u(r[t], t, umask_in);
-      }
-    } else if ((in_mask >> j) & 1) {
+    if ((in_mask >> j) & 1) {
       dev::planes_from_raw(r[t]);
       dev::mul_rt_poly(r[t], coef[j]);
     }
@@ -1049,11 +670,8 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   // formal derivative in E (slot t: p4 = t & 1, p5 = t >> 1; lane half p0; waves p1 p2 p3);
   // PASS 2: P = the derivative without its self term; PASS 1: none.  Each wave publishes its
   // two pre-derivative slots of round rho in its own region (its swap inbox); the waves with
-  // a wave bit b clear add the region of their partner w | 2^b.  AG_H8_PAIRDER: the regions
-  // are handed over by the epoch flags of the swaps (ready = published, done = this wave's
-  // reads finished; a region is rewritten once every reader of its last epoch is done)
-  // instead of workgroup barriers.  Epochs: swaps 1-3, derivative rounds 4-5, swaps 6-8.
-  constexpr int D = (PASS != 1 && AG_H8_PAIRDER) ? 2 : 0;  // FFT swap epochs 4 + D ..
+  // a wave bit b clear add the region of their partner w | 2^b.
+  constexpr int D = PASS != 1 ? 2 : 0;  // FFT swap epochs 4 + D ..
   // the readers of region x in a derivative round: x with one of its set wave bits cleared
   auto wait_readers = [&](int x, uint32_t e) __attribute__((always_inline)) {
     static_for<3>([&](auto Bb) {
@@ -1062,61 +680,45 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
     });
   };
   if constexpr (PASS != 1) {
-#if !AG_H8_PAIRDER
-  __syncthreads();  // every wave's swap reads are done: the exchange buffer is free
-#endif
-  static_for<2>([&](auto Rho) {
-    constexpr int rho = decltype(Rho)::value;
-#if AG_H8_PAIRDER
-    constexpr uint32_t e = 4 + rho;
-    if constexpr (rho == 1) wait_readers(wave, e - 1);  // round 0's readers of this region
-#endif
-    static_for<2>([&](auto U) { lds_put(lds, 2 * wave + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
-#if AG_H8_PAIRDER
-    x8_signal(&flags.ready[wave], e, lane);
-#endif
-    static_for<2>([&](auto U) {
-      constexpr int t = 2 * rho + decltype(U)::value;
-      // p0 term: the lower half (p0 clear) adds the upper half's pre-derivative value
-      uint32_t hi[16];
-      static_for<16>([&](auto P) {
-        constexpr int q = decltype(P)::value;
-        hi[q] = __builtin_amdgcn_permlane32_swap(r[t][q], 0u, false, false)[1];
-      });
-      // slot bits, ascending t: partners t | 1, t | 2 > t still hold pre-derivative values
-      if constexpr (PASS == 2) {
+    static_for<2>([&](auto Rho) {
+      constexpr int rho = decltype(Rho)::value;
+      constexpr uint32_t e = 4 + rho;
+      if constexpr (rho == 1) wait_readers(wave, e - 1);  // round 0's readers of this region
+      static_for<2>([&](auto U) { lds_put(lds, 2 * wave + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+      x8_signal(&flags.ready[wave], e, lane);
+      static_for<2>([&](auto U) {
+        constexpr int t = 2 * rho + decltype(U)::value;
+        // p0 term: the lower half (p0 clear) adds the upper half's pre-derivative value
+        uint32_t hi[16];
         static_for<16>([&](auto P) {
           constexpr int q = decltype(P)::value;
-          uint32_t v = hi[q];
-          if constexpr (!(t & 1)) v ^= r[t | 1][q];
-          if constexpr (!(t & 2)) v ^= r[t | 2][q];
-          r[t][q] = v;
+          hi[q] = __builtin_amdgcn_permlane32_swap(r[t][q], 0u, false, false)[1];
         });
-      } else {
-        if constexpr (!(t & 1)) dev::xor_planes(r[t], r[t | 1]);
-        if constexpr (!(t & 2)) dev::xor_planes(r[t], r[t | 2]);
-        dev::xor_planes(r[t], hi);
-      }
+        // slot bits, ascending t: partners t | 1, t | 2 > t still hold pre-derivative values
+        if constexpr (PASS == 2) {
+          static_for<16>([&](auto P) {
+            constexpr int q = decltype(P)::value;
+            uint32_t v = hi[q];
+            if constexpr (!(t & 1)) v ^= r[t | 1][q];
+            if constexpr (!(t & 2)) v ^= r[t | 2][q];
+            r[t][q] = v;
+          });
+        } else {
+          if constexpr (!(t & 1)) dev::xor_planes(r[t], r[t | 1]);
+          if constexpr (!(t & 2)) dev::xor_planes(r[t], r[t | 2]);
+          dev::xor_planes(r[t], hi);
+        }
+      });
+      static_for<3>([&](auto Bb) {
+        constexpr int b = decltype(Bb)::value;
+        if (!((wave >> b) & 1)) {
+          const int pw = wave | (1 << b);
+          x8_wait_ge(&flags.ready[pw], e);
+          static_for<2>([&](auto U) { lds_get_xor(lds, 2 * pw + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+        }
+      });
+      x8_signal(&flags.done[wave], e, lane);
     });
-#if !AG_H8_PAIRDER
-    __syncthreads();
-#endif
-    static_for<3>([&](auto Bb) {
-      constexpr int b = decltype(Bb)::value;
-      if (!((wave >> b) & 1)) {
-        const int pw = wave | (1 << b);
-#if AG_H8_PAIRDER
-        x8_wait_ge(&flags.ready[pw], e);
-#endif
-        static_for<2>([&](auto U) { lds_get_xor(lds, 2 * pw + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
-      }
-    });
-#if AG_H8_PAIRDER
-    x8_signal(&flags.done[wave], e, lane);
-#else
-    __syncthreads();
-#endif
-  });
   }
   // FFT_64 (skew delta DOUT), ending in A.  The first swap writes the partner's region: its
   // last derivative round's readers must be done with it.
@@ -1156,95 +758,36 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   x8_layer_t<LC, 2, false, DOUT>(wave, r);
   x8_swap<1, 0, 6 + D>(wave, lane, lds, &flags, r);
   x8_layer_t<LB, 1, false, DOUT>(wave, r);
-  Groups gout{};
-  if constexpr (LL) {
-    uint64_t c0_late = c0;
-    int lane_late = lane;
-    __asm__ volatile("" : "+s"(c0_late), "+v"(lane_late));
-    gout = groups(c0_late, lane_late, 1);
-    out_mask = ((lane >> 1) & 1) ? gout.mask[1] : gout.mask[0];
-  }
-  uint32_t mine = 0;
-  static_for<4>([&](auto T) { mine |= static_cast<uint32_t>((out_mask >> posA(decltype(T)::value)) & 1); });
-  if (__builtin_amdgcn_ballot_w64(mine != 0) == 0) return;  // nothing to restore in this wave
+  // the store predicates, packed before the first load or store of the store phase (bit t:
+  // slot t restores its position in this lane's block)
+  uint32_t qall = 0;
+  static_for<4>([&](auto T) { qall |= static_cast<uint32_t>((out_mask >> posA(decltype(T)::value)) & 1) << decltype(T)::value; });
+  if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;  // nothing to restore in this wave
   h8_relayout(r);
   h8_layer0<false, DOUT>(wave, h, r);
-  if constexpr (LL) {
-    // every store predicate packed before the first store (bit 4 t + q: piece q of slot t)
-    uint32_t qall = 0;
-    static_for<4>([&](auto T) {
-      constexpr int t = decltype(T)::value;
-      static_for<4>([&](auto Q) {
-        constexpr int q = decltype(Q)::value;
-        qall |= static_cast<uint32_t>((gout.mask[q >> 1] >> posA(t)) & 1) << (4 * t + q);
-      });
-      qall |= static_cast<uint32_t>((out_mask >> posA(t)) & 1) << (16 + t);  // the lane's own restore
-    });
-    static_for<4>([&](auto T) {
-      constexpr int t = decltype(T)::value;
-      const uint32_t j = posA(t);
-      const bool mine_t = (qall >> (16 + t)) & 1;
-      if (__builtin_amdgcn_ballot_w64(mine_t) == 0) return;  // (this slot only) wave-uniform
-      uint8_t* sh = p.orig + (DOUT + j - opos) * p.orig_shard_stride;
-      if constexpr (PASS == 2) {  // + pass 1's partial, in planes
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = posA(t);
+    if ((qall >> t) & 1) {
+      uint8_t* dst = p.orig + (DOUT + j - opos) * p.orig_shard_stride + off_o;
+      if constexpr (PASS == 2) {
+        // + pass 1's partial, in planes.  The load is the youngest memory operation when it is
+        // waited on (vmcnt(0)): the earlier slots' stores may alias it, so it is not hoisted
+        // above them (tools/scan_waitcnt.py)
         uint32_t o[16];
         static_for<4>([&](auto Q) {
           constexpr int q = decltype(Q)::value;
-          uint4 x = make_uint4(0, 0, 0, 0);
-          if ((qall >> (4 * t + q)) & 1) x = ld_piece(sh + piece_off(gout, q, p.orig_block_stride));
+          const uint4 x = ld_piece(dst + 16 * q);
           o[4 * q] = x.x;
           o[4 * q + 1] = x.y;
           o[4 * q + 2] = x.z;
           o[4 * q + 3] = x.w;
         });
-        quad_exchange(o, lane);
-        if (mine_t) {
-          dev::planes_from_raw(o);
-          dev::xor_planes(r[t], o);
-        }
+        dev::planes_from_raw(o);
+        dev::xor_planes(r[t], o);
       }
-      if constexpr (PASS != 1) {
-        if (mine_t) {
-          if constexpr (UNI) mul_u(r[t], t, umask_out); else dev::mul_rt_poly(r[t], coef[j]);
-        }
-      }
-      uint32_t v[16];
-      static_for<16>([&](auto P) { v[decltype(P)::value] = r[t][decltype(P)::value]; });
-      dev::transpose8(v);
-      dev::transpose8(v + 8);
-      quad_exchange(v, lane);
-      static_for<4>([&](auto Q) {
-        constexpr int q = decltype(Q)::value;
-        if ((qall >> (4 * t + q)) & 1)
-          st_piece(sh + piece_off(gout, q, p.orig_block_stride), v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
-      });
-    });
-    return;
-  }
-  static_for<4>([&](auto T) {
-    constexpr int t = decltype(T)::value;
-    const uint32_t j = posA(t);
-    if ((out_mask >> j) & 1) {
-      uint8_t* dst = p.orig + (DOUT + j - opos) * p.orig_shard_stride + off_o;
-      if constexpr (PASS == 1) {
-        dev::store_chunk<true>(dst, r[t]);  // the unmultiplied partial
-      } else {
-        if constexpr (PASS == 2) {  // + pass 1's partial, in planes
-          uint32_t o[16];
-          static_for<4>([&](auto Q) {
-            constexpr int q = decltype(Q)::value;
-            const uint4 x = ld_piece(dst + 16 * q);
-            o[4 * q] = x.x;
-            o[4 * q + 1] = x.y;
-            o[4 * q + 2] = x.z;
-            o[4 * q + 3] = x.w;
-          });
-          dev::planes_from_raw(o);
-          dev::xor_planes(r[t], o);
-        }
-        dev::mul_rt_poly(r[t], coef[j]);
-        dev::store_chunk<true>(dst, r[t]);
-      }
+      if constexpr (PASS != 1) dev::mul_rt_poly(r[t], coef[j]);
+      dev::store_chunk<true>(dst, r[t]);  // PASS 1: the unmultiplied partial
     }
   });
 }
@@ -1998,9 +1541,6 @@ __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t* dst, uint64
 }  // namespace
 
 // ---- launchers ----------------------------------------------------------------------
-// Kernel variant selector for in-process A/B timing (tools/ab_xform.py); 0 = default.
-int g_xform_variant = 0;
-int xform_variant() { return g_xform_variant; }
 bool xform_supported(unsigned n) { return n == 32 || n == 64; }
 
 hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hipStream_t stream) {
@@ -2018,9 +1558,9 @@ hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hi
     }
   } else if (n == 64) {
     switch (j) {
-      case 0: return launch_xform16(0, 64, p, stream);
-      case 1: return launch_xform16(0, 128, p, stream);
-      case 2: return launch_xform16(0, 192, p, stream);
+      case 0: return launch_xform64(0, 64, p, stream);
+      case 1: return launch_xform64(0, 128, p, stream);
+      case 2: return launch_xform64(0, 192, p, stream);
       default: return hipErrorInvalidValue;
     }
   } else {
@@ -2044,40 +1584,6 @@ hipError_t launch_xform_lowrate_decode(unsigned j, const XformParams& p, hipStre
   return hipGetLastError();
 }
 
-// A/B aid: AG_RS_DX_H8=0 keeps per-lane W = 64 decodes on decode_x16
-static bool use_h8() {
-  static const bool on = [] {
-    const char* e = std::getenv("AG_RS_DX_H8");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// A/B aid: AG_RS_H8U=1 runs one-pattern-per-tile W = 64 decodes on decode_h8 (UNI) instead
-// of decode_x16.
-static bool use_h8u() {
-  static const bool on = [] {
-    const char* e = std::getenv("AG_RS_H8U");
-    return e && e[0] == '1';
-  }();
-  return on;
-}
-
-// decode_h8 with IO 0 (per-lane patterns, whole-chunk lanes) or 2 (one pattern per tile,
-// lane-linear); 32-column tiles.  The lane-linear per-lane mode (IO 1) measured slower than
-// IO 0 on the follower's batches (14.0-14.1 vs 14.4-14.6 M slices/s, CodingOnly 7.6-8.0 vs
-// 7.5-7.6, profiles/r03_h8_ll_ab.jsonl) and is not launched.
-template <int O, int PS, int DI, int DO>
-static void launch_h8(bool uni, dim3 g, const DecodeXParams& pp, hipStream_t stream) {
-  if constexpr (PS == 0) {  // UNI passes 1 / 2 spill (pass 2: the partial's planes); not built
-    if (uni) {
-      hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO, 2>), g, dim3(512), 0, stream, pp);
-      return;
-    }
-  }
-  hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO, 0>), g, dim3(512), 0, stream, pp);
-}
-
 hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
   if (ntiles == 0) return hipSuccess;
   if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -2090,39 +1596,24 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
     else hipLaunchKernelGGL((decode_x_kernel<4>), grid, dim3(256), 0, stream, p);
     return hipGetLastError();
   }
-  // decode_h8: per-lane patterns (the caller's ntiles counts 64-column ones: 32-column tiles
-  // over every column), or one pattern per tile on 32-column tiles inside blocks (UNI; per
-  // block: the listed blocks' tiles)
-  const bool uni = W == 64 && !pl && use_h8u() && p.chunks_per_shard % 32 == 0 &&
-                   (!p.per_block || p.chunks_per_shard % 64 == 0);
-  const bool h8 = (pl && use_h8()) || uni;
-  DecodeXParams ph = p;
-  uint64_t t32 = (p.total_columns + 31) / 32;
-  if (uni && p.per_block) {
-    ph.tiles_per_block = p.chunks_per_shard / 32;
-    t32 = ntiles * 2;  // two 32-column tiles per 64-column one, block by block
-  }
+  // per-lane patterns run on decode_h8 (32-column tiles over every column; the caller's
+  // ntiles counts 64-column ones), one pattern per tile on decode_x16
+  const uint64_t t32 = (p.total_columns + 31) / 32;
   if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const dim3 g32(static_cast<unsigned>(t32));
-#define AG_H8(O, PS, DI, DO) launch_h8<O, PS, DI, DO>(uni, g32, ph, stream)
+#define AG_H8(O, PS, DI, DO) hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO>), g32, dim3(512), 0, stream, p)
+#define AG_X16(PS, DI, DO) hipLaunchKernelGGL((decode_x16_kernel<PS, DI, DO>), grid, dim3(1024), 0, stream, p)
   if (W == 64 && pass == 0) {
     if (p.rows_w != 64) return hipErrorInvalidValue;
-    if (h8) {
-      if (p.low_rate) AG_H8(0, 0, 0, 0);
-      else if (p.chunk == 32) AG_H8(1, 0, 0, 0);
-      else AG_H8(-1, 0, 0, 0);
-    } else if (pl) {
-      hipLaunchKernelGGL((decode_x16_kernel<true, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
-    } else {
-      hipLaunchKernelGGL((decode_x16_kernel<false, 0, 0, 0>), grid, dim3(1024), 0, stream, p);
-    }
+    if (!pl) AG_X16(0, 0, 0);
+    else if (p.low_rate) AG_H8(0, 0, 0, 0);
+    else if (p.chunk == 32) AG_H8(1, 0, 0, 0);
+    else AG_H8(-1, 0, 0, 0);
   } else if (W == 128 && (pass == 1 || pass == 2)) {
     // the originals must lie in one window half: LowRate k <= 64 (half 0); HighRate chunk 64
-    // (half 1)
+    // (half 1).  Both passes of a decode come from the same kernel family.
     if (p.rows_w != 128 || (p.low_rate ? p.k > 64 : p.chunk != 64)) return hipErrorInvalidValue;
-    if (h8) {
-      // decode_h8 passes (32-column tiles, deferred output multiply): both passes of a decode
-      // must come from the same kernel family
+    if (pl) {
       // LowRate: outputs (originals < 32 when k <= 32) in half 0; HighRate: half 1
       if (p.low_rate && p.k <= 32) {
         if (pass == 1) AG_H8(0, 1, 64, 0);
@@ -2134,21 +1625,18 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
         if (pass == 1) AG_H8(-1, 1, 0, 64);
         else AG_H8(-1, 2, 64, 64);
       }
-#undef AG_H8
-      return hipGetLastError();
+    } else if (p.low_rate) {  // outputs in half 0
+      if (pass == 1) AG_X16(1, 64, 0);
+      else AG_X16(2, 0, 0);
+    } else {                  // outputs in half 1
+      if (pass == 1) AG_X16(1, 0, 64);
+      else AG_X16(2, 64, 64);
     }
-#define AG_DX128(PLV, PS, DI, DO) hipLaunchKernelGGL((decode_x16_kernel<PLV, PS, DI, DO>), grid, dim3(1024), 0, stream, p)
-    if (p.low_rate) {  // outputs in half 0
-      if (pass == 1) { if (pl) AG_DX128(true, 1, 64, 0); else AG_DX128(false, 1, 64, 0); }
-      else { if (pl) AG_DX128(true, 2, 0, 0); else AG_DX128(false, 2, 0, 0); }
-    } else {           // outputs in half 1
-      if (pass == 1) { if (pl) AG_DX128(true, 1, 0, 64); else AG_DX128(false, 1, 0, 64); }
-      else { if (pl) AG_DX128(true, 2, 64, 64); else AG_DX128(false, 2, 64, 64); }
-    }
-#undef AG_DX128
   } else {
     return hipErrorInvalidValue;
   }
+#undef AG_H8
+#undef AG_X16
   return hipGetLastError();
 }
 
@@ -2223,44 +1711,22 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
   const dim3 grid(static_cast<unsigned>(groups));
   switch (kind) {
     // 32-point: xform<4> encodes (it runs at its load/store skeleton's speed), xform8
-    // reconstructs (half the exposed arithmetic per wave: -8% time).  A/B: variant 3 = xform<4>
-    // for both, variant 4 = xform8 for both.
+    // reconstructs (half the exposed arithmetic per wave: -8% time), with the pruned FFT when
+    // every restored original is < 16.
     case XformKind::kEncode32:
-      if (xform_variant() == 4)
-        hipLaunchKernelGGL((xform8_kernel<32, 0>), grid, dim3(512), 0, stream, p);
-      else
-        hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);
+      hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);
       break;
     case XformKind::kDecode32:
-      // variant 5: no output pruning (A/B)
-      if (xform_variant() == 3)
-        hipLaunchKernelGGL((xform_kernel<4, 0, 32>), grid, dim3(256), 0, stream, p);
-      else if (p.out_low_half && xform_variant() != 5)
+      if (p.out_low_half)
         hipLaunchKernelGGL((xform8_kernel<0, 32, true>), grid, dim3(512), 0, stream, p);
       else
         hipLaunchKernelGGL((xform8_kernel<0, 32>), grid, dim3(512), 0, stream, p);
       break;
-    // 64-point: launch_xform16 runs xform_h8 (32-column tiles, lane-linear I/O, two
-    // workgroups per CU; profiles/r03_ab_xform_h8.txt) or xform16 (variant 10; A/B against
-    // xform64h in profiles/r02_ab_xform16.json); variant 7 = xform64h, variant 1 = xform<8>.
+    // 64-point: xform_h8 (32-column tiles, lane-linear I/O, two workgroups per CU)
     case XformKind::kEncode64:
-      if (xform_variant() == 1)
-        hipLaunchKernelGGL((xform_kernel<8, 64, 0>), grid, dim3(512), 0, stream, p);
-      else if (xform_variant() == 7)
-        hipLaunchKernelGGL((xform64h_kernel<64, 0>), dim3(static_cast<unsigned>((p.total_columns + 31) / 32)),
-                           dim3(256), 0, stream, p);
-      else
-        return launch_xform16(64, 0, p, stream);
-      break;
+      return launch_xform64(64, 0, p, stream);
     case XformKind::kDecode64:
-      if (xform_variant() == 1)
-        hipLaunchKernelGGL((xform_kernel<8, 0, 64>), grid, dim3(512), 0, stream, p);
-      else if (xform_variant() == 7)
-        hipLaunchKernelGGL((xform64h_kernel<0, 64>), dim3(static_cast<unsigned>((p.total_columns + 31) / 32)),
-                           dim3(256), 0, stream, p);
-      else
-        return launch_xform16(0, 64, p, stream);
-      break;
+      return launch_xform64(0, 64, p, stream);
     default:
       return hipErrorInvalidValue;
   }
@@ -2321,11 +1787,7 @@ hipError_t launch_restride(const uint8_t* src, uint64_t src_block_stride, uint64
   const uint64_t groups = (per_block * nblocks + 255) / 256;
   if (per_block > 0x7FFFFFFFull || groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
   // tail-only unpack to an even destination (S even: the sizes are whole symbols)
-  static const bool lds_tail = [] {
-    const char* e = std::getenv("AG_RS_TAIL_PIECES");  // A/B: 1 = the per-piece path
-    return !(e && e[0] == '1');
-  }();
-  if (lds_tail && unpack && S > 0 && S < 64 && S % 2 == 0 &&
+  if (unpack && S > 0 && S < 64 && S % 2 == 0 &&
       ((reinterpret_cast<uintptr_t>(dst) | dst_block_stride | dst_shard_stride) & 1) == 0) {
     hipLaunchKernelGGL(unpack_tail_kernel, dim3(static_cast<unsigned>(groups)), dim3(256), 0, stream, p);
     return hipGetLastError();
@@ -2354,8 +1816,3 @@ hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nblocks, uint64_t block_b
 }
 
 }  // namespace ag
-
-extern "C" int ag_rs_internal_set_xform_variant(int v) {
-  ag::g_xform_variant = v;
-  return 0;
-}

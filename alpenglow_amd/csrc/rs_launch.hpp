@@ -28,14 +28,12 @@ struct XformParams {
 
 enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };
 
-// In-process A/B selector of kernel variants (tools/ab_xform.py); 0 = the default kernels.
-int xform_variant();
 
 hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream);
 // True when the bitsliced transform exists for this transform size.
 bool xform_supported(unsigned n);
-// The 64-point transform (xform16): (din, dout) in {(64, 0), (0, 64), (0, 128), (0, 192)}.
-hipError_t launch_xform16(unsigned din, unsigned dout, const XformParams& p, hipStream_t stream);
+// The 64-point transform (xform_h8): (din, dout) in {(64, 0), (0, 64), (0, 128), (0, 192)}.
+hipError_t launch_xform64(unsigned din, unsigned dout, const XformParams& p, hipStream_t stream);
 // LowRate encode, recovery chunk j: out = FFT_n(IFFT_n(in, 0), n * (j + 1)) for
 // n = next_pow2(k) in {32 (j < 4), 64 (j < 3)} -- the crate's LowRate encoder per chunk.
 hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hipStream_t stream);

@@ -156,29 +156,14 @@ __device__ __forceinline__ void lds_get(const uint4* lds, int slot, int lane, ui
 // Streamed shard pieces: read once, written once, so the transform kernels load and store
 // them non-temporally (nt).  Measured on the headline (profiles/r03_nt_ab.txt, two
 // interleaved rounds): encode 5.67 -> 5.81-5.85 TB/s, reconstruct 5.44-5.47 -> 5.89-5.93 TB/s
-// with both; loads alone +1-2 %, stores alone +2-5 %.  AG_NT_LOAD / AG_NT_STORE = 0: the
-// default-policy forms (A/B builds).
-#ifndef AG_NT_LOAD
-#define AG_NT_LOAD 1
-#endif
-#ifndef AG_NT_STORE
-#define AG_NT_STORE 1
-#endif
+// with both; loads alone +1-2 %, stores alone +2-5 %.
 __device__ __forceinline__ uint4 ld_piece(const uint8_t* p) {
-#if AG_NT_LOAD
   const dev::u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const dev::u32x4*>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
-#else
-  return *reinterpret_cast<const uint4*>(p);
-#endif
 }
 __device__ __forceinline__ void st_piece(uint8_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
-#if AG_NT_STORE
   const dev::u32x4 v = {a, b, c, d};
   __builtin_nontemporal_store(v, reinterpret_cast<dev::u32x4*>(p));
-#else
-  *reinterpret_cast<uint4*>(p) = make_uint4(a, b, c, d);
-#endif
 }
 // A tile is 64 consecutive 64-byte chunks (global chunk index g = 64 * tile + c; chunk g
 // is chunk g % C of block g / C, C = chunks per shard).  Each of a lane's four 16-byte
@@ -370,7 +355,7 @@ __device__ __forceinline__ uint32_t qmask_all(const TileIO& io, const uint64_t* 
 using Regs4 = uint32_t[4][16];
 
 // Position bits held by slot bits (S0, S1) and wave bits (W0, W1, W2[, W3]).  W3 < 0: three
-// wave bits (xform8, 32 points); W3 >= 0: sixteen waves (xform16, 64 points).
+// wave bits (xform8, 32 points); W3 >= 0: sixteen waves (decode_x16, 64 points).
 template <int S0, int S1, int W0, int W1, int W2, int W3 = -1>
 struct X8Lay {
   static constexpr int sb[2] = {S0, S1};
@@ -489,7 +474,7 @@ __device__ __forceinline__ void x8_layer(int wave, Regs4& r) {
   if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)], UPD_Y);
   if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)], UPD_Y);
 }
-// the same on an explicit layout type (xform8's pruned FFT layouts, xform16's layouts)
+// the same on an explicit layout type (xform8's pruned FFT layouts, decode_x16's layouts)
 template <typename Lay, int B, bool INV, int DELTA>
 __device__ __forceinline__ void x8_layer_t(int wave, Regs4& r) {
   constexpr int i = Lay::slot_of(B);
@@ -514,11 +499,8 @@ __device__ __forceinline__ void x8_layer_lay(int wave, Regs4& r) {
 // The branches for t and t ^ 2^I have complementary conditions; the asm markers keep
 // LLVM from merging them into one access through a phi of register-array pointers
 // (which would send the whole slot array to scratch).
-// AG_X8_PAIRSYNC: partner waves synchronise through LDS epoch flags instead of workgroup
-// barriers (ready[w] = last swap whose data w has written, done[w] = last swap w has read).
-#ifndef AG_X8_PAIRSYNC
-#define AG_X8_PAIRSYNC 1
-#endif
+// Partner waves synchronise through LDS epoch flags instead of workgroup barriers (ready[w] =
+// last swap whose data w has written, done[w] = last swap w has read).
 template <int NWAVES>
 struct XFlags {
   uint32_t ready[NWAVES];
@@ -536,10 +518,8 @@ template <int I, int J, int EP, int LIVE = 0xF, typename Flags>
 __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, Flags* fl, Regs4& r) {
   const int wj = (wave >> J) & 1;
   const int partner = wave ^ (1 << J);
-#if AG_X8_PAIRSYNC
   // region `partner` was last read by the partner in swap EP - 1
   if constexpr (EP > 1) x8_wait_ge(&fl->done[partner], EP - 1);
-#endif
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     constexpr int k = (t >> (1 - I)) & 1;  // the other slot bit: index within the pair
@@ -548,12 +528,8 @@ __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, Flags* f
       __asm__ volatile("; x8_swap put %0" ::"n"(t));
     }
   });
-#if AG_X8_PAIRSYNC
   x8_signal(&fl->ready[wave], EP, lane);
   x8_wait_ge(&fl->ready[partner], EP);
-#else
-  __syncthreads();
-#endif
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     constexpr int k = (t >> (1 - I)) & 1;
@@ -562,11 +538,7 @@ __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, Flags* f
       __asm__ volatile("; x8_swap get %0" ::"n"(t));
     }
   });
-#if AG_X8_PAIRSYNC
   x8_signal(&fl->done[wave], EP, lane);
-#else
-  __syncthreads();
-#endif
 }
 
 // ---- 32-column tiles with the lane half as a position bit (decode_h8, xform_h8) --------
@@ -647,24 +619,12 @@ __device__ __forceinline__ void quad_exchange(uint32_t* v, int lane) {
   static_for<8>([&](auto D) {
     constexpr int d = decltype(D)::value;
     const uint32_t a = v[d], b = v[8 + d];  // selects, not a pointer choice (keeps v in VGPRs)
-#ifdef AG_QX_SWIZZLE
-    const uint32_t recv = static_cast<uint32_t>(
-        __builtin_amdgcn_ds_swizzle(static_cast<int>(lo ? b : a), 0x804E /* quad mode, perm 2,3,0,1 */));
-#else
     const uint32_t recv = static_cast<uint32_t>(
         __builtin_amdgcn_mov_dpp(static_cast<int>(lo ? b : a), 0x4E /* quad_perm 2,3,0,1 */, 0xF, 0xF, false));
-#endif
     v[d] = lo ? a : recv;
     v[8 + d] = lo ? recv : b;
   });
 }
-
-#ifndef AG_X8_PRIO
-#define AG_X8_PRIO 0
-#endif
-#ifndef AG_X8_WAVES_PER_EU
-#define AG_X8_WAVES_PER_EU 4
-#endif
 
 }  // namespace
 }  // namespace ag

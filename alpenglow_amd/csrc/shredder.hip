@@ -121,6 +121,14 @@ __global__ __launch_bounds__(256) void pipe_merge_kernel(const uint32_t* fresh, 
 
 dim3 grid256(uint64_t n) { return dim3(static_cast<unsigned>((n + 255) / 256)); }
 
+// The lowest `budget` set bits of b: one step per kept bit (the host's window masks do the same,
+// rs_patterns.cpp window64_masks)
+__device__ __forceinline__ uint64_t keep_lowest(uint64_t b, uint32_t budget) {
+  uint64_t keep = 0;
+  for (uint32_t i = 0; i < budget && b; ++i, b &= b - 1) keep |= b & (~b + 1);
+  return keep;
+}
+
 // ANY_K survivors of one slice's kept shreds in the W = 64 window (decode_device's rule).
 __global__ __launch_bounds__(256) void pipe_patterns_kernel(const uint64_t* __restrict__ present, uint64_t n,
                                                             uint64_t* __restrict__ xm, uint8_t* __restrict__ few) {
@@ -132,8 +140,7 @@ __global__ __launch_bounds__(256) void pipe_patterns_kernel(const uint64_t* __re
   const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(pr));
   uint64_t in = 0, out = 0, e = 0;
   if (cnt >= kPipeData && ob != 0xFFFFFFFFull) {
-    const uint32_t budget = kPipeData - static_cast<uint32_t>(__builtin_popcountll(ob));
-    while (static_cast<uint32_t>(__builtin_popcountll(rb)) > budget) rb &= ~(uint64_t{1} << (63 - __builtin_clzll(rb)));
+    rb = keep_lowest(rb, kPipeData - static_cast<uint32_t>(__builtin_popcountll(ob)));
     in = rb | (ob << 32);
     out = (~ob & 0xFFFFFFFFull) << 32;
     e = (~rb & 0xFFFFFFFFull) | out;
@@ -159,8 +166,7 @@ __global__ __launch_bounds__(256) void pipe_patterns128_kernel(const uint64_t* _
   const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(p0) + __builtin_popcountll(p1));
   uint64_t e0 = 0, e1 = 0, in0 = 0, in1 = 0, out0 = 0;
   if (cnt >= kPipeData && ob != 0xFFFFFFFFull) {
-    const uint32_t budget = kPipeData - static_cast<uint32_t>(__builtin_popcountll(ob));
-    while (static_cast<uint32_t>(__builtin_popcountll(rb)) > budget) rb &= ~(uint64_t{1} << (63 - __builtin_clzll(rb)));
+    rb = keep_lowest(rb, kPipeData - static_cast<uint32_t>(__builtin_popcountll(ob)));
     in0 = ob | ((rb & 0xFFFFFFFFull) << 32);
     in1 = rb >> 32;
     out0 = ~ob & 0xFFFFFFFFull;

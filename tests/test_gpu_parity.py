@@ -203,36 +203,30 @@ def test_fast_decode_64_point(ctx, dev, erased):
     assert np.array_equal(got, blocks)
 
 
-@pytest.mark.parametrize("variant", [7, 9, 10])
-def test_transform64_kernel_variants(ctx, dev, variant):
-    """The 64-point transform's A/B kernels (7 = xform64h, 9 = xform_h8 on 32-column tiles --
-    the default the other tests run --, 10 = xform16 on 64-column tiles): HighRate encodes
-    with next_pow2(m) = 64, LowRate 64-point chunk encodes and full-recovery decodes with
-    per-block store masks, bit-exact against the C oracle."""
-    lib = rs.load()
-    lib.ag_rs_internal_set_xform_variant(variant)
-    try:
-        for k, m, S, n in [(64, 64, 2048, 7), (33, 64, 192, 5), (48, 60, 192, 3), (40, 128, 128, 4),
-                           (64, 192, 64, 3)]:
-            blocks = np.stack([np.frombuffer(o.block_bytes(4000 + variant + b, k * S), np.uint8).reshape(k, S)
-                               for b in range(n)])
-            assert np.array_equal(gpu_encode(ctx, dev, blocks, m), ro_c.encode_blocks(blocks, m, threads=8)), (k, m)
-        k, m, S, n = 64, 64, 1024, 9
-        rng = random.Random(variant)
-        blocks = np.stack([np.frombuffer(o.block_bytes(4100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
-        rec = ro_c.encode_blocks(blocks, m, threads=8)
-        for per_block in (False, True):
-            op = []
-            for b in range(n):
-                lost = set(rng.sample(range(k), rng.randrange(1, 64))) if per_block or b == 0 else lost
-                op.append([0 if i in lost else 1 for i in range(k)])
-            damaged = blocks.copy()
-            damaged[np.array(op) == 0] = 0x5A
-            flat = [x for row in op for x in row] if per_block else op[0]
-            got = gpu_decode(ctx, dev, damaged, rec, flat, [1] * m * (n if per_block else 1), rs.DECODE_ANY_K)
-            assert np.array_equal(got, blocks), per_block
-    finally:
-        lib.ag_rs_internal_set_xform_variant(0)
+@pytest.mark.parametrize("seed", [0, 1])
+def test_transform64_geometries(ctx, dev, seed):
+    """The 64-point transform (xform_h8): HighRate encodes with next_pow2(m) = 64, LowRate
+    64-point chunk encodes and full-recovery decodes with per-block store masks, bit-exact
+    against the C oracle."""
+    for k, m, S, n in [(64, 64, 2048, 7), (33, 64, 192, 5), (48, 60, 192, 3), (40, 128, 128, 4),
+                       (64, 192, 64, 3)]:
+        blocks = np.stack([np.frombuffer(o.block_bytes(4000 + 9 * seed + b, k * S), np.uint8).reshape(k, S)
+                           for b in range(n)])
+        assert np.array_equal(gpu_encode(ctx, dev, blocks, m), ro_c.encode_blocks(blocks, m, threads=8)), (k, m)
+    k, m, S, n = 64, 64, 1024, 9
+    rng = random.Random(seed)
+    blocks = np.stack([np.frombuffer(o.block_bytes(4100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    for per_block in (False, True):
+        op = []
+        for b in range(n):
+            lost = set(rng.sample(range(k), rng.randrange(1, 64))) if per_block or b == 0 else lost
+            op.append([0 if i in lost else 1 for i in range(k)])
+        damaged = blocks.copy()
+        damaged[np.array(op) == 0] = 0x5A
+        flat = [x for row in op for x in row] if per_block else op[0]
+        got = gpu_decode(ctx, dev, damaged, rec, flat, [1] * m * (n if per_block else 1), rs.DECODE_ANY_K)
+        assert np.array_equal(got, blocks), per_block
 
 
 @pytest.mark.parametrize("k,S,low", [(32, 2048, False), (64, 2048, False), (64, 1024, False), (64, 2048, True)])

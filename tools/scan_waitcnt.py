@@ -38,7 +38,7 @@ def scan(asm: str):
 
 
 def main():
-    srcs = sys.argv[1:] or ["rs_kernels.hip", "rs_xform16.hip", "rs_decode_c.hip"]
+    srcs = sys.argv[1:] or ["rs_kernels.hip", "rs_xform64.hip", "rs_decode_c.hip"]
     with tempfile.TemporaryDirectory() as d:
         for src in srcs:
             s = os.path.join(d, os.path.basename(src) + ".s")

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
-"""Repeat the 64-point transform decode with per-block store masks (test_transform64_kernel_
-variants' per-block case) many times in one process, per kernel variant, and report every
-mismatch (block, shard, first differing chunk) -- an intermittent-result hunt, no faults.
+"""Repeat the 64-point transform decode with per-block store masks (test_transform64_geometries'
+per-block case) many times in one process and report every mismatch (block, shard, first
+differing chunk) -- an intermittent-result hunt, no faults.  AG_RS_LIB_NAME selects another
+build of the library in alpenglow_amd/_lib (e.g. a diagnostic build of an older kernel).
 
-Usage: python tools/stress_xform64.py [--variants 9,10] [--iters 40] [--n 9] [--S 1024]
+Usage: python tools/stress_xform64.py [--iters 40] [--n 9] [--S 1024] [--seed 9]
 """
 import argparse
 import os
@@ -16,7 +17,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "oracle")]
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--variants", default="9,10")
+    ap.add_argument("--seed", type=int, default=9)
     ap.add_argument("--iters", type=int, default=40)
     ap.add_argument("--n", type=int, default=9)
     ap.add_argument("--S", type=int, default=1024)
@@ -28,7 +29,7 @@ def main():
     import rs_oracle as o
     from alpenglow_amd import rs
 
-    lib = rs.load()
+    rs.load()
     dev = torch.device("cuda:0")
     ctx = rs.Context(0)
     st = torch.cuda.Stream(dev)
@@ -39,8 +40,7 @@ def main():
     rec = ro_c.encode_blocks(blocks, m, threads=8)
     d_rec = torch.from_numpy(rec.reshape(n, m * S).copy()).to(dev)
     bad = {}
-    for v in [int(x) for x in args.variants.split(",")]:
-        lib.ag_rs_internal_set_xform_variant(v)
+    for v in [args.seed]:
         rng = random.Random(v)
         bad[v] = 0
         for it in range(args.iters):
@@ -59,7 +59,7 @@ def main():
                 bad[v] += 1
                 diff = np.argwhere(got != blocks)
                 shards = sorted({(int(b), int(s)) for b, s, _ in diff})
-                print(f"variant {v} iter {it}: {len(diff)} bytes differ in {len(shards)} shards, "
+                print(f"seed {v} iter {it}: {len(diff)} bytes differ in {len(shards)} shards, "
                       f"first {shards[:6]}, chunks {sorted({int(x) // 64 for _, _, x in diff})[:8]}, "
                       f"erased? {[bool(opa[b, s] == 0) for b, s in shards[:6]]}", flush=True)
                 if bad[v] <= 3:  # (chunk, 16-byte quarter) map of the first bad shard: '#' differs
@@ -80,7 +80,6 @@ def main():
                     print(f"   {len(badp)} bad pieces: {fill} hold the 0x5A fill; first as pieces of "
                           f"(block, shard, chunk, quarter): {where} (wanted chunk/quarter {[(pi // 4, pi % 4) for pi in badp[:6]]})",
                           flush=True)
-    lib.ag_rs_internal_set_xform_variant(0)
     print({"mismatching_iterations": bad, "iters": args.iters, "n": n, "S": S})
 
 
