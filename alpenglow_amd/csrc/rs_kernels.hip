@@ -131,8 +131,7 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
     using H1 = X8Lay<4, 1, 0, 2, 3>;
     using H0 = X8Lay<4, 0, 1, 2, 3>;
     static_assert(std::is_same_v<H3, X8Layout<3>>, "H3 is layout L3");
-    x8_layer<3, 4, true, DIN>(wave, r);
-    x8_layer<3, 4, false, DOUT, 0x5, false>(wave, r);
+    x8_layer_fused<X8Layout<3>, 4, DIN, DOUT, false>(r);  // IFFT b4 + FFT b4 (x only)
     x8_layer_lay<H3, 3, DOUT, 0x5>(wave, r);
     x8_swap<1, 2, 4, 0x5>(wave, lane, lds, &flags, r);
     x8_layer_lay<H2, 2, DOUT, 0x5>(wave, r);
@@ -160,8 +159,7 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
     });
     return;
   }
-  x8_layer<3, 4, true, DIN>(wave, r);
-  x8_layer<3, 4, false, DOUT>(wave, r);
+  x8_layer_fused<X8Layout<3>, 4, DIN, DOUT>(r);  // IFFT b4 + FFT b4
   x8_layer<3, 3, false, DOUT>(wave, r);
   x8_swap<0, 2, 4>(wave, lane, lds, &flags, r);
   x8_layer<2, 2, false, DOUT>(wave, r);

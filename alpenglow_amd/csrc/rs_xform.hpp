@@ -112,10 +112,27 @@ __device__ __forceinline__ void xf_pass_b_fft(Regs8& r) {
     });
   });
 }
+// IFFT layers, the top one fused with the FFT's first (dev::fused_bfly), FFT layers.
 template <int NW, int DIN, int DOUT>
 __device__ __forceinline__ void xf_pass_b(Regs8& r) {
-  xf_pass_b_ifft<NW, DIN>(r);
-  xf_pass_b_fft<NW, DOUT>(r);
+  constexpr int NL = PassB<NW>::kLayers;
+  static_for<NL - 1>([&](auto L) {  // ascending distance, below the top
+    static_for<4>([&](auto I) {
+      using P = typename PassB<NW>::template Pair<decltype(L)::value, decltype(I)::value>;
+      dev::ifft_bfly<P::g + P::d + DIN - 1>(r[P::t], r[P::u]);
+    });
+  });
+  static_for<4>([&](auto I) {
+    using P = typename PassB<NW>::template Pair<NL - 1, decltype(I)::value>;
+    static_assert(P::g == 0, "the top layer is one group");
+    dev::fused_bfly<P::d + DIN - 1, P::d + DOUT - 1>(r[P::t], r[P::u]);
+  });
+  static_for<NL - 1>([&](auto L) {  // descending distance, below the top
+    static_for<4>([&](auto I) {
+      using P = typename PassB<NW>::template Pair<NL - 2 - decltype(L)::value, decltype(I)::value>;
+      dev::fft_bfly<P::g + P::d + DOUT - 1>(r[P::t], r[P::u]);
+    });
+  });
 }
 
 template <int NW, int DOUT>
@@ -474,6 +491,21 @@ __device__ __forceinline__ void x8_layer(int wave, Regs4& r) {
   if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)], UPD_Y);
   if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)], UPD_Y);
 }
+// The top layer B of FFT_DOUT(IFFT_DIN(.)) as fused butterflies (dev::fused_bfly): no wave bit
+// lies above the top bit, so the constant is the same in every wave.  UPD_Y false: the FFT's
+// y ^= x is skipped (the pruned FFTs need only x).
+template <typename Lay, int B, int DIN, int DOUT, bool UPD_Y = true>
+__device__ __forceinline__ void x8_layer_fused(Regs4& r) {
+  constexpr int i = Lay::slot_of(B);
+  static_assert(i >= 0, "layer bit must be a slot bit");
+  static_assert(Lay::rel(B) == 0, "the fused layer is the top one");
+  constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;
+  constexpr int g0 = Lay::pos(0, t0) & ~((2 << B) - 1), g1 = Lay::pos(0, t1) & ~((2 << B) - 1);
+  static_assert(g0 == 0 && g1 == 0, "the top layer is one group");
+  dev::fused_bfly<(1 << B) + DIN - 1, (1 << B) + DOUT - 1, UPD_Y>(r[t0], r[t0 | (1 << i)]);
+  dev::fused_bfly<(1 << B) + DIN - 1, (1 << B) + DOUT - 1, UPD_Y>(r[t1], r[t1 | (1 << i)]);
+}
+
 // the same on an explicit layout type (xform8's pruned FFT layouts, decode_x16's layouts)
 template <typename Lay, int B, bool INV, int DELTA>
 __device__ __forceinline__ void x8_layer_t(int wave, Regs4& r) {
