@@ -822,6 +822,7 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
     p.chunks_per_shard = static_cast<uint32_t>(cps);
     p.total_columns = static_cast<uint64_t>(nblocks) * cps;
     p.rows_w = static_cast<uint32_t>(xw);
+    p.any_k = mode == AG_RS_DECODE_ANY_K ? 1u : 0u;
     uint64_t ntiles;
     if (npat == 1) {
       ntiles = (p.total_columns + 63) / 64;
@@ -1478,6 +1479,17 @@ namespace {
 // One codeword through the device, zero-copy: the kernels read the originals from and
 // write the recovery shards to mapped pinned host memory (a 32-shard slice is 32 KiB each
 // way; two DMA copies and their scheduling cost more than the kernel's PCIe accesses).
+// The single-codeword calls (one slice per call, the reference's pattern) wait for their
+// microseconds of device work by polling the stream: hipStreamSynchronize's blocking wait
+// added ~9 us per call over the kernel time (profiles/r04_call_latency_hip_api_stats.csv).
+int spin_sync(ag_rs_ctx* c) {
+  for (;;) {
+    const hipError_t e = hipStreamQuery(c->stream);
+    if (e == hipSuccess) return AG_RS_OK;
+    if (e != hipErrorNotReady) return AG_RS_ERR_DEVICE;
+  }
+}
+
 int run_one_encode(ag_rs_ctx* c, size_t k, size_t m, size_t S, const uint8_t* orig, uint8_t* rec) {
   int st;
   if ((st = c->enter())) return st;
@@ -1487,7 +1499,7 @@ int run_one_encode(ag_rs_ctx* c, size_t k, size_t m, size_t S, const uint8_t* or
   uint8_t* pd = c->one_pin.dev<uint8_t>();
   std::memcpy(pin, orig, ob);
   if ((st = encode_device(c, k, m, S, 1, pd, ob, pd + ob, rb))) return st;
-  AG_HIP(hipStreamSynchronize(c->stream));
+  if ((st = spin_sync(c))) return st;
   std::memcpy(rec, pin + ob, rb);
   return AG_RS_OK;
 }
@@ -1520,7 +1532,7 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, uint8_t* orig, co
   const bool reuse = coding && present == k && nr == m;
   if ((st = decode_device(c, k, m, S, 1, pd, ob, pd + ob, rb, opres, rpres, 1, mode))) return st;
   if (coding && !reuse && (st = encode_device(c, k, m, S, 1, pd, ob, pd + ob + rb, rb))) return st;
-  AG_HIP(hipStreamSynchronize(c->stream));
+  if ((st = spin_sync(c))) return st;
   std::memcpy(orig, pin, ob);
   if (coding) std::memcpy(coding, reuse ? rec : pin + ob + rb, rb);
   return AG_RS_OK;
@@ -2513,6 +2525,7 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   p.total_columns = static_cast<uint64_t>(n) * cps;
   p.per_lane = 1;
   p.rows_w = static_cast<uint32_t>(W);
+  p.any_k = 1;  // launch_pipe_patterns keeps exactly k survivors
   if (ag::launch_decode_x(static_cast<unsigned>(W), 0, p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   int64_t* strip = c->d_strip.as<int64_t>();

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
       const uint8_t* base = p.in + sh * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(base + io.off[q]);
+        const uint4 x = ld_piece_if(base + io.off[q], (io.valid >> q) & 1);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
       const uint8_t* base = is_rec ? p.rec + (g - rpos) * p.rec_shard_stride : p.orig + (g - opos) * p.orig_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(base + (is_rec ? io_r.off[q] : io_o.off[q]));
+        const uint4 x = ld_piece_if(base + (is_rec ? io_r.off[q] : io_o.off[q]), (io_r.valid >> q) & 1);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -790,6 +790,268 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   });
 }
 
+// =====================================================================================
+// decode_pk<OUTH>: decode_h8's W = 64 window for per-slice patterns on 1 KiB shreds (16 chunks
+// per shard: a 32-column tile is two slices) with the locator products packed.  In decode_h8 a
+// wave-slot holds four 16-lane groups -- two slices x two positions (lane half) -- and runs the
+// per-lane Horner product when ANY group's position is present: with random 32-of-64 arrival
+// that is ~94 % of the slots where 50 % carry data, and likewise for the restored outputs.
+// Here the products run on packed items instead (item = one slice's 16 columns of one position,
+// 1 KiB):
+//   1. the workgroup ranks each slice's survivors and restored positions (LDS lists);
+//   2. item i of the survivors (i < 64: ANY_K keeps at most 32 per slice) is loaded by row
+//      group i & 3 of slot (i >> 2) & 1 of wave i >> 3, bitsliced, multiplied by its locator
+//      constant and written to the 64 KiB exchange buffer;
+//   3. every lane reads its layout-A slots from there (absent positions are zero) and the
+//      transform runs as decode_h8's (swaps, derivative, the half-pruned FFT);
+//   4. the live waves write their restored positions' values as packed items, and each item is
+//      multiplied, converted to bytes and stored by one row group.
+// Survivor and restored counts bound the product work instead of the slot count: per 2-slice
+// tile 64 input items on 16 wave-slots (decode_h8: ~30 of 32) and the restored items on the
+// live waves' 16 wave-slots.  OUTH: the window half of the restored originals (1 HighRate chunk
+// 32, 0 the LowRate sub-window); only those geometries launch it.  Requires any_k (at most k
+// survivors per pattern) and 16 chunks per shard.
+// =====================================================================================
+template <int OUTH>
+__global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p) {
+  static_assert(OUTH == 0 || OUTH == 1, "the restored originals lie in one window half");
+  using LB = X8Lay<2, 1, 3, 4, 5>;
+  using LC = X8Lay<2, 3, 1, 4, 5>;
+  using LD = X8Lay<4, 3, 1, 2, 5>;
+  using LE = X8Lay<4, 5, 1, 2, 3>;
+  constexpr int W = 64, kSl = 16;           // positions, columns per slice
+  constexpr int D = 2;                      // derivative epochs 4, 5; FFT swaps 4 + D ..
+  __shared__ uint4 lds[16 * 4 * kXfLanes];  // 64 KiB: packed items ([item][q][16 lanes]) or swap regions
+  __shared__ X8Flags flags;
+  __shared__ uint32_t lcoef[2 * W];         // the two slices' locator constants (polynomial basis)
+  __shared__ uint64_t smask[2][2];          // per slice: positions present (loaded), restored
+  __shared__ uint8_t ilist[2][W], olist[2][W];  // per slice: survivor / restored positions by rank
+  const int lane = threadIdx.x & 63;
+  const int h = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
+  const uint64_t sb0 = static_cast<uint64_t>(tile) * 2;  // the tile's first slice (block)
+  const uint64_t nblk = p.total_columns / kSl;
+  const uint32_t opos = p.low_rate ? 0 : p.chunk, rpos = p.low_rate ? p.chunk : 0;
+  if (threadIdx.x < 2 * W) {
+    const uint32_t sl = threadIdx.x >> 6, j = threadIdx.x & 63;
+    uint64_t im = 0, om = 0;
+    if (sb0 + sl < nblk) {
+      im = p.pmask[2 * (sb0 + sl)];
+      om = p.pmask[2 * (sb0 + sl) + 1];
+      if (((im | om) >> j) & 1) lcoef[threadIdx.x] = p.rows[(sb0 + sl) * p.rows_w + j];
+    }
+    const uint64_t below = (uint64_t{1} << j) - 1;
+    if ((im >> j) & 1) ilist[sl][__builtin_popcountll(im & below)] = static_cast<uint8_t>(j);
+    if ((om >> j) & 1) olist[sl][__builtin_popcountll(om & below)] = static_cast<uint8_t>(j);
+    if (j == 0) {
+      smask[sl][0] = im;
+      smask[sl][1] = om;
+    }
+  }
+  if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t imA = smask[0][0], imB = smask[1][0], omA = smask[0][1], omB = smask[1][1];
+  const uint32_t nA = static_cast<uint32_t>(__builtin_popcountll(imA));
+  const uint32_t nin = nA + static_cast<uint32_t>(__builtin_popcountll(imB));
+  const uint32_t noA = static_cast<uint32_t>(__builtin_popcountll(omA));
+  const uint32_t nout = noA + static_cast<uint32_t>(__builtin_popcountll(omB));
+  if (nout == 0) return;  // nothing restored in either slice (workgroup-uniform)
+  const int col = lane & 15, row = lane >> 4;
+  // the byte offset of position g's shard of slice sl, column col (recovery shards below the
+  // originals in HighRate)
+  auto src_of = [&](uint32_t sl, uint32_t g) -> const uint8_t* {
+    const bool is_rec = p.low_rate ? g >= p.chunk : g < p.chunk;
+    const uint64_t blk = sb0 + sl;
+    return is_rec ? p.rec + (g - rpos) * p.rec_shard_stride + blk * p.rec_block_stride + col * 64
+                  : p.orig + (g - opos) * p.orig_shard_stride + blk * p.orig_block_stride + col * 64;
+  };
+  // 2. packed input products: item i on row group i & 3 of slot (i >> 2) & 1 of wave i >> 3
+  static_for<2>([&](auto U) {
+    constexpr int u = decltype(U)::value;
+    if (static_cast<uint32_t>(wave * 8 + u * 4) < nin) {  // wave-uniform
+      const uint32_t i = wave * 8 + u * 4 + row;
+      const bool ok = i < nin;
+      const uint32_t sl = i < nA ? 0u : 1u;
+      const uint32_t j = ok ? ilist[sl][i - (sl ? nA : 0u)] : 0u;
+      uint32_t v[16];
+      if (ok) {
+        const uint8_t* src = src_of(sl, j);
+        static_for<4>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          const uint4 x = ld_piece(src + 16 * q);
+          v[4 * q] = x.x;
+          v[4 * q + 1] = x.y;
+          v[4 * q + 2] = x.z;
+          v[4 * q + 3] = x.w;
+        });
+      } else {
+        static_for<16>([&](auto P) { v[decltype(P)::value] = 0; });
+      }
+      dev::planes_from_raw(v);
+      dev::mul_rt_poly(v, lcoef[sl * W + j]);
+      if (ok) {
+        static_for<4>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          lds[(i * 4 + q) * kSl + col] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        });
+      }
+    }
+  });
+  __syncthreads();
+  // 3. layout A from the packed items: lane column c = lane & 31 (slice c >> 4), slot t holds
+  // position t | h << 2 | wave << 3
+  const uint32_t lsl = static_cast<uint32_t>((lane & 31) >> 4);
+  const uint64_t in_mask = lsl ? imB : imA, out_mask = lsl ? omB : omA;
+  auto posA = [&](int t) -> uint32_t {
+    return static_cast<uint32_t>((t & 1) | ((t >> 1) << 1) | (h << 2) | (wave << 3));
+  };
+  Regs4 r;
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = posA(t);
+    if ((in_mask >> j) & 1) {
+      const uint32_t i = static_cast<uint32_t>(__builtin_popcountll(in_mask & ((uint64_t{1} << j) - 1))) + (lsl ? nA : 0u);
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = lds[(i * 4 + q) * kSl + col];
+        r[t][4 * q] = x.x;
+        r[t][4 * q + 1] = x.y;
+        r[t][4 * q + 2] = x.z;
+        r[t][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { r[t][decltype(P)::value] = 0; });
+    }
+  });
+  __syncthreads();  // every item read: the buffer becomes the swap regions
+  // IFFT_64
+  h8_layer0<true, 0>(wave, h, r);
+  h8_relayout(r);
+  x8_layer_t<LB, 1, true, 0>(wave, r);
+  x8_layer_t<LB, 2, true, 0>(wave, r);
+  x8_swap<1, 0, 1>(wave, lane, lds, &flags, r);
+  x8_layer_t<LC, 3, true, 0>(wave, r);
+  x8_swap<0, 1, 2>(wave, lane, lds, &flags, r);
+  x8_layer_t<LD, 4, true, 0>(wave, r);
+  x8_swap<1, 2, 3>(wave, lane, lds, &flags, r);
+  x8_layer_t<LE, 5, true, 0>(wave, r);
+  // formal derivative in E (decode_h8's, epochs 4 and 5)
+  auto wait_readers = [&](int x, uint32_t e) __attribute__((always_inline)) {
+    static_for<3>([&](auto Bb) {
+      constexpr int b = decltype(Bb)::value;
+      if ((x >> b) & 1) x8_wait_ge(&flags.done[x & ~(1 << b)], e);
+    });
+  };
+  static_for<2>([&](auto Rho) {
+    constexpr int rho = decltype(Rho)::value;
+    constexpr uint32_t e = 4 + rho;
+    if constexpr (rho == 1) wait_readers(wave, e - 1);
+    static_for<2>([&](auto U) { lds_put(lds, 2 * wave + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+    x8_signal(&flags.ready[wave], e, lane);
+    static_for<2>([&](auto U) {
+      constexpr int t = 2 * rho + decltype(U)::value;
+      uint32_t hi[16];
+      static_for<16>([&](auto P) {
+        constexpr int q = decltype(P)::value;
+        hi[q] = __builtin_amdgcn_permlane32_swap(r[t][q], 0u, false, false)[1];
+      });
+      if constexpr (!(t & 1)) dev::xor_planes(r[t], r[t | 1]);
+      if constexpr (!(t & 2)) dev::xor_planes(r[t], r[t | 2]);
+      dev::xor_planes(r[t], hi);
+    });
+    static_for<3>([&](auto Bb) {
+      constexpr int b = decltype(Bb)::value;
+      if (!((wave >> b) & 1)) {
+        const int pw = wave | (1 << b);
+        x8_wait_ge(&flags.ready[pw], e);
+        static_for<2>([&](auto U) { lds_get_xor(lds, 2 * pw + decltype(U)::value, lane, r[2 * rho + decltype(U)::value]); });
+      }
+    });
+    x8_signal(&flags.done[wave], e, lane);
+  });
+  // FFT_64 down to A; the waves of the other window half hand over their live slots and retire
+  x8_layer_t<LE, 5, false, 0>(wave, r);
+  x8_layer_t<LE, 4, false, 0>(wave, r);
+  wait_readers(wave ^ 4, 5);
+  {
+    const int partner = wave ^ 4;
+    if (((wave >> 2) & 1) != OUTH) {
+      x8_wait_ge(&flags.done[partner], 3 + D);
+      static_for<4>([&](auto T) {
+        constexpr int t = decltype(T)::value;
+        if constexpr (((t >> 1) & 1) == OUTH) {
+          lds_put(lds, 2 * partner + (t & 1), lane, r[t]);
+          __asm__ volatile("; pk put %0" ::"n"(t));
+        }
+      });
+      x8_signal(&flags.ready[wave], 4 + D, lane);
+      return;
+    }
+    x8_wait_ge(&flags.ready[partner], 4 + D);
+    static_for<4>([&](auto T) {
+      constexpr int t = decltype(T)::value;
+      if constexpr (((t >> 1) & 1) != OUTH) {
+        lds_get(lds, 2 * wave + (t & 1), lane, r[t]);
+        __asm__ volatile("; pk get %0" ::"n"(t));
+      }
+    });
+    x8_signal(&flags.done[wave], 4 + D, lane);
+  }
+  x8_layer_t<LD, 3, false, 0>(wave, r);
+  x8_swap<0, 1, 5 + D>(wave, lane, lds, &flags, r);
+  x8_layer_t<LC, 2, false, 0>(wave, r);
+  x8_swap<1, 0, 6 + D>(wave, lane, lds, &flags, r);
+  x8_layer_t<LB, 1, false, 0>(wave, r);
+  h8_relayout(r);
+  h8_layer0<false, 0>(wave, h, r);
+  // 4. packed output products.  Every live wave's last swap read is done before any item
+  // overwrites a region; items written, then every live wave's items visible before reads.
+  const int lw = wave & 3;  // live waves: wave bit 2 == OUTH
+  static_for<4>([&](auto Wv) {
+    constexpr int w2 = decltype(Wv)::value;
+    x8_wait_ge(&flags.done[w2 | (OUTH << 2)], 6 + D);
+  });
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    const uint32_t j = posA(t);
+    if ((out_mask >> j) & 1) {
+      const uint32_t o = static_cast<uint32_t>(__builtin_popcountll(out_mask & ((uint64_t{1} << j) - 1))) + (lsl ? noA : 0u);
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        lds[(o * 4 + q) * kSl + col] = make_uint4(r[t][4 * q], r[t][4 * q + 1], r[t][4 * q + 2], r[t][4 * q + 3]);
+      });
+    }
+  });
+  x8_signal(&flags.ready[wave], 7 + D, lane);
+  static_for<4>([&](auto Wv) {
+    constexpr int w2 = decltype(Wv)::value;
+    x8_wait_ge(&flags.ready[w2 | (OUTH << 2)], 7 + D);
+  });
+  // item o on row group o & 3 of slot (o >> 2) & 3 of live wave o >> 4
+  static_for<4>([&](auto U) {
+    constexpr int u = decltype(U)::value;
+    if (static_cast<uint32_t>(lw * 16 + u * 4) < nout) {  // wave-uniform
+      const uint32_t o = lw * 16 + u * 4 + row;
+      if (o < nout) {
+        const uint32_t sl = o < noA ? 0u : 1u;
+        const uint32_t j = olist[sl][o - (sl ? noA : 0u)];
+        uint32_t v[16];
+        static_for<4>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          const uint4 x = lds[(o * 4 + q) * kSl + col];
+          v[4 * q] = x.x;
+          v[4 * q + 1] = x.y;
+          v[4 * q + 2] = x.z;
+          v[4 * q + 3] = x.w;
+        });
+        dev::mul_rt_poly(v, lcoef[sl * W + j]);
+        dev::store_chunk<true>(const_cast<uint8_t*>(src_of(sl, j)), v);
+      }
+    }
+  });
+}
+
 // Per pattern and window position x: the decoder's locator constant as a bitsliced
 // multiply matrix.  loc(x) = sum_{e erased, e != x} log(x ^ e) (mod 65535) -- the crate's
 // eval_poly over the window up to one constant factor, which cancels between the input
@@ -858,7 +1120,7 @@ __device__ __forceinline__ void mc_load(const XformParams& p, const TileIO& io, 
       const uint8_t* base = p.in + (s0 + t) * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(base + io.off[q]);
+        const uint4 x = ld_piece_if(base + io.off[q], (io.valid >> q) & 1);
         raw[t][4 * q] = x.x;
         raw[t][4 * q + 1] = x.y;
         raw[t][4 * q + 2] = x.z;
@@ -950,7 +1212,7 @@ __device__ __forceinline__ void syn_load(const DecodeSynParams& p, const TileIO&
       const uint8_t* base = p.orig + s * p.orig_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(base + io.off[q]);
+        const uint4 x = ld_piece_if(base + io.off[q], (io.valid >> q) & 1);
         raw[t][4 * q] = x.x;
         raw[t][4 * q + 1] = x.y;
         raw[t][4 * q + 2] = x.z;
@@ -1603,7 +1865,11 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
 #define AG_X16(PS, DI, DO) hipLaunchKernelGGL((decode_x16_kernel<PS, DI, DO>), grid, dim3(1024), 0, stream, p)
   if (W == 64 && pass == 0) {
     if (p.rows_w != 64) return hipErrorInvalidValue;
-    if (!pl) AG_X16(0, 0, 0);
+    const bool packed = pl && p.any_k && p.chunks_per_shard == 16 && (p.low_rate || p.chunk == 32);
+    if (packed) {
+      if (p.low_rate) hipLaunchKernelGGL((decode_pk_kernel<0>), g32, dim3(512), 0, stream, p);
+      else hipLaunchKernelGGL((decode_pk_kernel<1>), g32, dim3(512), 0, stream, p);
+    } else if (!pl) AG_X16(0, 0, 0);
     else if (p.low_rate) AG_H8(0, 0, 0, 0);
     else if (p.chunk == 32) AG_H8(1, 0, 0, 0);
     else AG_H8(-1, 0, 0, 0);

@@ -152,6 +152,7 @@ struct DecodeXParams {
   uint32_t chunks_per_shard;
   uint64_t total_columns;  // batch blocks * chunks_per_shard
   uint32_t rows_w;         // constants per pattern in rows (W = 64: 64; W = 128: 128)
+  uint32_t any_k;          // 1: every pattern loads at most k survivors (ANY_K; the packed kernel)
 };
 // W = 32 / 64: pass 0.  W = 128: pass 1 (the other half's inputs, raw partial outputs), then
 // pass 2 (the output half's inputs, the partial added, output multiply); masks per pass.

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
       const uint8_t* base = p.in + s * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(base + io.off[q]);
+        const uint4 x = ld_piece_if(base + io.off[q], (io.valid >> q) & 1);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;

@@ -866,6 +866,37 @@ def test_decode_per_slice_random_patterns(ctx, dev, S, n, mode):
     assert np.array_equal(got, blocks)
 
 
+@pytest.mark.parametrize("k,m,n", [(32, 32, 25), (32, 32, 64), (32, 64, 11), (20, 40, 9)])
+def test_packed_window64_follower(ctx, dev, k, m, n):
+    """decode_pk (the W = 64 window with packed locator products) on 1 KiB shreds, ANY_K: the
+    follower's random 32-of-64 arrival (exactly k survivors, the device-pattern path's shape),
+    slices with every data shred present, slices that lost only coding shreds, an odd slice
+    count (a one-slice last tile) and the LowRate sub-window (32:64, 20:40), against the
+    original data.  Every lost shred's bytes are overwritten first."""
+    S = 1024
+    rng = random.Random(k * 7 + m + n)
+    blocks = np.stack([np.frombuffer(o.block_bytes(5100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    d_o, d_r, op, rp = blocks.copy(), rec.copy(), [], []
+    pool = k + m if k > m else k + min(m, 32)
+    for b in range(n):
+        keep = set(rng.sample(range(pool), k))
+        if b % 5 == 3:
+            keep = set(range(k)) | set(rng.sample(range(k, pool), 3))  # nothing to restore
+        if b % 7 == 5:
+            keep = set(range(k + min(m, 32)))  # every shard inside the window
+        op += [1 if i in keep else 0 for i in range(k)]
+        rp += [1 if k + j in keep else 0 for j in range(m)]
+        for i in range(k):
+            if i not in keep:
+                d_o[b, i] = 0x3C
+        for j in range(m):
+            if k + j not in keep:
+                d_r[b, j] = 0xC3
+    got = gpu_decode(ctx, dev, d_o, d_r, op, rp, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
+
+
 @pytest.mark.parametrize("k,m", [(32, 32), (32, 64), (32, 33), (40, 16), (48, 8), (20, 40)])
 @pytest.mark.parametrize("S,n", [(1024, 24), (64, 70), (192, 23)])
 @pytest.mark.parametrize("mode", [rs.DECODE_ANY_K, rs.DECODE_EXACT])

@@ -1,0 +1,88 @@
+// Per-call latency of the crate-API route (INTEGRATION.md Route A) without an interpreter in
+// the way: a C++ caller of the C ABI, as the Rust facade would be.  One ReedSolomonCoder with
+// a private context, one 32 767-byte slice per call (the reference's shape: block_producer.rs
+// :339-345 -> reed_solomon.rs:88-128 shred; slot_block_data.rs:353 -> :140-208 deshred).
+// Prints one JSON line: median / p90 / min microseconds per call for
+//   shred           payload -> 32 data + 32 coding shreds of 1 KiB
+//   deshred_coding  from the 32 coding shreds only (benches/shredder.rs:49-53's shape)
+//   deshred_random  from a random 32 of the 64 shreds (the follower's arrival)
+// Usage: latency_probe [calls]   (built by tools/latency/build.sh against the in-tree library)
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <vector>
+
+#include "alpenglow_rs.h"
+
+using clk = std::chrono::steady_clock;
+
+struct Stat {
+  double med, p90, min;
+};
+static Stat stat(std::vector<double> v) {
+  std::sort(v.begin(), v.end());
+  return {v[v.size() / 2], v[v.size() * 9 / 10], v[0]};
+}
+
+int main(int argc, char** argv) {
+  const int calls = argc > 1 ? std::atoi(argv[1]) : 400;
+  ag_rs_coder* coder = nullptr;
+  if (ag_rs_coder_new_on_device(0, 32, &coder)) {
+    std::fprintf(stderr, "no coder (no device?)\n");
+    return 1;
+  }
+  std::mt19937_64 rng(7);
+  std::vector<uint8_t> payload(AG_RS_MAX_DATA_PER_SLICE);
+  for (auto& b : payload) b = static_cast<uint8_t>(rng());
+  std::vector<uint8_t> data(32 * 1024), coding(32 * 1024), pout(32 * 1024), dout(32 * 1024), cout(32 * 1024);
+  size_t S = 0, plen = 0;
+  auto shred = [&] { return ag_rs_coder_shred(coder, payload.data(), payload.size(), data.data(), coding.data(), &S); };
+  if (shred() || S != 1024) return 1;
+  std::vector<const uint8_t*> ptr(64);
+  std::vector<size_t> lens(64, S);
+  std::vector<uint8_t> is_data(64);
+  for (int i = 0; i < 64; ++i) is_data[i] = i < 32;
+  auto set_present = [&](const std::vector<int>& keep) {
+    std::fill(ptr.begin(), ptr.end(), nullptr);
+    for (int i : keep) ptr[i] = i < 32 ? data.data() + i * S : coding.data() + (i - 32) * S;
+  };
+  auto deshred = [&] {
+    return ag_rs_coder_deshred(coder, 32, ptr.data(), lens.data(), is_data.data(), pout.data(), &plen, dout.data(),
+                               cout.data(), &S);
+  };
+  auto time = [&](auto&& f) {
+    for (int i = 0; i < 20; ++i) f();
+    std::vector<double> t;
+    for (int i = 0; i < calls; ++i) {
+      const auto a = clk::now();
+      if (f()) std::exit(2);
+      t.push_back(std::chrono::duration<double, std::micro>(clk::now() - a).count());
+    }
+    return stat(t);
+  };
+  const Stat s_shred = time(shred);
+  std::vector<int> coding_only;
+  for (int i = 32; i < 64; ++i) coding_only.push_back(i);
+  set_present(coding_only);
+  const Stat s_dc = time(deshred);
+  if (plen != payload.size() || std::memcmp(pout.data(), payload.data(), plen)) return 3;
+  std::vector<int> all(64);
+  for (int i = 0; i < 64; ++i) all[i] = i;
+  std::shuffle(all.begin(), all.end(), rng);
+  all.resize(32);
+  set_present(all);
+  const Stat s_dr = time(deshred);
+  if (plen != payload.size() || std::memcmp(pout.data(), payload.data(), plen) ||
+      std::memcmp(cout.data(), coding.data(), 32 * S))
+    return 4;
+  std::printf("{\"unit\": \"us per call\", \"caller\": \"C++ through the C ABI\", \"calls\": %d, "
+              "\"shred\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
+              "\"deshred_coding_only\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
+              "\"deshred_random_32_of_64\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}}\n",
+              calls, s_shred.med, s_shred.p90, s_shred.min, s_dc.med, s_dc.p90, s_dc.min, s_dr.med, s_dr.p90, s_dr.min);
+  ag_rs_coder_free(coder);
+  return 0;
+}
