@@ -187,23 +187,6 @@ __device__ __forceinline__ void ifft_bfly(uint32_t* x, uint32_t* y) {
   if constexpr (kSkewLog[S] != 65535) mul_acc<S>(x, y);
 }
 
-// The crate's IFFT butterfly with skew A followed by its FFT butterfly with skew B on the same
-// pair -- the top layer of FFT_B(IFFT_A(.)) -- as one multiply by the field sum of the two
-// constants (gen_consts.cpp, kFusedA / kFusedB): y ^= x; x ^= y (c_A + c_B); y ^= x (UPD_Y).
-constexpr int fused_index(int a, int b) {
-  for (int i = 0; i < kFusedCount; ++i)
-    if (kFusedA[i] == a && kFusedB[i] == b) return kSkewCount + i;
-  return -1;
-}
-template <int A, int B, bool UPD_Y = true>
-__device__ __forceinline__ void fused_bfly(uint32_t* x, uint32_t* y) {
-  constexpr int F = fused_index(A, B);
-  static_assert(F >= 0, "no fused constant generated for this skew pair");
-  xor_planes(y, x);
-  if constexpr (kSkewLog[F] != 65535) mul_acc<F>(x, y);
-  if constexpr (UPD_Y) xor_planes(y, x);
-}
-
 // ---- XCD-aware tile order ----------------------------------------------------------
 // Workgroups are dispatched round-robin over the 8 XCDs (XCD = b % 8).  xcd_tile gives
 // each XCD one contiguous range of tiles, so the tiles in flight on one XCD are HBM

@@ -104,7 +104,7 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
       const uint8_t* base = p.in + sh * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece_if(base + io.off[q], (io.valid >> q) & 1);
+        const uint4 x = ld_piece(base + io.off[q]);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -131,7 +131,8 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
     using H1 = X8Lay<4, 1, 0, 2, 3>;
     using H0 = X8Lay<4, 0, 1, 2, 3>;
     static_assert(std::is_same_v<H3, X8Layout<3>>, "H3 is layout L3");
-    x8_layer_fused<X8Layout<3>, 4, DIN, DOUT, false>(r);  // IFFT b4 + FFT b4 (x only)
+    x8_layer<3, 4, true, DIN>(wave, r);
+    x8_layer<3, 4, false, DOUT, 0x5, false>(wave, r);
     x8_layer_lay<H3, 3, DOUT, 0x5>(wave, r);
     x8_swap<1, 2, 4, 0x5>(wave, lane, lds, &flags, r);
     x8_layer_lay<H2, 2, DOUT, 0x5>(wave, r);
@@ -159,7 +160,8 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
     });
     return;
   }
-  x8_layer_fused<X8Layout<3>, 4, DIN, DOUT>(r);  // IFFT b4 + FFT b4
+  x8_layer<3, 4, true, DIN>(wave, r);
+  x8_layer<3, 4, false, DOUT>(wave, r);
   x8_layer<3, 3, false, DOUT>(wave, r);
   x8_swap<0, 2, 4>(wave, lane, lds, &flags, r);
   x8_layer<2, 2, false, DOUT>(wave, r);
@@ -405,7 +407,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
 // partial (in planes), output multiply (linear: one product per restored original).  Loads
 // and masks are the pass's loaded half (window positions DIN + j); outputs are window
 // positions DOUT + j.  One pattern per tile (tiles never straddle blocks): the constants are
-// wave-uniform words, multiplied by the Horner scheme in the polynomial basis (mul_rt_poly).
+// wave-uniform words, multiplied by the Horner scheme in the polynomial basis with the
+// coefficient bits tested on the scalar unit (mul_rt_poly_u: a clear bit costs no VALU).
 // Per-lane patterns run on decode_h8.
 // =====================================================================================
 template <int PASS, int DIN, int DOUT>
@@ -449,7 +452,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
       const uint8_t* base = is_rec ? p.rec + (g - rpos) * p.rec_shard_stride : p.orig + (g - opos) * p.orig_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece_if(base + (is_rec ? io_r.off[q] : io_o.off[q]), (io_r.valid >> q) & 1);
+        const uint4 x = ld_piece(base + (is_rec ? io_r.off[q] : io_o.off[q]));
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -465,7 +468,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
     if ((in_mask >> j) & 1) {
       swap_halves(r[t]);
       dev::planes_from_raw(r[t]);
-      dev::mul_rt_poly(r[t], coef[j]);
+      dev::mul_rt_poly_u(r[t], coef[j]);  // wave-uniform constant: scalar-branch Horner
     }
   });
   // IFFT_64 (skew delta DIN)
@@ -552,7 +555,7 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
       }
       // the output multiply is linear: pass 1 stores its unmultiplied partial, pass 2 has
       // added it in planes and multiplies once
-      if constexpr (PASS != 1) dev::mul_rt_poly(r[t], coef_out[j]);
+      if constexpr (PASS != 1) dev::mul_rt_poly_u(r[t], coef_out[j]);
       store_shard(dst, io_o, io_o.valid, r[t]);
     }
   });
@@ -1120,7 +1123,7 @@ __device__ __forceinline__ void mc_load(const XformParams& p, const TileIO& io, 
       const uint8_t* base = p.in + (s0 + t) * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece_if(base + io.off[q], (io.valid >> q) & 1);
+        const uint4 x = ld_piece(base + io.off[q]);
         raw[t][4 * q] = x.x;
         raw[t][4 * q + 1] = x.y;
         raw[t][4 * q + 2] = x.z;
@@ -1212,7 +1215,7 @@ __device__ __forceinline__ void syn_load(const DecodeSynParams& p, const TileIO&
       const uint8_t* base = p.orig + s * p.orig_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece_if(base + io.off[q], (io.valid >> q) & 1);
+        const uint4 x = ld_piece(base + io.off[q]);
         raw[t][4 * q] = x.x;
         raw[t][4 * q + 1] = x.y;
         raw[t][4 * q + 2] = x.z;

@@ -112,27 +112,10 @@ __device__ __forceinline__ void xf_pass_b_fft(Regs8& r) {
     });
   });
 }
-// IFFT layers, the top one fused with the FFT's first (dev::fused_bfly), FFT layers.
 template <int NW, int DIN, int DOUT>
 __device__ __forceinline__ void xf_pass_b(Regs8& r) {
-  constexpr int NL = PassB<NW>::kLayers;
-  static_for<NL - 1>([&](auto L) {  // ascending distance, below the top
-    static_for<4>([&](auto I) {
-      using P = typename PassB<NW>::template Pair<decltype(L)::value, decltype(I)::value>;
-      dev::ifft_bfly<P::g + P::d + DIN - 1>(r[P::t], r[P::u]);
-    });
-  });
-  static_for<4>([&](auto I) {
-    using P = typename PassB<NW>::template Pair<NL - 1, decltype(I)::value>;
-    static_assert(P::g == 0, "the top layer is one group");
-    dev::fused_bfly<P::d + DIN - 1, P::d + DOUT - 1>(r[P::t], r[P::u]);
-  });
-  static_for<NL - 1>([&](auto L) {  // descending distance, below the top
-    static_for<4>([&](auto I) {
-      using P = typename PassB<NW>::template Pair<NL - 2 - decltype(L)::value, decltype(I)::value>;
-      dev::fft_bfly<P::g + P::d + DOUT - 1>(r[P::t], r[P::u]);
-    });
-  });
+  xf_pass_b_ifft<NW, DIN>(r);
+  xf_pass_b_fft<NW, DOUT>(r);
 }
 
 template <int NW, int DOUT>
@@ -177,12 +160,6 @@ __device__ __forceinline__ void lds_get(const uint4* lds, int slot, int lane, ui
 __device__ __forceinline__ uint4 ld_piece(const uint8_t* p) {
   const dev::u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const dev::u32x4*>(p));
   return make_uint4(v.x, v.y, v.z, v.w);
-}
-// A piece of a tile column that exists (TileIO::valid); columns past the batch read as zero
-// instead of re-reading the last column (over PCIe, for the zero-copy single-codeword calls,
-// those re-reads were three quarters of the read requests of a 16-column codeword).
-__device__ __forceinline__ uint4 ld_piece_if(const uint8_t* p, bool ok) {
-  return ok ? ld_piece(p) : make_uint4(0, 0, 0, 0);
 }
 __device__ __forceinline__ void st_piece(uint8_t* p, uint32_t a, uint32_t b, uint32_t c, uint32_t d) {
   const dev::u32x4 v = {a, b, c, d};
@@ -240,7 +217,7 @@ __device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& 
       const uint8_t* base = p.in + s * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece_if(base + io.off[q], (io.valid >> q) & 1);
+        const uint4 x = ld_piece(base + io.off[q]);
         raw[t][4 * q] = x.x;
         raw[t][4 * q + 1] = x.y;
         raw[t][4 * q + 2] = x.z;
@@ -497,21 +474,6 @@ __device__ __forceinline__ void x8_layer(int wave, Regs4& r) {
   if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)], UPD_Y);
   if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)], UPD_Y);
 }
-// The top layer B of FFT_DOUT(IFFT_DIN(.)) as fused butterflies (dev::fused_bfly): no wave bit
-// lies above the top bit, so the constant is the same in every wave.  UPD_Y false: the FFT's
-// y ^= x is skipped (the pruned FFTs need only x).
-template <typename Lay, int B, int DIN, int DOUT, bool UPD_Y = true>
-__device__ __forceinline__ void x8_layer_fused(Regs4& r) {
-  constexpr int i = Lay::slot_of(B);
-  static_assert(i >= 0, "layer bit must be a slot bit");
-  static_assert(Lay::rel(B) == 0, "the fused layer is the top one");
-  constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;
-  constexpr int g0 = Lay::pos(0, t0) & ~((2 << B) - 1), g1 = Lay::pos(0, t1) & ~((2 << B) - 1);
-  static_assert(g0 == 0 && g1 == 0, "the top layer is one group");
-  dev::fused_bfly<(1 << B) + DIN - 1, (1 << B) + DOUT - 1, UPD_Y>(r[t0], r[t0 | (1 << i)]);
-  dev::fused_bfly<(1 << B) + DIN - 1, (1 << B) + DOUT - 1, UPD_Y>(r[t1], r[t1 | (1 << i)]);
-}
-
 // the same on an explicit layout type (xform8's pruned FFT layouts, decode_x16's layouts)
 template <typename Lay, int B, bool INV, int DELTA>
 __device__ __forceinline__ void x8_layer_t(int wave, Regs4& r) {

@@ -57,7 +57,7 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
       const uint8_t* base = p.in + s * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece_if(base + io.off[q], (io.valid >> q) & 1);
+        const uint4 x = ld_piece(base + io.off[q]);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -81,8 +81,9 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
   x8_swap<0, 1, 2>(wave, lane, lds, &flags, r);
   x8_layer_t<LD, 4, true, DIN>(wave, r);
   x8_swap<1, 2, 3>(wave, lane, lds, &flags, r);
-  // IFFT b5 + FFT b5 fused, then the FFT_64 (skew delta DOUT) down to A
-  x8_layer_fused<LE, 5, DIN, DOUT>(r);
+  x8_layer_t<LE, 5, true, DIN>(wave, r);
+  // FFT_64 (skew delta DOUT), ending in A
+  x8_layer_t<LE, 5, false, DOUT>(wave, r);
   x8_layer_t<LE, 4, false, DOUT>(wave, r);
   if constexpr (!HALF) {
     x8_swap<1, 2, 4>(wave, lane, lds, &flags, r);

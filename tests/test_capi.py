@@ -86,26 +86,8 @@ def test_generated_constants_match_oracle_skew():
     text = open(os.path.join(build.CSRC, "rs_consts.inc")).read()
     body = text.split("kSkewLog[kSkewConstCount] = {")[1].split("};")[0]
     vals = [int(x) for x in re.findall(r"\d+", body)]
-    exp, log, skew, _ = o.tables()
-    nskew = int(re.search(r"kSkewCount = (\d+);", text).group(1))
-    assert vals[:nskew] == [int(x) for x in skew[:nskew]]
-    # fused top-layer constants: the field sum of the pair's skew factors, and the fused
-    # butterfly equals the crate's IFFT butterfly followed by its FFT butterfly
-    fa = [int(x) for x in re.search(r"kFusedA\[kFusedCount\] = \{([^}]*)\}", text).group(1).split(",")]
-    fb = [int(x) for x in re.search(r"kFusedB\[kFusedCount\] = \{([^}]*)\}", text).group(1).split(",")]
-    assert len(vals) == nskew + len(fa) and len(fa) == len(fb)
-    val = lambda lg: 0 if lg == 65535 else int(exp[lg])
-    rng = np.random.default_rng(3)
-    for i, (a, b) in enumerate(zip(fa, fb)):
-        assert val(vals[nskew + i]) == val(int(skew[a])) ^ val(int(skew[b]))
-        x, y = rng.integers(0, 1 << 16, 64), rng.integers(0, 1 << 16, 64)
-        mulv = lambda v, lg: o.mul(v, lg) if lg != 65535 else np.zeros_like(v)
-        y1 = y ^ x  # crate IFFT butterfly (skew a), then FFT butterfly (skew b)
-        x1 = x ^ mulv(y1, int(skew[a]))
-        x2 = x1 ^ mulv(y1, int(skew[b]))
-        y2 = y1 ^ x2
-        fx = x ^ mulv(y ^ x, vals[nskew + i])  # fused
-        assert np.array_equal(fx, x2) and np.array_equal((y ^ x) ^ fx, y2)
+    _, _, skew, _ = o.tables()
+    assert vals == [int(x) for x in skew[:len(vals)]]
     # spot-check a multiply matrix row against the oracle's field multiply
     rows = text.split("kMulRow[kSkewConstCount][16] = {")[1]
     first = [int(x, 16) for x in re.findall(r"0x([0-9a-f]{4})", rows)[: 16 * 8]]
