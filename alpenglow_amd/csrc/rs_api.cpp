@@ -555,8 +555,11 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
   bool any_lr = false;
   // decode_c: the 32-point full-window geometries (HighRate, m = 32, k <= 32) with lost
   // recovery shards; any k survivors, same tiling rule
+  // (a batch of fewer tiles than CUs is latency-bound -- a single slice per call -- and the
+  // correction's serial SALU phase made one tile a 43 us kernel: those take the window decoder)
+  const uint64_t ncols = static_cast<uint64_t>(nblocks) * cps;
   const bool corr_geo = mode == AG_RS_DECODE_ANY_K && hr == 1 && m == 32 && k <= 32 && S % 64 == 0 && aligned &&
-                        (npat == 1 || cps % 64 == 0) && static_cast<uint64_t>(nblocks) * cps < (uint64_t{1} << 31);
+                        (npat == 1 || cps % 64 == 0) && ncols < (uint64_t{1} << 31) && ncols >= 64 * 256;
   // W = 128 windows as two 64-point passes (decode_x16 PASS 1 / 2): the originals in one
   // window half -- HighRate with next_pow2(m) = 64 (originals at 64..127), LowRate with
   // next_pow2(k) <= 64 and next_pow2(k) + m in (64, 128] (originals at 0..k-1).  Any k

@@ -1981,7 +1981,13 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
     // reconstructs (half the exposed arithmetic per wave: -8% time), with the pruned FFT when
     // every restored original is < 16.
     case XformKind::kEncode32:
-      hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);
+      // batches of fewer tiles than CUs (a single slice per call: one tile) are latency-bound:
+      // xform8 spreads a tile's transform over 8 waves of 4 slots, half xform<4>'s instruction
+      // stream per wave
+      if (groups < 256)
+        hipLaunchKernelGGL((xform8_kernel<32, 0>), grid, dim3(512), 0, stream, p);
+      else
+        hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);
       break;
     case XformKind::kDecode32:
       if (p.out_low_half)

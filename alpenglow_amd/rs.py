@@ -200,6 +200,12 @@ def device_count() -> int:
     return n.value
 
 
+def _split(buf, S: int, n: int) -> list:
+    """n consecutive S-byte shreds of a ctypes buffer (one copy of the used bytes)."""
+    raw = ctypes.string_at(buf, S * n)
+    return [raw[i * S:(i + 1) * S] for i in range(n)]
+
+
 def _buf(data: bytes):
     return ctypes.create_string_buffer(bytes(data), len(data)) if data else ctypes.create_string_buffer(1)
 
@@ -478,11 +484,10 @@ class ReedSolomonCoder:
         data = ctypes.create_string_buffer(DATA_SHREDS * MAX_DATA_PER_SHRED)
         coding = ctypes.create_string_buffer(self.num_coding * MAX_DATA_PER_SHRED)
         sb = ctypes.c_size_t()
-        _check(self._lib.ag_rs_coder_shred(self.handle, _buf(payload), len(payload), data, coding,
-                                           ctypes.byref(sb)), "ReedSolomonCoder::shred")
-        S = sb.value
-        return RawShreds(data=[data.raw[i * S:(i + 1) * S] for i in range(DATA_SHREDS)],
-                         coding=[coding.raw[i * S:(i + 1) * S] for i in range(self.num_coding)])
+        # a bytes object passes as a read-only pointer to its own buffer (no copy)
+        _check(self._lib.ag_rs_coder_shred(self.handle, payload, len(payload), data, coding, ctypes.byref(sb)),
+               "ReedSolomonCoder::shred")
+        return RawShreds(data=_split(data, sb.value, DATA_SHREDS), coding=_split(coding, sb.value, self.num_coding))
 
     def deshred(self, shreds, data_shreds: int | None = None):
         """``shreds``: TOTAL_SHREDS entries, each None or (is_data, bytes) -- the
@@ -491,9 +496,9 @@ class ReedSolomonCoder:
         if data_shreds is None:
             data_shreds = TOTAL_SHREDS - self.num_coding
         assert len(shreds) == TOTAL_SHREDS
-        keep = [_buf(s[1]) if s is not None else None for s in shreds]
-        ptrs = (ctypes.c_void_p * TOTAL_SHREDS)(
-            *[ctypes.cast(b, ctypes.c_void_p) if b is not None else None for b in keep])
+        # pointers straight into bytes objects (no copy for bytes; `keep` holds them through the call)
+        keep = [bytes(s[1]) if s is not None else None for s in shreds]
+        ptrs = (ctypes.c_char_p * TOTAL_SHREDS)(*keep)
         lens = (ctypes.c_size_t * TOTAL_SHREDS)(*[len(s[1]) if s is not None else 0 for s in shreds])
         isd = (ctypes.c_uint8 * TOTAL_SHREDS)(*[1 if (s is not None and s[0]) else 0 for s in shreds])
         cap = max([len(s[1]) for s in shreds if s is not None] + [1])
@@ -505,9 +510,8 @@ class ReedSolomonCoder:
                                              ctypes.byref(plen), data, coding, ctypes.byref(sb)),
                "ReedSolomonCoder::deshred")
         S = sb.value
-        raw = RawShreds(data=[data.raw[i * S:(i + 1) * S] for i in range(DATA_SHREDS)],
-                        coding=[coding.raw[i * S:(i + 1) * S] for i in range(self.num_coding)])
-        return payload.raw[:plen.value], raw
+        raw = RawShreds(data=_split(data, S, DATA_SHREDS), coding=_split(coding, S, self.num_coding))
+        return ctypes.string_at(payload, plen.value), raw
 
     def __del__(self):
         if getattr(self, "handle", None):

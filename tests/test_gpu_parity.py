@@ -61,6 +61,19 @@ def gpu_decode(ctx, dev, orig: np.ndarray, rec: np.ndarray, opres, rpres, mode):
     return d_o.cpu().numpy().reshape(n, k, S)
 
 
+# decode_c serves batches of at least this many 64-byte shard columns (256 tiles: fewer tiles
+# than CUs are latency-bound and take the window decoder) -- rs_api.cpp decode_cols corr_geo
+CORR_MIN_COLS = 64 * 256
+
+
+def _blocks(seed, n, k, S):
+    """(n, k, S) uint8 originals: the oracle's block_bytes for small batches, numpy's PCG64
+    for large ones (data only; the parity is checked against the re-encoded blocks)."""
+    if n * k * S <= (1 << 22):
+        return np.stack([np.frombuffer(o.block_bytes(seed + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    return np.random.default_rng(seed).integers(0, 256, (n, k, S), dtype=np.uint8)
+
+
 # ------------------------------------------------------------------------------ encode
 
 def test_encode_golden(ctx, dev, golden):
@@ -322,26 +335,34 @@ def test_correction_decode_one_pattern(ctx, dev, k, S, n, ne, nl):
     restored originals must equal the encoded ones."""
     m = 32
     rng = random.Random(k * 7919 + S + ne * 31 + nl)
-    blocks = np.stack([np.frombuffer(o.block_bytes(900 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
-    rec = ro_c.encode_blocks(blocks, m, threads=8)
     lost, lost_r = rng.sample(range(k), ne), rng.sample(range(m), nl)
-    damaged = blocks.copy()
-    damaged[:, lost] = 0x5A
-    rec_d = rec.copy()
-    rec_d[:, lost_r] = 0xA5  # lost recovery shards must not be read
     op = [0 if i in lost else 1 for i in range(k)]
     rp = [0 if j in lost_r else 1 for j in range(m)]
-    got = gpu_decode(ctx, dev, damaged, rec_d, op, rp, rs.DECODE_ANY_K)
-    assert np.array_equal(got, blocks)
+    # n blocks (fewer tiles than CUs: the window decoder) and a batch of CORR_MIN_COLS columns
+    # (decode_c itself when nl <= 16)
+    for nb in (n, max(n, -(-CORR_MIN_COLS // (S // 64)))):
+        blocks = _blocks(900 + nb, nb, k, S)
+        rec = ro_c.encode_blocks(blocks, m, threads=8)
+        damaged = blocks.copy()
+        damaged[:, lost] = 0x5A
+        rec_d = rec.copy()
+        rec_d[:, lost_r] = 0xA5  # lost recovery shards must not be read
+        got = gpu_decode(ctx, dev, damaged, rec_d, op, rp, rs.DECODE_ANY_K)
+        assert np.array_equal(got, blocks), nb
+        classes = rs.last_decode_classes(ctx)
+        if nb * (S // 64) >= CORR_MIN_COLS and 0 < nl <= 16:
+            assert classes.get("correction", 0) > 0, classes
+        else:
+            assert "correction" not in classes, classes
 
 
-@pytest.mark.parametrize("S,n", [(4096, 24), (8192, 9)])
+@pytest.mark.parametrize("S,n", [(4096, 256), (8192, 128)])
 def test_correction_decode_per_block_patterns(ctx, dev, S, n):
     """A random pattern per block across the 32:32 decoders: full recovery set (transform),
     1..16 lost recovery shards (decode_c), more (decode_x), nothing erased; then a second
     pattern set through the same context (pattern cache)."""
     k = m = 32
-    blocks = np.stack([np.frombuffer(o.block_bytes(1300 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
+    blocks = _blocks(1300, n, k, S)
     rec = ro_c.encode_blocks(blocks, m, threads=8)
     for seed in (1, 2):
         rng = random.Random(S + n + seed)
@@ -356,6 +377,7 @@ def test_correction_decode_per_block_patterns(ctx, dev, S, n):
             rp += [0 if j in lost_r else 1 for j in range(m)]
         got = gpu_decode(ctx, dev, damaged, rec_d, op, rp, rs.DECODE_ANY_K)
         assert np.array_equal(got, blocks), seed
+        assert rs.last_decode_classes(ctx).get("correction", 0) > 0
 
 
 @pytest.mark.parametrize("k,m,S,n", [(16, 4, 4096, 6), (16, 3, 640, 5), (13, 4, 128, 7), (64, 4, 1024, 3),
