@@ -180,12 +180,26 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
     }
   }
   const uint32_t qall = qmask_all<4>(out_io, mask, 4 * wave, p.n_out);
-  if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;
-  x8_layer<0, 0, false, DOUT>(wave, r);
+  // slots some lane stores (wave-uniform): a decode restores only the erased originals, so
+  // the last FFT layer skips butterflies with no stored output (y not updated where only x is
+  // stored) and unstored slots skip their planes -> bytes conversion
+  uint32_t need = 0;
+  static_for<4>([&](auto T) {
+    constexpr int t = decltype(T)::value;
+    if (__builtin_amdgcn_ballot_w64(((qall >> (4 * t)) & 15u) != 0) != 0) need |= 1u << t;
+  });
+  if (need == 0) return;
+  {
+    using L0 = X8Layout<0>;
+    const int v = x8_compress<L0::rel(0)>(wave);
+    if (need & 3u) x8_bfly_w<L0, 0, false, DOUT, 0>(v, r[0], r[1], (need & 2u) != 0);
+    if (need & 12u) x8_bfly_w<L0, 0, false, DOUT, 2>(v, r[2], r[3], (need & 8u) != 0);
+  }
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t sh = 4 * wave + t;  // wave-uniform
-    if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, r[t]);
+    if (((need >> t) & 1u) && sh < p.n_out)
+      store_shard(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, r[t]);
   });
 }
 
@@ -295,10 +309,13 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void decode_x_kernel(cons
   TileIO io_r, io_o;
   uint64_t off_r = 0, off_o = 0;
   if constexpr (PL) {
-    const uint64_t gc = static_cast<uint64_t>(tile) * kXfLanes + lane;
-    const bool ok = gc < p.total_columns;
-    const uint64_t blk = ok ? gc / p.chunks_per_shard : 0;
-    const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
+    const uint64_t g0 = static_cast<uint64_t>(tile) * kXfLanes;  // wave-uniform: one scalar division
+    const uint64_t b0 = g0 / p.chunks_per_shard;
+    const uint32_t cc = static_cast<uint32_t>(g0 - b0 * p.chunks_per_shard) + lane;
+    const bool ok = g0 + lane < p.total_columns;
+    const uint32_t d = ok ? cc / p.chunks_per_shard : 0;
+    const uint64_t blk = ok ? b0 + d : 0;
+    const uint64_t col = ok ? cc - d * p.chunks_per_shard : 0;
     in_mask = ok ? p.pmask[2 * blk] : 0;
     out_mask = ok ? p.pmask[2 * blk + 1] : 0;
     rows = p.rows + blk * W;  // polynomial-basis constants, one word per position
@@ -616,8 +633,10 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   __syncthreads();
   const uint64_t gc = c0 + (lane & 31);
   const bool ok = gc < p.total_columns;
-  const uint64_t blk = ok ? gc / p.chunks_per_shard : sb0;
-  const uint64_t col = ok ? gc - blk * p.chunks_per_shard : 0;
+  const uint32_t cc = static_cast<uint32_t>(c0 - sb0 * p.chunks_per_shard) + (lane & 31);  // 32-bit per lane
+  const uint32_t d = ok ? cc / p.chunks_per_shard : 0;
+  const uint64_t blk = sb0 + d;
+  const uint64_t col = ok ? cc - d * p.chunks_per_shard : 0;
   const uint64_t in_mask = ok ? p.pmask[2 * blk] : 0;
   const uint64_t out_mask = ok ? p.pmask[2 * blk + 1] : 0;
   const uint32_t* coef = lcoef + (blk - sb0) * W;

@@ -182,14 +182,29 @@ __device__ __forceinline__ TileIO tile_io_g(uint64_t total_columns, uint32_t chu
   TileIO io;
   io.valid = 0;
   const uint32_t quarter = ((lane >> 5) << 1) | (lane & 1);
+  // the tile's first chunk once per wave (scalar division); lanes add < 64 chunks to its
+  // in-block index, so a lane crosses at most one block boundary when C >= 64 (the 64-bit
+  // division per lane and piece cost ~10 % of a reconstruct's VALU)
+  const uint32_t C = chunks_per_shard;
+  const uint64_t g0 = tile * kXfLanes;
+  const uint64_t b0 = g0 / C;
+  const uint32_t r0 = static_cast<uint32_t>(g0 - b0 * C);
+  const uint64_t base = b0 * block_stride;
+  const uint32_t lc = (lane & 31) >> 1;
   static_for<4>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
-    const uint64_t g = tile * kXfLanes + 16 * q + ((lane & 31) >> 1);
-    const bool ok = g < total_columns;
-    const uint64_t gc = ok ? g : total_columns - 1;
-    const uint64_t blk = gc / chunks_per_shard;
-    io.blk[q] = blk;
-    io.off[q] = blk * block_stride + (gc - blk * chunks_per_shard) * 64 + 16 * quarter;
+    const bool ok = g0 + 16 * q + lc < total_columns;
+    const uint32_t c = ok ? r0 + 16 * q + lc : r0;  // idle pieces re-read the tile's first chunk, never store
+    uint32_t d, rem;
+    if (C >= kXfLanes) {
+      d = c >= C ? 1u : 0u;
+      rem = d ? c - C : c;
+    } else {
+      d = c / C;
+      rem = c - d * C;
+    }
+    io.blk[q] = b0 + d;
+    io.off[q] = base + d * block_stride + static_cast<uint64_t>(rem) * 64 + 16 * quarter;
     io.valid |= ok ? (1u << q) : 0u;
   });
   return io;
@@ -602,14 +617,27 @@ __device__ __forceinline__ TileIO tile_io_l32(uint64_t total_columns, uint32_t c
   TileIO io;
   io.valid = 0;
   const uint32_t i = lane & 31;
+  // as tile_io_g: one scalar division per wave, lanes add < 32 chunks
+  const uint32_t C = chunks_per_shard;
+  const uint64_t g0 = tile * 32;
+  const uint64_t b0 = g0 / C;
+  const uint32_t r0 = static_cast<uint32_t>(g0 - b0 * C);
+  const uint64_t base = b0 * block_stride;
   static_for<4>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
-    const uint64_t g = tile * 32 + (i >> 2) + 8 * q;
-    const bool ok = g < total_columns;
-    const uint64_t gc = ok ? g : total_columns - 1;
-    const uint64_t blk = gc / chunks_per_shard;
-    io.blk[q] = blk;
-    io.off[q] = blk * block_stride + (gc - blk * chunks_per_shard) * 64 + 16 * (i & 3);
+    const uint32_t lc = (i >> 2) + 8 * q;
+    const bool ok = g0 + lc < total_columns;
+    const uint32_t c = ok ? r0 + lc : r0;  // idle pieces re-read the tile's first chunk, never store
+    uint32_t d, rem;
+    if (C >= 32) {
+      d = c >= C ? 1u : 0u;
+      rem = d ? c - C : c;
+    } else {
+      d = c / C;
+      rem = c - d * C;
+    }
+    io.blk[q] = b0 + d;
+    io.off[q] = base + d * block_stride + static_cast<uint64_t>(rem) * 64 + 16 * (i & 3);
     io.valid |= ok ? (1u << q) : 0u;
   });
   return io;
