@@ -15,6 +15,7 @@ import os
 import shutil
 import subprocess
 import sys
+import sysconfig
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
@@ -119,5 +120,22 @@ def build(force: bool = False) -> str:
     return LIB
 
 
+PYCODER = os.path.join(LIBDIR, "_pycoder" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+
+
+def build_pycoder(force: bool = False) -> str:
+    """The CPython binding of the per-call coder path (csrc/pycoder.c; host code, gcc)."""
+    src = os.path.join(CSRC, "pycoder.c")
+    hdr = os.path.join(INCLUDE, "alpenglow_rs.h")
+    if force or _mtime(PYCODER) < max(_mtime(src), _mtime(hdr)):
+        os.makedirs(LIBDIR, exist_ok=True)
+        tmp = PYCODER + ".tmp"
+        _run([os.environ.get("CC_HOST", "gcc"), "-O2", "-shared", "-fPIC", "-Wall", "-Wextra", "-Wno-unused-parameter",
+              f"-I{sysconfig.get_paths()['include']}", f"-I{INCLUDE}", src, "-o", tmp])
+        os.replace(tmp, PYCODER)
+    return PYCODER
+
+
 if __name__ == "__main__":
+    build_pycoder(force="--force" in sys.argv)
     print(build(force="--force" in sys.argv))

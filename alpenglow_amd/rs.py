@@ -206,6 +206,31 @@ def _split(buf, S: int, n: int) -> list:
     return [raw[i * S:(i + 1) * S] for i in range(n)]
 
 
+_pycoder = None
+
+
+def _coder_binding():
+    """The CPython binding of ag_rs_coder_shred / _deshred (csrc/pycoder.c, built next to the
+    library by ``python -m alpenglow_amd.build``), bound to the loaded library's entry points;
+    None if it was not built (the ctypes path then marshals the arguments)."""
+    global _pycoder
+    if _pycoder is None:
+        import importlib.util
+        import sysconfig
+
+        path = os.path.join(os.path.dirname(LIB_PATH), "_pycoder" + (sysconfig.get_config_var("EXT_SUFFIX") or ".so"))
+        mod = False
+        if os.path.exists(path):
+            spec = importlib.util.spec_from_file_location("_pycoder", path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            L = load()
+            addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
+            mod.bind(addr(L.ag_rs_coder_shred), addr(L.ag_rs_coder_deshred))
+        _pycoder = mod
+    return _pycoder or None
+
+
 def _buf(data: bytes):
     return ctypes.create_string_buffer(bytes(data), len(data)) if data else ctypes.create_string_buffer(1)
 
@@ -455,11 +480,36 @@ class ReedSolomonDecoder:
             self.handle = None
 
 
-@dataclass
 class RawShreds:
-    """reed_solomon.rs:35-40."""
-    data: list
-    coding: list
+    """reed_solomon.rs:35-40: the data and coding shreds (lists of bytes).  The coder's
+    results keep the contiguous shred bytes and split them into shreds on first access."""
+
+    __slots__ = ("_data", "_coding", "_packed")
+
+    def __init__(self, data=None, coding=None, packed=None):
+        self._data, self._coding, self._packed = data, coding, packed  # packed: (data, coding, S)
+
+    @staticmethod
+    def _cut(raw: bytes, S: int) -> list:
+        return [raw[i:i + S] for i in range(0, len(raw), S)] if S else []
+
+    @property
+    def data(self) -> list:
+        if self._data is None:
+            self._data = self._cut(self._packed[0], self._packed[2])
+        return self._data
+
+    @property
+    def coding(self) -> list:
+        if self._coding is None:
+            self._coding = self._cut(self._packed[1], self._packed[2])
+        return self._coding
+
+    def __eq__(self, other):
+        return isinstance(other, RawShreds) and self.data == other.data and self.coding == other.coding
+
+    def __repr__(self):
+        return f"RawShreds(data={len(self.data)} shreds, coding={len(self.coding)} shreds)"
 
 
 class ReedSolomonCoder:
@@ -480,6 +530,11 @@ class ReedSolomonCoder:
         self.handle = h
 
     def shred(self, payload: bytes) -> RawShreds:
+        pc = _coder_binding()
+        if pc is not None:
+            st, data, coding, S = pc.shred(self.handle.value, payload, self.num_coding)
+            _check(st, "ReedSolomonCoder::shred")
+            return RawShreds(packed=(data, coding, S))
         payload = bytes(payload)
         data = ctypes.create_string_buffer(DATA_SHREDS * MAX_DATA_PER_SHRED)
         coding = ctypes.create_string_buffer(self.num_coding * MAX_DATA_PER_SHRED)
@@ -496,6 +551,11 @@ class ReedSolomonCoder:
         if data_shreds is None:
             data_shreds = TOTAL_SHREDS - self.num_coding
         assert len(shreds) == TOTAL_SHREDS
+        pc = _coder_binding()
+        if pc is not None:
+            st, payload, data, coding, S = pc.deshred(self.handle.value, shreds, data_shreds, self.num_coding)
+            _check(st, "ReedSolomonCoder::deshred")
+            return payload, RawShreds(packed=(data, coding, S))
         # pointers straight into bytes objects (no copy for bytes; `keep` holds them through the call)
         keep = [bytes(s[1]) if s is not None else None for s in shreds]
         ptrs = (ctypes.c_char_p * TOTAL_SHREDS)(*keep)

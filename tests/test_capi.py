@@ -117,3 +117,21 @@ def test_private_context_objects_fail_loudly_without_device(lib):
         with pytest.raises(rs.RSError) as e:
             make()
         assert e.value.kind == "NoDevice"
+
+
+def test_pycoder_binding_marshalling(lib):
+    """The CPython binding of the per-call coder path (csrc/pycoder.c) is built, bound to the
+    loaded library, and rejects malformed shred lists before any device call."""
+    build.build_pycoder()
+    pc = rs._coder_binding()
+    assert pc is not None
+    with pytest.raises(ValueError):
+        pc.deshred(0, [None] * 3, 32, 32)
+    with pytest.raises(TypeError):
+        pc.deshred(0, [None] * 63 + [b"not a tuple"], 32, 32)
+    with pytest.raises(TypeError):
+        pc.deshred(0, [None] * 63 + [(True, 12345)], 32, 32)
+    # a RawShreds built from packed bytes splits on access and compares by content
+    raw = rs.RawShreds(packed=(bytes(range(8)), bytes(range(8, 12)), 2))
+    assert raw.data == [b"\x00\x01", b"\x02\x03", b"\x04\x05", b"\x06\x07"] and raw.coding == [b"\x08\x09", b"\x0a\x0b"]
+    assert raw == rs.RawShreds(data=list(raw.data), coding=list(raw.coding))
