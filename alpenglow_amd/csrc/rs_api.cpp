@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
@@ -183,6 +184,12 @@ struct ag_rs_ctx {
   hipStream_t h2d = nullptr, d2h = nullptr;
   DevBuf one_in, one_out;                 // crate-API single codeword
   PinBuf one_pin;                         // its pinned host staging
+  // per-call server (latency_server_kernel): mailbox in mapped host memory, its own stream
+  ag::LatencyMailbox* mb = nullptr;
+  ag::LatencyMailbox* mb_dev = nullptr;
+  hipStream_t server_stream = nullptr;
+  uint32_t server_seq = 0;
+  bool server_broken = false;  // a job timed out: the server path is off for this context
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
   std::vector<uint64_t> stage_mask_host;  // last restride masks uploaded to stage_mask
   std::vector<uint64_t> xmask_host;       // last general-decode masks (d_xmask), W = xmask_w
@@ -239,7 +246,26 @@ struct ag_rs_ctx {
     return AG_RS_OK;
   }
 
+  void server_stop() {
+    if (!mb) return;
+    (void)hipSetDevice(device);
+    const auto t0 = std::chrono::steady_clock::now();
+    if (__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) != 0) {
+      mb->kind = ag::kJobQuit;
+      __atomic_store_n(&mb->doorbell, ++server_seq, __ATOMIC_RELEASE);
+      while (__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) != 0 &&
+             std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
+      }
+    }
+    (void)hipStreamSynchronize(server_stream);  // the server exits on quit or its idle timeout
+    (void)hipStreamDestroy(server_stream);
+    (void)hipHostFree(mb);
+    mb = mb_dev = nullptr;
+    server_stream = nullptr;
+  }
+
   ~ag_rs_ctx() {
+    server_stop();
     if (own_stream) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(own_stream);
@@ -1493,6 +1519,69 @@ int spin_sync(ag_rs_ctx* c) {
   }
 }
 
+// ---- per-call server: one single-tile 32-point job through the mailbox ----------------
+// A 32:32 codeword of S <= 4 KiB (S % 64 == 0) is one tile of xform8: the resident server
+// runs it without a kernel dispatch or completion signal (tools/latency: one slice's shred
+// was dispatch + kernel + signal).  Started on first use, restarted when it has idled out.
+constexpr uint64_t kServerIdleTicks = 2000000;  // 20 ms of the 100 MHz wall clock
+bool server_fits(ag_rs_ctx* c, size_t k, size_t m, size_t S) {
+  return !c->server_broken && k == 32 && m == 32 && S % 64 == 0 && S >= 64 && S <= 64 * 64;
+}
+ag::XformParams one_tile(const uint8_t* in, size_t in_stride, uint8_t* out, size_t out_stride, size_t S) {
+  ag::XformParams p{};
+  p.in = in;
+  p.in_block_stride = in_stride;
+  p.in_shard_stride = S;
+  p.out = out;
+  p.out_block_stride = out_stride;
+  p.out_shard_stride = S;
+  p.n_in = 32;
+  p.n_out = 32;
+  p.chunks_per_shard = static_cast<uint32_t>(S / 64);
+  p.total_columns = S / 64;
+  return p;
+}
+int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t mask) {
+  if (!c->mb) {
+    void* h = nullptr;
+    AG_HIP(hipHostMalloc(&h, sizeof(ag::LatencyMailbox), hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(h, 0, sizeof(ag::LatencyMailbox));
+    void* d = nullptr;
+    if (hipHostGetDevicePointer(&d, h, 0) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->server_stream, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipHostFree(h);
+      c->server_stream = nullptr;
+      return AG_RS_ERR_DEVICE;
+    }
+    c->mb = static_cast<ag::LatencyMailbox*>(h);
+    c->mb_dev = static_cast<ag::LatencyMailbox*>(d);
+  }
+  ag::LatencyMailbox* mb = c->mb;
+  mb->kind = kind;
+  mb->mask = mask;
+  std::memcpy(static_cast<void*>(&mb->p), &p, sizeof p);
+  const uint32_t seq = ++c->server_seq;
+  __atomic_store_n(&mb->doorbell, seq, __ATOMIC_RELEASE);  // x86: the job's fields are visible first
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spins = 0;; ++spins) {
+    if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) return AG_RS_OK;
+    if (__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) == 0) {
+      // no server (first call, or it idled out -- possibly just after this doorbell)
+      if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) return AG_RS_OK;
+      __atomic_store_n(&mb->alive, 2u, __ATOMIC_RELEASE);
+      if (ag::launch_latency_server(c->mb_dev, kServerIdleTicks, c->server_stream) != hipSuccess) {
+        __atomic_store_n(&mb->alive, 0u, __ATOMIC_RELEASE);
+        return AG_RS_ERR_DEVICE;
+      }
+    }
+    if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+      c->server_broken = true;
+      return AG_RS_ERR_DEVICE;
+    }
+    __builtin_ia32_pause();
+  }
+}
+
 int run_one_encode(ag_rs_ctx* c, size_t k, size_t m, size_t S, const uint8_t* orig, uint8_t* rec) {
   int st;
   if ((st = c->enter())) return st;
@@ -1501,8 +1590,12 @@ int run_one_encode(ag_rs_ctx* c, size_t k, size_t m, size_t S, const uint8_t* or
   uint8_t* pin = c->one_pin.as<uint8_t>();
   uint8_t* pd = c->one_pin.dev<uint8_t>();
   std::memcpy(pin, orig, ob);
-  if ((st = encode_device(c, k, m, S, 1, pd, ob, pd + ob, rb))) return st;
-  if ((st = spin_sync(c))) return st;
+  if (server_fits(c, k, m, S)) {
+    if ((st = server_job(c, ag::kJobEncode32, one_tile(pd, ob, pd + ob, rb, S), 0))) return st;
+  } else {
+    if ((st = encode_device(c, k, m, S, 1, pd, ob, pd + ob, rb))) return st;
+    if ((st = spin_sync(c))) return st;
+  }
   std::memcpy(rec, pin + ob, rb);
   return AG_RS_OK;
 }
@@ -1533,9 +1626,24 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, uint8_t* orig, co
   size_t nr = 0;
   for (size_t i = 0; i < m; ++i) nr += rpres[i] != 0;
   const bool reuse = coding && present == k && nr == m;
-  if ((st = decode_device(c, k, m, S, 1, pd, ob, pd + ob, rb, opres, rpres, 1, mode))) return st;
-  if (coding && !reuse && (st = encode_device(c, k, m, S, 1, pd, ob, pd + ob + rb, rb))) return st;
-  if ((st = spin_sync(c))) return st;
+  if (nr == m && (present == k || mode == AG_RS_DECODE_ANY_K) && server_fits(c, k, m, S)) {
+    // the whole recovery set: the erased originals are one transform of it (the decode class
+    // "none" route of decode_cols), run by the per-call server
+    uint64_t mask = 0;
+    for (size_t i = 0; i < k; ++i)
+      if (!opres[i]) mask |= uint64_t{1} << i;
+    std::fill(std::begin(c->last_classes), std::end(c->last_classes), uint64_t{0});
+    ++c->last_classes[mask ? 1 : 0];  // "transform" (or "none")
+    if (mask && (st = server_job(c, (mask >> 16) ? ag::kJobDecode32 : ag::kJobDecode32Half,
+                                 one_tile(pd + ob, rb, pd, ob, S), mask)))
+      return st;
+    if (coding && !reuse && (st = server_job(c, ag::kJobEncode32, one_tile(pd, ob, pd + ob + rb, rb, S), 0)))
+      return st;
+  } else {
+    if ((st = decode_device(c, k, m, S, 1, pd, ob, pd + ob, rb, opres, rpres, 1, mode))) return st;
+    if (coding && !reuse && (st = encode_device(c, k, m, S, 1, pd, ob, pd + ob + rb, rb))) return st;
+    if ((st = spin_sync(c))) return st;
+  }
   std::memcpy(orig, pin, ob);
   if (coding) std::memcpy(coding, reuse ? rec : pin + ob + rb, rb);
   return AG_RS_OK;

@@ -86,17 +86,18 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
 //   H2 slots p4 p2 | waves p0 p1 p3   FFT b2
 //   H1 slots p4 p1 | waves p0 p2 p3   FFT b1
 //   H0 slots p4 p0 | waves p1 p2 p3   FFT b0, store shards 2w, 2w + 1
+// One tile (flags zeroed by the caller, every wave of the 512-thread workgroup calls it):
+// xform8_kernel's grid and the per-call server's jobs (latency_server_kernel).
 template <int DIN, int DOUT, bool HALF = false>
-__global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
-  __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
-  __shared__ X8Flags flags;
+__device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile, uint4* lds, X8Flags* fl) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
-  __syncthreads();
-  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
   const TileIO io = tile_io(p, tile, lane, p.in_block_stride);
   Regs4 r;
+  // a tile past the batch's last column (one slice per call: 16 of 64 columns) loads only
+  // its existing pieces -- over PCIe from mapped host memory, the idle re-reads were 3/4 of
+  // the per-call server's input traffic
+  const bool whole = p.total_columns >= (static_cast<uint64_t>(tile) + 1) * kXfLanes;
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t sh = 4 * wave + t;  // LA: wave-uniform
@@ -104,7 +105,8 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
       const uint8_t* base = p.in + sh * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(base + io.off[q]);
+        uint4 x = make_uint4(0, 0, 0, 0);
+        if (whole || ((io.valid >> q) & 1)) x = ld_piece(base + io.off[q]);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -120,11 +122,11 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
   });
   x8_layer<0, 0, true, DIN>(wave, r);
   x8_layer<0, 1, true, DIN>(wave, r);
-  x8_swap<0, 0, 1>(wave, lane, lds, &flags, r);
+  x8_swap<0, 0, 1>(wave, lane, lds, fl, r);
   x8_layer<1, 2, true, DIN>(wave, r);
-  x8_swap<1, 1, 2>(wave, lane, lds, &flags, r);
+  x8_swap<1, 1, 2>(wave, lane, lds, fl, r);
   x8_layer<2, 3, true, DIN>(wave, r);
-  x8_swap<0, 2, 3>(wave, lane, lds, &flags, r);
+  x8_swap<0, 2, 3>(wave, lane, lds, fl, r);
   if constexpr (HALF) {
     using H3 = X8Lay<4, 3, 0, 1, 2>;
     using H2 = X8Lay<4, 2, 0, 1, 3>;
@@ -134,11 +136,11 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
     x8_layer<3, 4, true, DIN>(wave, r);
     x8_layer<3, 4, false, DOUT, 0x5, false>(wave, r);
     x8_layer_lay<H3, 3, DOUT, 0x5>(wave, r);
-    x8_swap<1, 2, 4, 0x5>(wave, lane, lds, &flags, r);
+    x8_swap<1, 2, 4, 0x5>(wave, lane, lds, fl, r);
     x8_layer_lay<H2, 2, DOUT, 0x5>(wave, r);
-    x8_swap<1, 1, 5, 0x5>(wave, lane, lds, &flags, r);
+    x8_swap<1, 1, 5, 0x5>(wave, lane, lds, fl, r);
     x8_layer_lay<H1, 1, DOUT, 0x5>(wave, r);
-    x8_swap<1, 0, 6, 0x5>(wave, lane, lds, &flags, r);
+    x8_swap<1, 0, 6, 0x5>(wave, lane, lds, fl, r);
     const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
     uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
     if (p.out_mask) {
@@ -163,11 +165,11 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
   x8_layer<3, 4, true, DIN>(wave, r);
   x8_layer<3, 4, false, DOUT>(wave, r);
   x8_layer<3, 3, false, DOUT>(wave, r);
-  x8_swap<0, 2, 4>(wave, lane, lds, &flags, r);
+  x8_swap<0, 2, 4>(wave, lane, lds, fl, r);
   x8_layer<2, 2, false, DOUT>(wave, r);
-  x8_swap<1, 1, 5>(wave, lane, lds, &flags, r);
+  x8_swap<1, 1, 5>(wave, lane, lds, fl, r);
   x8_layer<1, 1, false, DOUT>(wave, r);
-  x8_swap<0, 0, 6>(wave, lane, lds, &flags, r);
+  x8_swap<0, 0, 6>(wave, lane, lds, fl, r);
   // store masks fetched only now: live across the transform they cost registers (spills)
   const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
   uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
@@ -201,6 +203,15 @@ __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
     if (((need >> t) & 1u) && sh < p.n_out)
       store_shard(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, r[t]);
   });
+}
+
+template <int DIN, int DOUT, bool HALF = false>
+__global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
+  __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
+  __shared__ X8Flags flags;
+  if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
+  __syncthreads();
+  xform8_tile<DIN, DOUT, HALF>(p, dev::xcd_tile(blockIdx.x, gridDim.x), lds, &flags);
 }
 
 // =====================================================================================
@@ -1987,6 +1998,78 @@ hipError_t launch_decode_syn(unsigned chunk, const DecodeSynParams& p, hipStream
     case 4: hipLaunchKernelGGL((decode_syn_kernel<4>), grid, dim3(256), 0, stream, p); break;
     default: return hipErrorInvalidValue;
   }
+  return hipGetLastError();
+}
+
+// ---- per-call server --------------------------------------------------------------
+// One workgroup of xform8's shape, resident between per-slice calls (LatencyMailbox in
+// rs_launch.hpp).  Thread 0 polls the doorbell with system-scope loads (vector memory; the
+// host memory is fine-grained, so nothing is cached across jobs) and every wave invalidates
+// its caches at job start; each wave releases its stores at system scope before thread 0
+// publishes done.  Every wave leaves the loop together on kJobQuit or the idle timeout.
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* a) {
+  return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* mb, uint64_t idle_ticks) {
+  __shared__ uint4 lds[16 * 4 * kXfLanes];
+  __shared__ X8Flags flags;
+  __shared__ uint32_t job[sizeof(XformParams) / 4];
+  __shared__ uint64_t mask;
+  __shared__ uint32_t cmd;
+  static_assert(sizeof(XformParams) % 4 == 0 && sizeof(XformParams) / 4 <= 512, "params copy");
+  uint32_t last = 0;
+  if (threadIdx.x == 0) {
+    last = sys_load(&mb->done);
+    __hip_atomic_store(&mb->alive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  for (;;) {
+    if (threadIdx.x == 0) {
+      const uint64_t t0 = wall_clock64();
+      uint32_t kind = kJobQuit;
+      for (;;) {
+        const uint32_t d = __hip_atomic_load(&mb->doorbell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        if (d != last) {
+          last = d;
+          kind = sys_load(&mb->kind);
+          break;
+        }
+        if (wall_clock64() - t0 > idle_ticks) break;
+        __builtin_amdgcn_s_sleep(2);
+      }
+      cmd = kind;
+    }
+    __syncthreads();
+    const uint32_t kind = __builtin_amdgcn_readfirstlane(cmd);
+    if (kind >= kJobQuit) break;
+    if (threadIdx.x < sizeof(XformParams) / 4)
+      job[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->p) + threadIdx.x);
+    if (threadIdx.x == 64) {
+      const uint32_t* m = reinterpret_cast<const uint32_t*>(&mb->mask);
+      mask = static_cast<uint64_t>(sys_load(m)) | static_cast<uint64_t>(sys_load(m + 1)) << 32;
+    }
+    if (threadIdx.x >= 128 && threadIdx.x < 144) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x - 128] = 0;
+    __syncthreads();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale input bytes in this CU's caches
+    XformParams p;
+    uint32_t* pw = reinterpret_cast<uint32_t*>(&p);
+    for (unsigned i = 0; i < sizeof(XformParams) / 4; ++i) pw[i] = __builtin_amdgcn_readfirstlane(job[i]);
+    p.out_mask = kind == kJobEncode32 ? nullptr : &mask;
+    p.pattern_per_block = 0;
+    if (kind == kJobEncode32)
+      xform8_tile<32, 0>(p, 0, lds, &flags);
+    else if (kind == kJobDecode32)
+      xform8_tile<0, 32>(p, 0, lds, &flags);
+    else
+      xform8_tile<0, 32, true>(p, 0, lds, &flags);
+    __threadfence_system();  // this wave's stores reach the host before done is published
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&mb->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&mb->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+hipError_t launch_latency_server(LatencyMailbox* mb_dev, uint64_t idle_ticks, hipStream_t stream) {
+  hipLaunchKernelGGL(latency_server_kernel, dim3(1), dim3(512), 0, stream, mb_dev, idle_ticks);
   return hipGetLastError();
 }
 

@@ -28,6 +28,23 @@ struct XformParams {
 
 enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };
 
+// The per-call server (latency_server_kernel): one resident workgroup per context serves
+// single-tile 32-point transforms posted through a mailbox in mapped, fine-grained host
+// memory, so a per-slice call costs no kernel dispatch and no completion signal.
+//   host:   writes kind / mask / p, then doorbell = seq; spins until done == seq
+//   server: polls doorbell, runs the job, releases its stores, writes done = seq; exits
+//           (alive = 0) on kJobQuit or after idle_ticks of the 100 MHz wall clock with no job
+enum LatencyJob : uint32_t { kJobEncode32 = 0, kJobDecode32 = 1, kJobDecode32Half = 2, kJobQuit = 3 };
+struct LatencyMailbox {
+  uint32_t doorbell;  // host: sequence number of the posted job
+  uint32_t done;      // server: sequence number of the last finished job
+  uint32_t alive;     // 0 no server, 1 server running, 2 launch requested (host)
+  uint32_t kind;      // LatencyJob
+  uint64_t mask;      // decode: store mask (bit s: shard s restored); the server copies it to LDS
+  XformParams p;      // in / out: device addresses of mapped host memory; p.out_mask ignored
+};
+hipError_t launch_latency_server(LatencyMailbox* mb_dev, uint64_t idle_ticks, hipStream_t stream);
+
 
 hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream);
 // True when the bitsliced transform exists for this transform size.

@@ -1187,3 +1187,29 @@ def test_window128_decode(ctx, dev, k, m, S, n, per_block, lo, lc):
                 surplus -= 1
     got = gpu_decode(ctx, dev, d_o, d_r, op2, rp2, rs.DECODE_EXACT)
     assert np.array_equal(got, blocks)
+
+
+@pytest.mark.gpu
+def test_per_call_server_jobs_and_restart(ctx):
+    """The resident per-call server (latency_server_kernel): back-to-back shreds and
+    coding-only deshreds of 32:32 slices with S % 64 == 0 run as mailbox jobs, other sizes take
+    the launch path in between, and calls after a gap longer than the server's 20 ms idle
+    timeout restart it -- every result against the oracle."""
+    import time
+
+    coder = rs.ReedSolomonCoder(ctx, 32)
+    rng = random.Random(4242)
+    sizes = [32767, 32704, 2047, 4095, 1000, 16383, 63, 0, 20000]
+    for i in range(45):
+        payload = o.splitmix64_bytes(5000 + i, sizes[i % len(sizes)])
+        raw = coder.shred(payload)
+        exp = o.coder_shred(payload, 32)
+        assert raw.data == exp.data and raw.coding == exp.coding, (i, len(payload))
+        got, raw2 = coder.deshred([None] * 32 + [(False, c) for c in raw.coding])
+        assert got == payload and raw2.coding == exp.coding, (i, len(payload))
+        keep = sorted(rng.sample(range(64), 32))
+        shreds = [((j < 32), (raw.data + raw.coding)[j]) if j in keep else None for j in range(64)]
+        got, _ = coder.deshred(shreds)
+        assert got == payload, (i, keep)
+        if i % 15 == 14:
+            time.sleep(0.06)  # the server idles out; the next call relaunches it
