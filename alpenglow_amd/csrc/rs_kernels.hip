@@ -2085,8 +2085,12 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
     case XformKind::kEncode32:
       // batches of fewer tiles than CUs (a single slice per call: one tile) are latency-bound:
       // xform8 spreads a tile's transform over 8 waves of 4 slots, half xform<4>'s instruction
-      // stream per wave
-      if (groups < 256)
+      // stream per wave.  Shards of 8 and 16 KiB (2 or 4 tiles per shard) also take xform8:
+      // xform<4> drops to 5.49-5.77 TB/s there while xform8 runs 5.93-6.18, and xform<4> wins
+      // by 0.03-0.31 TB/s at every other measured size (profiles/r04_encode_kernel_grid.txt; a
+      // copy with either kernel's load/store skeleton shows no such dip, tools/membench/
+      // membench7.hip, so it is the kernel's access order against that stride)
+      if (groups < 256 || p.chunks_per_shard == 128 || p.chunks_per_shard == 256)
         hipLaunchKernelGGL((xform8_kernel<32, 0>), grid, dim3(512), 0, stream, p);
       else
         hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);
