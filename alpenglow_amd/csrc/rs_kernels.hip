@@ -963,11 +963,11 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
   h8_relayout(r);
   x8_layer_t<LB, 1, true, 0>(wave, r);
   x8_layer_t<LB, 2, true, 0>(wave, r);
-  x8_swap<1, 0, 1>(wave, lane, lds, &flags, r);
+  x8_swap<1, 0, 1, 0xF, false>(wave, lane, lds, &flags, r);
   x8_layer_t<LC, 3, true, 0>(wave, r);
-  x8_swap<0, 1, 2>(wave, lane, lds, &flags, r);
+  x8_swap<0, 1, 2, 0xF, false>(wave, lane, lds, &flags, r);
   x8_layer_t<LD, 4, true, 0>(wave, r);
-  x8_swap<1, 2, 3>(wave, lane, lds, &flags, r);
+  x8_swap<1, 2, 3, 0xF, false>(wave, lane, lds, &flags, r);
   x8_layer_t<LE, 5, true, 0>(wave, r);
   // formal derivative in E (decode_h8's, epochs 4 and 5)
   auto wait_readers = [&](int x, uint32_t e) __attribute__((always_inline)) {
@@ -1032,9 +1032,9 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
     x8_signal(&flags.done[wave], 4 + D, lane);
   }
   x8_layer_t<LD, 3, false, 0>(wave, r);
-  x8_swap<0, 1, 5 + D>(wave, lane, lds, &flags, r);
+  x8_swap<0, 1, 5 + D, 0xF, false>(wave, lane, lds, &flags, r);
   x8_layer_t<LC, 2, false, 0>(wave, r);
-  x8_swap<1, 0, 6 + D>(wave, lane, lds, &flags, r);
+  x8_swap<1, 0, 6 + D, 0xF, false>(wave, lane, lds, &flags, r);
   x8_layer_t<LB, 1, false, 0>(wave, r);
   h8_relayout(r);
   h8_layer0<false, 0>(wave, h, r);

@@ -529,7 +529,11 @@ __device__ __forceinline__ void x8_signal(uint32_t* f, uint32_t e, int lane) {
   if (lane == 0) __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-template <int I, int J, int EP, int LIVE = 0xF, typename Flags>
+// SPLIT (default): each branch reads its slot behind an opaque zero offset, so LLVM cannot
+// hoist the two branches' identical reads into one read ahead of the branch (which left a
+// 16-32 VGPR copy after it: -96 VALU per xform8 wave).  decode_c and decode_pk keep the
+// hoisted form: at their register pressure the split reads spill (35 and 4-6 VGPRs).
+template <int I, int J, int EP, int LIVE = 0xF, bool SPLIT = true, typename Flags>
 __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, Flags* fl, Regs4& r) {
   const int wj = (wave >> J) & 1;
   const int partner = wave ^ (1 << J);
@@ -549,7 +553,9 @@ __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, Flags* f
     constexpr int t = decltype(T)::value;
     constexpr int k = (t >> (1 - I)) & 1;
     if (((LIVE >> t) & 1) && ((t >> I) & 1) != wj) {
-      lds_get(lds, 2 * wave + k, lane, r[t]);
+      int z = 0;
+      if constexpr (SPLIT) __asm__ volatile("s_mov_b32 %0, 0 ; x8_swap slot %1" : "=s"(z) : "n"(t));
+      lds_get(lds, 2 * wave + k + z, lane, r[t]);
       __asm__ volatile("; x8_swap get %0" ::"n"(t));
     }
   });
