@@ -66,20 +66,25 @@ __device__ __forceinline__ uint32_t xsum64(uint32_t acc, const uint32_t* s) {
 
 // x ^= y * skew[S]   (bitsliced; S is a compile-time skew index).  Shared sub-sums of the
 // 16x16 network (kCse*, gen_consts.cpp) are computed once: ~36 VALU ops on average.
-template <int S>
+// TAB 0: the cheapest programs (subset and cancellation greedies, ~32.8 VALU); TAB 1: the
+// subset greedy's (~35.2), for decode_c and decode_pk, whose register allocation spills with
+// TAB 0.
+template <int S, int TAB = 0>
 __device__ __forceinline__ void mul_acc(uint32_t* x, const uint32_t* y) {
   static_assert(S >= 0 && S < kSkewConstCount, "skew index outside generated table");
-  constexpr int NT = kCseNTemps[S];
-  uint32_t sig[16 + kCseMaxTemps];
+  constexpr int NT = TAB ? kCseSubNTemps[S] : kCseNTemps[S];
+  uint32_t sig[16 + (kCseMaxTemps > kCseSubMaxTemps ? kCseMaxTemps : kCseSubMaxTemps)];
   static_for<16>([&](auto I) { sig[decltype(I)::value] = y[decltype(I)::value]; });
   static_for<NT>([&](auto J) {
     constexpr int j = decltype(J)::value;
-    constexpr int a = kCseTemp[S][j][0], b = kCseTemp[S][j][1], c = kCseTemp[S][j][2];
+    constexpr int a = TAB ? kCseSubTemp[S][j][0] : kCseTemp[S][j][0];
+    constexpr int b = TAB ? kCseSubTemp[S][j][1] : kCseTemp[S][j][1];
+    constexpr int c = TAB ? kCseSubTemp[S][j][2] : kCseTemp[S][j][2];
     if constexpr (c == 255) sig[16 + j] = sig[a] ^ sig[b]; else sig[16 + j] = xor3(sig[a], sig[b], sig[c]);
   });
   static_for<16>([&](auto O) {
     constexpr int o = decltype(O)::value;
-    x[o] = xsum64<kCseRow[S][o]>(x[o], sig);
+    x[o] = xsum64<TAB ? kCseSubRow[S][o] : kCseRow[S][o]>(x[o], sig);
   });
 }
 
@@ -175,16 +180,16 @@ __device__ __forceinline__ void xor_planes(uint32_t* y, const uint32_t* x) {
 }
 
 // FFT butterfly (crate fft_butterfly_two): x ^= y * skew; y ^= x.
-template <int S>
+template <int S, int TAB = 0>
 __device__ __forceinline__ void fft_bfly(uint32_t* x, uint32_t* y) {
-  if constexpr (kSkewLog[S] != 65535) mul_acc<S>(x, y);
+  if constexpr (kSkewLog[S] != 65535) mul_acc<S, TAB>(x, y);
   xor_planes(y, x);
 }
 // IFFT butterfly (crate ifft_butterfly_two): y ^= x; x ^= y * skew.
-template <int S>
+template <int S, int TAB = 0>
 __device__ __forceinline__ void ifft_bfly(uint32_t* x, uint32_t* y) {
   xor_planes(y, x);
-  if constexpr (kSkewLog[S] != 65535) mul_acc<S>(x, y);
+  if constexpr (kSkewLog[S] != 65535) mul_acc<S, TAB>(x, y);
 }
 
 // ---- XCD-aware tile order ----------------------------------------------------------

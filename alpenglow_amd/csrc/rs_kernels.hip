@@ -845,6 +845,8 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
 // 32, 0 the LowRate sub-window); only those geometries launch it.  Requires any_k (at most k
 // survivors per pattern) and 16 chunks per shard.
 // =====================================================================================
+// The transform's multiplies use the subset-greedy programs (TAB 1, rs_device.hpp mul_acc): with
+// the cancellation programs this kernel's allocation spills (14 VGPRs).
 template <int OUTH>
 __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p) {
   static_assert(OUTH == 0 || OUTH == 1, "the restored originals lie in one window half");
@@ -959,16 +961,16 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
   });
   __syncthreads();  // every item read: the buffer becomes the swap regions
   // IFFT_64
-  h8_layer0<true, 0>(wave, h, r);
+  h8_layer0<true, 0, 1>(wave, h, r);
   h8_relayout(r);
-  x8_layer_t<LB, 1, true, 0>(wave, r);
-  x8_layer_t<LB, 2, true, 0>(wave, r);
+  x8_layer_t<LB, 1, true, 0, 1>(wave, r);
+  x8_layer_t<LB, 2, true, 0, 1>(wave, r);
   x8_swap<1, 0, 1, 0xF, false>(wave, lane, lds, &flags, r);
-  x8_layer_t<LC, 3, true, 0>(wave, r);
+  x8_layer_t<LC, 3, true, 0, 1>(wave, r);
   x8_swap<0, 1, 2, 0xF, false>(wave, lane, lds, &flags, r);
-  x8_layer_t<LD, 4, true, 0>(wave, r);
+  x8_layer_t<LD, 4, true, 0, 1>(wave, r);
   x8_swap<1, 2, 3, 0xF, false>(wave, lane, lds, &flags, r);
-  x8_layer_t<LE, 5, true, 0>(wave, r);
+  x8_layer_t<LE, 5, true, 0, 1>(wave, r);
   // formal derivative in E (decode_h8's, epochs 4 and 5)
   auto wait_readers = [&](int x, uint32_t e) __attribute__((always_inline)) {
     static_for<3>([&](auto Bb) {
@@ -1004,8 +1006,8 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
     x8_signal(&flags.done[wave], e, lane);
   });
   // FFT_64 down to A; the waves of the other window half hand over their live slots and retire
-  x8_layer_t<LE, 5, false, 0>(wave, r);
-  x8_layer_t<LE, 4, false, 0>(wave, r);
+  x8_layer_t<LE, 5, false, 0, 1>(wave, r);
+  x8_layer_t<LE, 4, false, 0, 1>(wave, r);
   wait_readers(wave ^ 4, 5);
   {
     const int partner = wave ^ 4;
@@ -1031,13 +1033,13 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
     });
     x8_signal(&flags.done[wave], 4 + D, lane);
   }
-  x8_layer_t<LD, 3, false, 0>(wave, r);
+  x8_layer_t<LD, 3, false, 0, 1>(wave, r);
   x8_swap<0, 1, 5 + D, 0xF, false>(wave, lane, lds, &flags, r);
-  x8_layer_t<LC, 2, false, 0>(wave, r);
+  x8_layer_t<LC, 2, false, 0, 1>(wave, r);
   x8_swap<1, 0, 6 + D, 0xF, false>(wave, lane, lds, &flags, r);
-  x8_layer_t<LB, 1, false, 0>(wave, r);
+  x8_layer_t<LB, 1, false, 0, 1>(wave, r);
   h8_relayout(r);
-  h8_layer0<false, 0>(wave, h, r);
+  h8_layer0<false, 0, 1>(wave, h, r);
   // 4. packed output products.  Every live wave's last swap read is done before any item
   // overwrites a region; items written, then every live wave's items visible before reads.
   const int lw = wave & 3;  // live waves: wave bit 2 == OUTH

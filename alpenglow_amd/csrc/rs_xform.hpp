@@ -420,93 +420,93 @@ constexpr int x8_expand(int v, int rel) {
 
 // The butterfly on slots (T, T | 2^i) of layer bit B in layout Lay for the wave bits V.
 // FFT butterflies with upd_y false skip y ^= x (y's new value is never used).
-template <typename Lay, int B, bool INV, int DELTA, int T, int V>
+template <typename Lay, int B, bool INV, int DELTA, int T, int V, int TAB = 0>
 __device__ __forceinline__ void x8_bfly(uint32_t* x, uint32_t* y, bool upd_y) {
   constexpr int w = x8_expand(V, Lay::rel(B));
   constexpr int S = (Lay::pos(w, T) & ~((2 << B) - 1)) + (1 << B) + DELTA - 1;
   if constexpr (INV) {
-    dev::ifft_bfly<S>(x, y);
+    dev::ifft_bfly<S, TAB>(x, y);
   } else {
-    if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(x, y);
+    if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S, TAB>(x, y);
     if (upd_y) dev::xor_planes(y, x);
   }
 }
-template <typename Lay, int B, bool INV, int DELTA, int T>
+template <typename Lay, int B, bool INV, int DELTA, int T, int TAB = 0>
 __device__ __forceinline__ void x8_bfly_w(int v, uint32_t* x, uint32_t* y, bool upd_y = true) {
   constexpr int n = 1 << x8_popc(Lay::rel(B));
   if constexpr (n == 1) {
-    x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y);
+    x8_bfly<Lay, B, INV, DELTA, T, 0, TAB>(x, y, upd_y);
   } else if constexpr (n == 2) {
-    if (v == 0) x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); else x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y);
+    if (v == 0) x8_bfly<Lay, B, INV, DELTA, T, 0, TAB>(x, y, upd_y); else x8_bfly<Lay, B, INV, DELTA, T, 1, TAB>(x, y, upd_y);
   } else if constexpr (n == 4) {
     switch (v) {
-      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); break;
-      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y); break;
-      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2>(x, y, upd_y); break;
-      default: x8_bfly<Lay, B, INV, DELTA, T, 3>(x, y, upd_y); break;
+      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0, TAB>(x, y, upd_y); break;
+      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1, TAB>(x, y, upd_y); break;
+      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2, TAB>(x, y, upd_y); break;
+      default: x8_bfly<Lay, B, INV, DELTA, T, 3, TAB>(x, y, upd_y); break;
     }
   } else if constexpr (n == 8) {
     switch (v) {
-      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); break;
-      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y); break;
-      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2>(x, y, upd_y); break;
-      case 3: x8_bfly<Lay, B, INV, DELTA, T, 3>(x, y, upd_y); break;
-      case 4: x8_bfly<Lay, B, INV, DELTA, T, 4>(x, y, upd_y); break;
-      case 5: x8_bfly<Lay, B, INV, DELTA, T, 5>(x, y, upd_y); break;
-      case 6: x8_bfly<Lay, B, INV, DELTA, T, 6>(x, y, upd_y); break;
-      default: x8_bfly<Lay, B, INV, DELTA, T, 7>(x, y, upd_y); break;
+      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0, TAB>(x, y, upd_y); break;
+      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1, TAB>(x, y, upd_y); break;
+      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2, TAB>(x, y, upd_y); break;
+      case 3: x8_bfly<Lay, B, INV, DELTA, T, 3, TAB>(x, y, upd_y); break;
+      case 4: x8_bfly<Lay, B, INV, DELTA, T, 4, TAB>(x, y, upd_y); break;
+      case 5: x8_bfly<Lay, B, INV, DELTA, T, 5, TAB>(x, y, upd_y); break;
+      case 6: x8_bfly<Lay, B, INV, DELTA, T, 6, TAB>(x, y, upd_y); break;
+      default: x8_bfly<Lay, B, INV, DELTA, T, 7, TAB>(x, y, upd_y); break;
     }
   } else {
     switch (v) {
-      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0>(x, y, upd_y); break;
-      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1>(x, y, upd_y); break;
-      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2>(x, y, upd_y); break;
-      case 3: x8_bfly<Lay, B, INV, DELTA, T, 3>(x, y, upd_y); break;
-      case 4: x8_bfly<Lay, B, INV, DELTA, T, 4>(x, y, upd_y); break;
-      case 5: x8_bfly<Lay, B, INV, DELTA, T, 5>(x, y, upd_y); break;
-      case 6: x8_bfly<Lay, B, INV, DELTA, T, 6>(x, y, upd_y); break;
-      case 7: x8_bfly<Lay, B, INV, DELTA, T, 7>(x, y, upd_y); break;
-      case 8: x8_bfly<Lay, B, INV, DELTA, T, 8>(x, y, upd_y); break;
-      case 9: x8_bfly<Lay, B, INV, DELTA, T, 9>(x, y, upd_y); break;
-      case 10: x8_bfly<Lay, B, INV, DELTA, T, 10>(x, y, upd_y); break;
-      case 11: x8_bfly<Lay, B, INV, DELTA, T, 11>(x, y, upd_y); break;
-      case 12: x8_bfly<Lay, B, INV, DELTA, T, 12>(x, y, upd_y); break;
-      case 13: x8_bfly<Lay, B, INV, DELTA, T, 13>(x, y, upd_y); break;
-      case 14: x8_bfly<Lay, B, INV, DELTA, T, 14>(x, y, upd_y); break;
-      default: x8_bfly<Lay, B, INV, DELTA, T, 15>(x, y, upd_y); break;
+      case 0: x8_bfly<Lay, B, INV, DELTA, T, 0, TAB>(x, y, upd_y); break;
+      case 1: x8_bfly<Lay, B, INV, DELTA, T, 1, TAB>(x, y, upd_y); break;
+      case 2: x8_bfly<Lay, B, INV, DELTA, T, 2, TAB>(x, y, upd_y); break;
+      case 3: x8_bfly<Lay, B, INV, DELTA, T, 3, TAB>(x, y, upd_y); break;
+      case 4: x8_bfly<Lay, B, INV, DELTA, T, 4, TAB>(x, y, upd_y); break;
+      case 5: x8_bfly<Lay, B, INV, DELTA, T, 5, TAB>(x, y, upd_y); break;
+      case 6: x8_bfly<Lay, B, INV, DELTA, T, 6, TAB>(x, y, upd_y); break;
+      case 7: x8_bfly<Lay, B, INV, DELTA, T, 7, TAB>(x, y, upd_y); break;
+      case 8: x8_bfly<Lay, B, INV, DELTA, T, 8, TAB>(x, y, upd_y); break;
+      case 9: x8_bfly<Lay, B, INV, DELTA, T, 9, TAB>(x, y, upd_y); break;
+      case 10: x8_bfly<Lay, B, INV, DELTA, T, 10, TAB>(x, y, upd_y); break;
+      case 11: x8_bfly<Lay, B, INV, DELTA, T, 11, TAB>(x, y, upd_y); break;
+      case 12: x8_bfly<Lay, B, INV, DELTA, T, 12, TAB>(x, y, upd_y); break;
+      case 13: x8_bfly<Lay, B, INV, DELTA, T, 13, TAB>(x, y, upd_y); break;
+      case 14: x8_bfly<Lay, B, INV, DELTA, T, 14, TAB>(x, y, upd_y); break;
+      default: x8_bfly<Lay, B, INV, DELTA, T, 15, TAB>(x, y, upd_y); break;
     }
   }
 }
 // One butterfly layer on position bit B in layout L (skew delta DELTA).  LIVE: the slots
 // that still carry needed values (half-pruned FFT); UPD_Y false: FFT x updates only.
-template <int L, int B, bool INV, int DELTA, int LIVE = 0xF, bool UPD_Y = true>
+template <int L, int B, bool INV, int DELTA, int LIVE = 0xF, bool UPD_Y = true, int TAB = 0>
 __device__ __forceinline__ void x8_layer(int wave, Regs4& r) {
   using Lay = X8Layout<L>;
   constexpr int i = Lay::slot_of(B);
   static_assert(i >= 0, "layer bit must be a slot bit");
   const int v = x8_compress<Lay::rel(B)>(wave);
   constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;  // the slots with bit i clear
-  if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)], UPD_Y);
-  if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)], UPD_Y);
+  if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, INV, DELTA, t0, TAB>(v, r[t0], r[t0 | (1 << i)], UPD_Y);
+  if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, INV, DELTA, t1, TAB>(v, r[t1], r[t1 | (1 << i)], UPD_Y);
 }
 // the same on an explicit layout type (xform8's pruned FFT layouts, decode_x16's layouts)
-template <typename Lay, int B, bool INV, int DELTA>
+template <typename Lay, int B, bool INV, int DELTA, int TAB = 0>
 __device__ __forceinline__ void x8_layer_t(int wave, Regs4& r) {
   constexpr int i = Lay::slot_of(B);
   static_assert(i >= 0, "layer bit must be a slot bit");
   const int v = x8_compress<Lay::rel(B)>(wave);
   constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;
-  x8_bfly_w<Lay, B, INV, DELTA, t0>(v, r[t0], r[t0 | (1 << i)]);
-  x8_bfly_w<Lay, B, INV, DELTA, t1>(v, r[t1], r[t1 | (1 << i)]);
+  x8_bfly_w<Lay, B, INV, DELTA, t0, TAB>(v, r[t0], r[t0 | (1 << i)]);
+  x8_bfly_w<Lay, B, INV, DELTA, t1, TAB>(v, r[t1], r[t1 | (1 << i)]);
 }
-template <typename Lay, int B, int DELTA, int LIVE>
+template <typename Lay, int B, int DELTA, int LIVE, int TAB = 0>
 __device__ __forceinline__ void x8_layer_lay(int wave, Regs4& r) {
   constexpr int i = Lay::slot_of(B);
   static_assert(i >= 0, "layer bit must be a slot bit");
   const int v = x8_compress<Lay::rel(B)>(wave);
   constexpr int t0 = 0, t1 = i == 0 ? 2 : 1;
-  if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, false, DELTA, t0>(v, r[t0], r[t0 | (1 << i)]);
-  if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, false, DELTA, t1>(v, r[t1], r[t1 | (1 << i)]);
+  if constexpr ((LIVE >> t0) & 1) x8_bfly_w<Lay, B, false, DELTA, t0, TAB>(v, r[t0], r[t0 | (1 << i)]);
+  if constexpr ((LIVE >> t1) & 1) x8_bfly_w<Lay, B, false, DELTA, t1, TAB>(v, r[t1], r[t1 | (1 << i)]);
 }
 
 // Slot bit I <-> wave bit J.  Slot t of wave w moves iff t_I != w_J: to slot t ^ 2^I of
@@ -566,14 +566,14 @@ __device__ __forceinline__ void x8_swap(int wave, int lane, uint4* lds, Flags* f
 // Lane l holds column l & 31 of the tile; h = l >> 5 is position bit 2 in layout A (slots p0
 // p1 | h p2 | waves p3 p4 p5).  A <-> B (h8_relayout) trades slot bit 0 and the lane half.
 // The layer-0 butterfly of layout A; HPOS = the lane half's position bit (4 or 0).
-template <typename Lay, int B, bool INV, int DELTA, int T, int V, int HPOS>
+template <typename Lay, int B, bool INV, int DELTA, int T, int V, int HPOS, int TAB = 0>
 __device__ __forceinline__ void h8_bfly(uint32_t* x, uint32_t* y) {
   constexpr int w = x8_expand(V, Lay::rel(B));
   constexpr int S = ((Lay::pos(w, T) | HPOS) & ~((2 << B) - 1)) + (1 << B) + DELTA - 1;
-  if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S>(x, y);
+  if constexpr (kSkewLog[S] != 65535) dev::mul_acc<S, TAB>(x, y);
 }
 // layer 0 in layout A: butterflies on slots (0, 1) and (2, 3); the lane half is p2
-template <bool INV, int DELTA>
+template <bool INV, int DELTA, int TAB = 0>
 __device__ __forceinline__ void h8_layer0(int wave, int h, Regs4& r) {
   using LA = X8Lay<0, 1, 3, 4, 5>;
   static_for<2>([&](auto TT) {
@@ -581,8 +581,8 @@ __device__ __forceinline__ void h8_layer0(int wave, int h, Regs4& r) {
     if constexpr (INV) dev::xor_planes(r[t + 1], r[t]);
     auto mul = [&](auto Vc) {
       constexpr int v = decltype(Vc)::value;
-      if (h) h8_bfly<LA, 0, INV, DELTA, t, v, 4>(r[t], r[t + 1]);
-      else h8_bfly<LA, 0, INV, DELTA, t, v, 0>(r[t], r[t + 1]);
+      if (h) h8_bfly<LA, 0, INV, DELTA, t, v, 4, TAB>(r[t], r[t + 1]);
+      else h8_bfly<LA, 0, INV, DELTA, t, v, 0, TAB>(r[t], r[t + 1]);
     };
     switch (wave) {  // every wave bit lies above bit 0
       case 0: mul(std::integral_constant<int, 0>{}); break;
