@@ -74,7 +74,9 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
     const uint32_t s = 8 * wave + t;  // wave-uniform
-    if (s < p.n_out) store_shard(p.out + s * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, ra[t]);
+    const uint32_t q = (qall >> (4 * t)) & 15u;
+    // a slot no lane stores skips its planes -> bytes conversion (a decode restores a subset)
+    if (s < p.n_out && __builtin_amdgcn_ballot_w64(q != 0) != 0) store_shard(p.out + s * p.out_shard_stride, out_io, q, ra[t]);
   });
 }
 
@@ -2100,6 +2102,8 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
     case XformKind::kDecode32:
       if (p.out_low_half)
         hipLaunchKernelGGL((xform8_kernel<0, 32, true>), grid, dim3(512), 0, stream, p);
+      else if (getenv("AG_DIAG_X4DEC"))
+        hipLaunchKernelGGL((xform_kernel<4, 0, 32>), grid, dim3(256), 0, stream, p);
       else
         hipLaunchKernelGGL((xform8_kernel<0, 32>), grid, dim3(512), 0, stream, p);
       break;
