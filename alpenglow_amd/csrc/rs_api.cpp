@@ -366,11 +366,18 @@ int encode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
     } else if (mc) {
       e = ag::launch_encode_mc(mc, p, c->stream);
     } else {
-      for (size_t j = 0; j * lr < m && e == hipSuccess; ++j) {  // one launch per recovery chunk
+      for (size_t j = 0; j * lr < m && e == hipSuccess;) {  // one launch per recovery chunk
         ag::XformParams pj = p;
         pj.out = rec + j * lr * sstride;
+        if (lr == 32 && j % 2 == 0 && (j + 1) * lr < m && j < 4) {  // chunks j, j + 1 in one launch
+          pj.n_out = static_cast<uint32_t>(std::min<size_t>(2 * lr, m - j * lr));
+          e = ag::launch_xform_lowrate2(static_cast<unsigned>(j / 2), pj, c->stream);
+          j += 2;
+          continue;
+        }
         pj.n_out = static_cast<uint32_t>(std::min<size_t>(lr, m - j * lr));
         e = ag::launch_xform_lowrate(lr, static_cast<unsigned>(j), pj, c->stream);
+        ++j;
       }
     }
     return e == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
@@ -2581,7 +2588,7 @@ int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, si
   if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(k * S), n, strip, c->stream) != hipSuccess ||
       ag::launch_pipe_store_masks(few, strip, n, c->d_pipe_mask.as<uint64_t>(), c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
-  for (unsigned j = 0; j * 32 < m; ++j) {  // one launch per recovery chunk (encode_cols' LowRate loop)
+  for (unsigned j = 0; j * 32 < m;) {  // the recovery chunks, two per launch (encode_cols' LowRate loop)
     ag::XformParams xp{};
     xp.in = cw;
     xp.in_block_stride = cw_stride;
@@ -2589,13 +2596,17 @@ int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, si
     xp.out = cw + (k + 32 * j) * S;
     xp.out_block_stride = cw_stride;
     xp.out_shard_stride = S;
-    xp.out_mask = c->d_pipe_mask.as<uint64_t>();
+    xp.out_mask = c->d_pipe_mask.as<uint64_t>();  // all or none of a slice's coding shreds
     xp.pattern_per_block = 1;
     xp.n_in = static_cast<uint32_t>(k);
-    xp.n_out = 32;
     xp.chunks_per_shard = static_cast<uint32_t>(cps);
     xp.total_columns = static_cast<uint64_t>(n) * cps;
-    if (ag::launch_xform_lowrate(32, j, xp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    const bool pair = j % 2 == 0 && (j + 1) * 32 < m && j < 4;
+    xp.n_out = pair ? static_cast<uint32_t>(std::min<size_t>(64, m - 32 * j)) : 32;
+    if ((pair ? ag::launch_xform_lowrate2(j / 2, xp, c->stream) : ag::launch_xform_lowrate(32, j, xp, c->stream)) !=
+        hipSuccess)
+      return AG_RS_ERR_DEVICE;
+    j += pair ? 2 : 1;
   }
   return pipe_coder_finish(c, n, strip, few, plen);
 }

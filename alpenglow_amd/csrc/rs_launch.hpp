@@ -54,6 +54,9 @@ hipError_t launch_xform64(unsigned din, unsigned dout, const XformParams& p, hip
 // LowRate encode, recovery chunk j: out = FFT_n(IFFT_n(in, 0), n * (j + 1)) for
 // n = next_pow2(k) in {32 (j < 4), 64 (j < 3)} -- the crate's LowRate encoder per chunk.
 hipError_t launch_xform_lowrate(unsigned n, unsigned j, const XformParams& p, hipStream_t stream);
+// LowRate recovery chunks 2 pair and 2 pair + 1 of a 32-point code (k <= 32) in one launch
+// (xform_h8 LR2): in = the k originals, out = recovery shard 64 pair, n_out <= 64.
+hipError_t launch_xform_lowrate2(unsigned pair, const XformParams& p, hipStream_t stream);
 // LowRate decode from a fully present recovery chunk j < 4 (next_pow2(k) = 32):
 // originals = FFT_0(IFFT_{32(j+1)}(chunk j)); in = chunk j, out = originals (masked).
 hipError_t launch_xform_lowrate_decode(unsigned j, const XformParams& p, hipStream_t stream);

@@ -34,7 +34,14 @@ using dev::static_for;
 // HALF: every stored shard is < 32 (position bit 5 clear; a reconstruct whose erased originals
 // all lie in shards 0..31): after FFT layer 4 the waves whose slots would hold p5 = 1 hand
 // over their live slots and retire (decode_h8's OUTH pruning).
-template <int DIN, int DOUT, bool HALF = false>
+// LR2: two LowRate recovery chunks of a 32-point code (k <= 32) in one launch.  The crate's
+// chunk j is FFT_32,32(j+1)(IFFT_32,0(data)); FFT_64,δ of (u, 0) is (FFT_32,δ(u),
+// FFT_32,δ+32(u)) because its top layer maps (u, 0) to (u, u) for any skew.  So with the data in
+// positions 0..31 and nothing in 32..63, the IFFT stops before its top layer (layers 0-4 are
+// the 32-point IFFT of each half; the empty half stays zero, and its waves skip them) and the
+// FFT_64 at δ = 32(2i + 1) yields chunks 2i and 2i + 1 as positions 0..63: the data is read
+// once and its IFFT computed once for both chunks.
+template <int DIN, int DOUT, bool HALF = false, bool LR2 = false>
 __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
   using LB = X8Lay<2, 1, 3, 4, 5>;
   using LC = X8Lay<2, 3, 1, 4, 5>;
@@ -71,17 +78,21 @@ __global__ __launch_bounds__(512, 4) void xform_h8_kernel(const XformParams p) {
     quad_exchange(r[decltype(T)::value], lane);
     dev::planes_from_raw(r[decltype(T)::value]);
   });
-  // IFFT_64 (skew delta DIN)
-  h8_layer0<true, DIN>(wave, h, r);
-  h8_relayout(r);
-  x8_layer_t<LB, 1, true, DIN>(wave, r);
-  x8_layer_t<LB, 2, true, DIN>(wave, r);
+  // IFFT_64 (skew delta DIN); LR2: the waves of the empty half (p5 = wave bit 2 in A-D) hold
+  // zeros through layer 4, and the top layer is not applied
+  const bool ifft = !LR2 || !((wave >> 2) & 1);
+  if (ifft) {
+    h8_layer0<true, DIN>(wave, h, r);
+    h8_relayout(r);
+    x8_layer_t<LB, 1, true, DIN>(wave, r);
+    x8_layer_t<LB, 2, true, DIN>(wave, r);
+  }
   x8_swap<1, 0, 1>(wave, lane, lds, &flags, r);
-  x8_layer_t<LC, 3, true, DIN>(wave, r);
+  if (ifft) x8_layer_t<LC, 3, true, DIN>(wave, r);
   x8_swap<0, 1, 2>(wave, lane, lds, &flags, r);
-  x8_layer_t<LD, 4, true, DIN>(wave, r);
+  if (ifft) x8_layer_t<LD, 4, true, DIN>(wave, r);
   x8_swap<1, 2, 3>(wave, lane, lds, &flags, r);
-  x8_layer_t<LE, 5, true, DIN>(wave, r);
+  if constexpr (!LR2) x8_layer_t<LE, 5, true, DIN>(wave, r);
   // FFT_64 (skew delta DOUT), ending in A
   x8_layer_t<LE, 5, false, DOUT>(wave, r);
   x8_layer_t<LE, 4, false, DOUT>(wave, r);
@@ -179,6 +190,18 @@ hipError_t launch_xform64(unsigned din, unsigned dout, const XformParams& p, hip
   else if (din == 0 && dout == 64) hipLaunchKernelGGL((xform_h8_kernel<0, 64>), g32, dim3(512), 0, stream, p);
   else if (din == 0 && dout == 128) hipLaunchKernelGGL((xform_h8_kernel<0, 128>), g32, dim3(512), 0, stream, p);
   else if (din == 0 && dout == 192) hipLaunchKernelGGL((xform_h8_kernel<0, 192>), g32, dim3(512), 0, stream, p);
+  else return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+hipError_t launch_xform_lowrate2(unsigned pair, const XformParams& p, hipStream_t stream) {
+  if (p.total_columns == 0) return hipSuccess;
+  if (p.n_in > 32 || p.n_out > 64) return hipErrorInvalidValue;
+  const uint64_t t32 = (p.total_columns + 31) / 32;
+  if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  const dim3 g32(static_cast<unsigned>(t32));
+  if (pair == 0) hipLaunchKernelGGL((xform_h8_kernel<0, 32, false, true>), g32, dim3(512), 0, stream, p);
+  else if (pair == 1) hipLaunchKernelGGL((xform_h8_kernel<0, 96, false, true>), g32, dim3(512), 0, stream, p);
   else return hipErrorInvalidValue;
   return hipGetLastError();
 }

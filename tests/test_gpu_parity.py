@@ -149,7 +149,8 @@ def test_multichunk_small_encode(ctx, dev, k, m, S):
 @pytest.mark.parametrize("k,m,S", [(32, 64, 1024), (32, 33, 4096), (20, 100, 128), (32, 20, 192), (17, 128, 64),
                                    (64, 33, 256), (40, 128, 128), (64, 192, 64)])
 def test_lowrate_encode_transform(ctx, dev, k, m, S):
-    """LowRate (CodingOnly 32:64, PETS 32:33, ...): one transform launch per recovery chunk."""
+    """LowRate (CodingOnly 32:64, PETS 32:33, ...): two recovery chunks per launch for 32-point
+    codes (pairs 0-1 and 2-3, odd counts and partial pairs included), one per chunk for 64-point."""
     assert rs.has_fast_path(k, m, S) and not rs.use_high_rate(k, m)
     n = 5
     blocks = np.stack([np.frombuffer(o.block_bytes(1100 + b, k * S), np.uint8).reshape(k, S) for b in range(n)])
