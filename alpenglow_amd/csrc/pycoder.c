@@ -17,19 +17,41 @@
 
 typedef __typeof__(ag_rs_coder_shred)* shred_fn;
 typedef __typeof__(ag_rs_coder_deshred)* deshred_fn;
+typedef __typeof__(ag_rs_coder_num_coding)* num_coding_fn;
 
 static shred_fn g_shred;
 static deshred_fn g_deshred;
+static num_coding_fn g_num_coding;
 
 enum { kTotal = AG_RS_TOTAL_SHREDS, kData = AG_RS_DATA_SHREDS };
 
 static PyObject* bind(PyObject* self, PyObject* args) {
-  unsigned long long a, b;
+  unsigned long long a, b, n;
   (void)self;
-  if (!PyArg_ParseTuple(args, "KK", &a, &b)) return NULL;
+  if (!PyArg_ParseTuple(args, "KKK", &a, &b, &n)) return NULL;
   g_shred = (shred_fn)(uintptr_t)a;
   g_deshred = (deshred_fn)(uintptr_t)b;
+  g_num_coding = (num_coding_fn)(uintptr_t)n;
   Py_RETURN_NONE;
+}
+
+/* The library writes num_coding * S coding bytes whatever the caller says: the caller's count
+ * must be the coder's own, or the bytes object it sizes would overflow. */
+static int check_num_coding(unsigned long long h, Py_ssize_t nc) {
+  size_t own = 0;
+  if (nc < 0) {
+    PyErr_Format(PyExc_ValueError, "num_coding %zd < 0", nc);
+    return -1;
+  }
+  if (g_num_coding((const ag_rs_coder*)(uintptr_t)h, &own) != 0) {
+    PyErr_Format(PyExc_ValueError, "pycoder: not a coder handle");
+    return -1;
+  }
+  if ((size_t)nc != own) {
+    PyErr_Format(PyExc_ValueError, "num_coding %zd, the coder has %zu", nc, own);
+    return -1;
+  }
+  return 0;
 }
 
 /* shred(coder, payload, num_coding) -> (status, data, coding, S): data / coding are the
@@ -41,6 +63,10 @@ static PyObject* shred(PyObject* self, PyObject* args) {
   (void)self;
   if (!g_shred) return PyErr_Format(PyExc_RuntimeError, "pycoder: bind() not called");
   if (!PyArg_ParseTuple(args, "Ky*n", &h, &pay, &nc)) return NULL;
+  if (check_num_coding(h, nc) < 0) {
+    PyBuffer_Release(&pay);
+    return NULL;
+  }
   /* padding 0x80 00.. to a multiple of 2 * DATA_SHREDS: S as the library computes it */
   const size_t len = (size_t)pay.len;
   const size_t S = (len + (2 * kData - len % (2 * kData))) / kData;
@@ -112,6 +138,7 @@ static PyObject* deshred(PyObject* self, PyObject* args) {
     isd[i] = (uint8_t)flag;
     if (lens[i] > cap) cap = lens[i];
   }
+  if (check_num_coding(h, nc) < 0) goto done;
   {
     PyObject* payload = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)(kData * cap));
     PyObject* data = PyBytes_FromStringAndSize(NULL, (Py_ssize_t)(kData * cap));
@@ -149,7 +176,7 @@ done:
 }
 
 static PyMethodDef methods[] = {
-    {"bind", bind, METH_VARARGS, "bind(shred_addr, deshred_addr)"},
+    {"bind", bind, METH_VARARGS, "bind(shred_addr, deshred_addr, num_coding_addr)"},
     {"shred", shred, METH_VARARGS, "shred(coder, payload, num_coding) -> (status, data, coding, S)"},
     {"deshred", deshred, METH_VARARGS, "deshred(coder, shreds, data_shreds, num_coding) -> (status, payload, data, coding, S)"},
     {NULL, NULL, 0, NULL}};

@@ -161,6 +161,7 @@ struct ag_rs_ctx {
   DevBuf d_x128, d_rows128;                 // W = 128 two-pass decode: masks, constants
   uint64_t last_classes[16] = {};           // patterns per decoder class of the last decode call
   int decode_depth = 0;                     // decode_device nesting (tail restrides decode inside)
+  uint32_t last_encode_kernels = 0;         // EncodeKernelBit of the last ag_rs_encode_batch call
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
   DevBuf d_corr, d_corrk, d_corrblocks;     // correction decoder: patterns, K picks, block ids
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
@@ -190,6 +191,7 @@ struct ag_rs_ctx {
   hipStream_t server_stream = nullptr;
   uint32_t server_seq = 0;
   bool server_broken = false;  // a job timed out: the server path is off for this context
+  std::vector<PinBuf> abandoned_pins;  // staging a timed-out job named (freed once the server is gone)
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
   std::vector<uint64_t> stage_mask_host;  // last restride masks uploaded to stage_mask
   std::vector<uint64_t> xmask_host;       // last general-decode masks (d_xmask), W = xmask_w
@@ -257,7 +259,18 @@ struct ag_rs_ctx {
              std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2)) {
       }
     }
-    (void)hipStreamSynchronize(server_stream);  // the server exits on quit or its idle timeout
+    if (__atomic_load_n(&mb->alive, __ATOMIC_ACQUIRE) != 0) {
+      // a server that neither served nor quit (server_broken): waiting on its stream could
+      // block forever, and it may still write the mailbox or an abandoned staging buffer,
+      // so those stay allocated
+      mb = mb_dev = nullptr;
+      server_stream = nullptr;
+      abandoned_pins.clear();
+      return;
+    }
+    (void)hipStreamSynchronize(server_stream);  // the server has exited (quit or idle timeout)
+    for (PinBuf& b : abandoned_pins) b.release();
+    abandoned_pins.clear();
     (void)hipStreamDestroy(server_stream);
     (void)hipHostFree(mb);
     mb = mb_dev = nullptr;
@@ -326,6 +339,7 @@ int encode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t Sv, size_t sstride
   const size_t group = std::max<size_t>(1, kRestrideGroupBytes / per_block);
   int st = c->stage_pad.ensure(std::min(group, nblocks) * per_block, c->stream);
   if (st) return st;
+  c->last_encode_kernels |= ag::kEkRestride;
   uint8_t* pad = c->stage_pad.as<uint8_t>();
   for (size_t b0 = 0; b0 < nblocks; b0 += group) {
     const size_t nb = std::min(group, nblocks - b0);
@@ -362,8 +376,10 @@ int encode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
     p.total_columns = static_cast<uint64_t>(nblocks) * (S / 64);
     hipError_t e = hipSuccess;
     if (npts) {
+      c->last_encode_kernels |= npts == 32 ? ag::encode32_kernel(p) : ag::kEkXformH8;
       e = ag::launch_xform(npts == 32 ? ag::XformKind::kEncode32 : ag::XformKind::kEncode64, p, c->stream);
     } else if (mc) {
+      c->last_encode_kernels |= ag::kEkEncodeMc;
       e = ag::launch_encode_mc(mc, p, c->stream);
     } else {
       for (size_t j = 0; j * lr < m && e == hipSuccess;) {  // one launch per recovery chunk
@@ -371,11 +387,13 @@ int encode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
         pj.out = rec + j * lr * sstride;
         if (lr == 32 && j % 2 == 0 && (j + 1) * lr < m && j < 4) {  // chunks j, j + 1 in one launch
           pj.n_out = static_cast<uint32_t>(std::min<size_t>(2 * lr, m - j * lr));
+          c->last_encode_kernels |= ag::kEkLowRate2;
           e = ag::launch_xform_lowrate2(static_cast<unsigned>(j / 2), pj, c->stream);
           j += 2;
           continue;
         }
         pj.n_out = static_cast<uint32_t>(std::min<size_t>(lr, m - j * lr));
+        c->last_encode_kernels |= ag::kEkLowRate;
         e = ag::launch_xform_lowrate(lr, static_cast<unsigned>(j), pj, c->stream);
         ++j;
       }
@@ -410,6 +428,7 @@ int encode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
     p.nblocks = std::min(per_launch, nblocks - b0);
     p.scratch = c->scratch.as<uint16_t>();
     p.t = c->dtables();
+    c->last_encode_kernels |= ag::kEkGeneric;
     if (ag::launch_generic_encode(p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   }
   return AG_RS_OK;
@@ -944,6 +963,8 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
       p.tiles_per_block = static_cast<uint32_t>(cps / 64);
       for (size_t b = 0; b < nblocks; ++b)
         if (cls[b] == 8) ids.push_back(static_cast<uint32_t>(b));
+      // count before the upload below moves `ids` into the context
+      ntiles = static_cast<uint64_t>(ids.size()) * p.tiles_per_block;
       if (ids.size() != nblocks) {
         AG_HIP(hipStreamSynchronize(c->stream));  // a pending id upload may still read x128_ids
         if ((st = c->d_xblocks.ensure(ids.size() * 4, c->stream))) return st;
@@ -952,7 +973,6 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
                               c->stream));
         p.block_ids = c->d_xblocks.as<uint32_t>();
       }
-      ntiles = static_cast<uint64_t>(ids.size()) * p.tiles_per_block;
     }
     // recovery shards beyond the window half the kernel loads are addressed from p.rec with
     // the window position; launch_decode_x checks the geometry
@@ -1153,6 +1173,14 @@ int ag_rs_internal_last_decode_classes(ag_rs_ctx* c, uint64_t* out16) {
   return AG_RS_OK;
 }
 
+// Test aid (not in the header): the encode kernels (ag::EncodeKernelBit) the last
+// ag_rs_encode_batch call on this context launched.
+int ag_rs_internal_last_encode_kernels(ag_rs_ctx* c, uint32_t* out) {
+  if (!c || !out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = c->last_encode_kernels;
+  return AG_RS_OK;
+}
+
 int ag_rs_has_fast_path(size_t k, size_t m, size_t S) {
   // shard sizes that are not whole 64-byte chunks run restrided (padded) on the same kernels
   if (S == 0 || S % 2) return 0;
@@ -1167,6 +1195,7 @@ int ag_rs_encode_batch(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblock
   if (st) return st;
   if (ostride < k * S || rstride < m * S) return AG_RS_ERR_INVALID_ARGUMENT;
   if ((st = c->enter())) return st;
+  c->last_encode_kernels = 0;
   if (memory == AG_RS_MEM_DEVICE) return encode_device(c, k, m, S, nblocks, orig, ostride, rec, rstride);
   if (memory != AG_RS_MEM_HOST) return AG_RS_ERR_INVALID_ARGUMENT;
   // host memory: groups of blocks through two device staging slots, H2D / compute / D2H
@@ -1582,7 +1611,14 @@ int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t m
       }
     }
     if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+      // Retire the job: a queued or slow server that wakes later finds a quit job instead.
+      // It may already be inside the job, so the staging buffer the job names is abandoned
+      // (kept allocated, never reused) and later calls take the launch path.
       c->server_broken = true;
+      mb->kind = ag::kJobQuit;
+      __atomic_store_n(&mb->doorbell, ++c->server_seq, __ATOMIC_RELEASE);
+      c->abandoned_pins.push_back(c->one_pin);
+      c->one_pin = PinBuf{};
       return AG_RS_ERR_DEVICE;
     }
     __builtin_ia32_pause();
@@ -1909,6 +1945,12 @@ int ag_rs_coder_new_on_device(int device, size_t num_coding, ag_rs_coder** out) 
 }
 
 void ag_rs_coder_free(ag_rs_coder* c) { delete c; }
+
+int ag_rs_coder_num_coding(const ag_rs_coder* c, size_t* out) {
+  if (!c || !out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = c->num_coding;
+  return AG_RS_OK;
+}
 
 int ag_rs_coder_shred(ag_rs_coder* c, const uint8_t* payload, size_t len, uint8_t* data_out, uint8_t* coding_out,
                       size_t* shred_bytes) {

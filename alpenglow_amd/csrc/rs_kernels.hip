@@ -2094,7 +2094,7 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
       // by 0.03-0.31 TB/s at every other measured size (profiles/r04_encode_kernel_grid.txt; a
       // copy with either kernel's load/store skeleton shows no such dip, tools/membench/
       // membench7.hip, so it is the kernel's access order against that stride)
-      if (groups < 256 || p.chunks_per_shard == 128 || p.chunks_per_shard == 256)
+      if (encode32_kernel(p) == kEkXform8)
         hipLaunchKernelGGL((xform8_kernel<32, 0>), grid, dim3(512), 0, stream, p);
       else
         hipLaunchKernelGGL((xform_kernel<4, 32, 0>), grid, dim3(256), 0, stream, p);

@@ -28,6 +28,25 @@ struct XformParams {
 
 enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };
 
+// Encode kernels, as bits of the per-context record of the last encode call (test aid:
+// ag_rs_internal_last_encode_kernels).
+enum EncodeKernelBit : uint32_t {
+  kEkXform4 = 1u << 0,    // xform_kernel<4, 32, 0>: the headline 32-point encode
+  kEkXform8 = 1u << 1,    // xform8_kernel<32, 0>: small batches, 8 / 16 KiB shards
+  kEkXformH8 = 1u << 2,   // xform_h8: 64-point encode
+  kEkEncodeMc = 1u << 3,  // encode_mc: multi-chunk HighRate (16:4)
+  kEkLowRate = 1u << 4,   // xform_lowrate: one LowRate recovery chunk
+  kEkLowRate2 = 1u << 5,  // xform_h8 LR2: two LowRate chunks of a 32-point code
+  kEkGeneric = 1u << 6,   // generic_encode_kernel (table-driven)
+  kEkRestride = 1u << 7,  // tail bytes restrided through padded shards
+};
+// The 32-point encode kernel launch_xform(kEncode32, p) runs: xform8 for batches of fewer
+// than 256 tiles and for 8 / 16 KiB shards (chunks_per_shard 128 / 256), else xform<4>.
+inline EncodeKernelBit encode32_kernel(const XformParams& p) {
+  const uint64_t groups = (p.total_columns + 63) / 64;
+  return groups < 256 || p.chunks_per_shard == 128 || p.chunks_per_shard == 256 ? kEkXform8 : kEkXform4;
+}
+
 // The per-call server (latency_server_kernel): one resident workgroup per context serves
 // single-tile 32-point transforms posted through a mailbox in mapped, fine-grained host
 // memory, so a per-slice call costs no kernel dispatch and no completion signal.

@@ -72,7 +72,7 @@ EXPORTS = (
     "ag_rs_decoder_new", "ag_rs_decoder_reset", "ag_rs_decoder_add_original_shard",
     "ag_rs_decoder_add_recovery_shard", "ag_rs_decoder_decode",
     "ag_rs_decoder_restored_original", "ag_rs_decoder_free",
-    "ag_rs_coder_new", "ag_rs_coder_free", "ag_rs_coder_shred", "ag_rs_coder_deshred",
+    "ag_rs_coder_new", "ag_rs_coder_free", "ag_rs_coder_num_coding", "ag_rs_coder_shred", "ag_rs_coder_deshred",
     "ag_rs_encoder_new_on_device", "ag_rs_decoder_new_on_device", "ag_rs_coder_new_on_device",
     "ag_rs_coder_shred_batch", "ag_rs_coder_deshred_batch",
     "ag_merkle_empty_root", "ag_merkle_height", "ag_merkle_node_count", "ag_merkle_build_batch",
@@ -141,6 +141,7 @@ def load():
         "ag_rs_decoder_new_on_device": ([i, sz, sz, sz, pp], i),
         "ag_rs_coder_new_on_device": ([i, sz, pp], i),
         "ag_rs_coder_free": ([p], None),
+        "ag_rs_coder_num_coding": ([p, psz], i),
         "ag_rs_coder_shred": ([p, p, sz, p, p, psz], i),
         "ag_rs_coder_deshred": ([p, sz, p, p, p, p, psz, p, p, psz], i),
         "ag_rs_coder_shred_batch": ([p, sz, sz, sz, p, sz, p, p, sz], i),
@@ -168,6 +169,7 @@ def load():
         "ag_shredder_deshred_batch": ([p, sz, sz, p, sz, p, p, p, p, p, p, p, p, p, p, p], i),
     }
     sigs["ag_rs_internal_last_decode_classes"] = ([p, p], i)  # test aid, not in the header
+    sigs["ag_rs_internal_last_encode_kernels"] = ([p, p], i)  # test aid, not in the header
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
             continue              # check the shipped library exports everything
@@ -226,7 +228,7 @@ def _coder_binding():
             spec.loader.exec_module(mod)
             L = load()
             addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
-            mod.bind(addr(L.ag_rs_coder_shred), addr(L.ag_rs_coder_deshred))
+            mod.bind(addr(L.ag_rs_coder_shred), addr(L.ag_rs_coder_deshred), addr(L.ag_rs_coder_num_coding))
         _pycoder = mod
     return _pycoder or None
 
@@ -369,6 +371,17 @@ def last_decode_classes(ctx: Context) -> dict:
     out = np.zeros(16, np.uint64)
     _check(load().ag_rs_internal_last_decode_classes(ctx.handle, out.ctypes.data), "last_decode_classes")
     return {DECODE_CLASSES.get(i, str(i)): int(v) for i, v in enumerate(out) if v}
+
+
+ENCODE_KERNELS = ("xform4", "xform8", "xform_h8", "encode_mc", "lowrate", "lowrate2", "generic", "restride")
+
+
+def last_encode_kernels(ctx: Context) -> set:
+    """The encode kernels the last ``encode_batch`` on ``ctx`` launched (test aid; the bits of
+    ``ag::EncodeKernelBit``, rs_launch.hpp)."""
+    out = ctypes.c_uint32(0)
+    _check(load().ag_rs_internal_last_encode_kernels(ctx.handle, ctypes.byref(out)), "last_encode_kernels")
+    return {name for i, name in enumerate(ENCODE_KERNELS) if out.value >> i & 1}
 
 
 def fill_splitmix(ctx: Context, device_dst, nblocks: int, block_bytes: int, dst_block_stride: int,

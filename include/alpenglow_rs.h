@@ -187,6 +187,9 @@ void ag_rs_coder_free(ag_rs_coder* coder);
 /* ReedSolomonCoder::new on a private context of `device` (its encoder and decoder share it;
  * destroyed by ag_rs_coder_free): one per ShredderPool entry (pool.rs:33-93). */
 int ag_rs_coder_new_on_device(int device, size_t num_coding, ag_rs_coder** out);
+/* The coder's num_coding (the coding_out capacity ag_rs_coder_shred / _deshred fill is
+ * num_coding * shred bytes): lets bindings size their buffers from the coder itself. */
+int ag_rs_coder_num_coding(const ag_rs_coder* coder, size_t* out);
 
 /* ReedSolomonCoder::shred: pads payload with 0x80 00.. to a multiple of 64 bytes, splits
  * it into 32 shards of *shred_bytes and encodes num_coding coding shards.  data_out must

@@ -131,6 +131,14 @@ def test_pycoder_binding_marshalling(lib):
         pc.deshred(0, [None] * 63 + [b"not a tuple"], 32, 32)
     with pytest.raises(TypeError):
         pc.deshred(0, [None] * 63 + [(True, 12345)], 32, 32)
+    # the coding-output size comes from the coder: a negative or foreign num_coding (or a
+    # handle that is no coder) is refused before anything is allocated or called
+    with pytest.raises(ValueError):
+        pc.shred(0, b"abc", -1)
+    with pytest.raises(ValueError):
+        pc.shred(0, b"abc", 32)
+    with pytest.raises(ValueError):
+        pc.deshred(0, [None] * 64, 32, 32)
     # a RawShreds built from packed bytes splits on access and compares by content
     raw = rs.RawShreds(packed=(bytes(range(8)), bytes(range(8, 12)), 2))
     assert raw.data == [b"\x00\x01", b"\x02\x03", b"\x04\x05", b"\x06\x07"] and raw.coding == [b"\x08\x09", b"\x0a\x0b"]

@@ -101,6 +101,27 @@ def test_fast_encode_many_blocks(ctx, dev, S, n):
     got = gpu_encode(ctx, dev, blocks, 32)
     want = ro_c.encode_blocks(blocks, 32, threads=8)
     assert np.array_equal(got, want)
+    assert rs.last_encode_kernels(ctx) == {"xform8"}  # fewer than 256 tiles: the latency route
+
+
+@pytest.mark.parametrize("S,n,kernel", [
+    (32768, 40, "xform4"),   # the headline shape (1 MiB blocks), 320 tiles
+    (4096, 300, "xform4"),   # one tile per block, 300 tiles
+    (65536, 9, "xform4"),    # 2 MiB blocks, 288 tiles
+    (8192, 130, "xform8"),   # 256 KiB blocks: the measured 8 KiB-shard dispatch, 260 tiles
+    (16384, 66, "xform8"),   # 512 KiB blocks: 16 KiB shards, 264 tiles
+])
+def test_headline_encode_dispatch(ctx, dev, S, n, kernel):
+    """32:32 device-resident encodes of at least 256 tiles (64-column tiles): the headline
+    kernel xform<4> and the 8 / 16 KiB-shard rule that sends those to xform8
+    (launch_xform, rs_kernels.hip) against the C oracle, asserting which kernel ran."""
+    tiles = n * (S // 64) // 64
+    assert tiles >= 256
+    blocks = _blocks(7100 + S, n, 32, S)
+    got = gpu_encode(ctx, dev, blocks, 32)
+    assert rs.last_encode_kernels(ctx) == {kernel}
+    want = ro_c.encode_blocks(blocks, 32, threads=8)
+    assert np.array_equal(got, want)
 
 
 @pytest.mark.parametrize("k,m", [(32, 32), (20, 30), (17, 17), (25, 32)])
@@ -1188,6 +1209,44 @@ def test_window128_decode(ctx, dev, k, m, S, n, per_block, lo, lc):
                 surplus -= 1
     got = gpu_decode(ctx, dev, d_o, d_r, op2, rp2, rs.DECODE_EXACT)
     assert np.array_equal(got, blocks)
+
+
+@pytest.mark.parametrize("k,m", [(64, 64), (32, 64)])
+def test_window128_per_block_mixed_classes(ctx, dev, k, m):
+    """Per-block patterns on whole-tile shards (S = 4096: one pattern per tile) where only some
+    blocks need the W = 128 window and the others decode by another class (nothing lost, the
+    full recovery set, a W = 64 window): the window128 launch covers exactly its blocks' tiles
+    (a zero-tile launch here once left their erased originals unrestored with status OK)."""
+    S, n = 4096, 9
+    rng = random.Random(128 * k + m)
+    blocks = np.stack([np.frombuffer(o.block_bytes(31000 + 7 * k + b, k * S), np.uint8).reshape(k, S)
+                       for b in range(n)])
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    d_o, d_r = blocks.copy(), rec.copy()
+    op, rp = [], []
+    for b in range(n):
+        kind = b % 3
+        if kind == 0:    # W = 128: fewer than k survivors within the first 64 window positions
+            if k == 64:  # HighRate 64:64: any lost coding shred with lost originals
+                lost_o, lost_r = set(rng.sample(range(k), 16)), set(rng.sample(range(m), 8))
+            else:        # LowRate 32:64: originals + first recovery chunk hold 24 < 32 survivors
+                lost_o, lost_r = set(rng.sample(range(k), 24)), set(rng.sample(range(32), 16))
+        elif kind == 1:  # nothing lost, or only originals with the whole recovery set present
+            lost_o = set(rng.sample(range(k), k // 4)) if b % 2 else set()
+            lost_r = set()
+        else:            # a few originals and a few coding shreds: whatever small class fits
+            lost_o = set(rng.sample(range(k), 2))
+            lost_r = set(rng.sample(range(m), 2))
+        op += [0 if i in lost_o else 1 for i in range(k)]
+        rp += [0 if j in lost_r else 1 for j in range(m)]
+        for i in lost_o:
+            d_o[b, i] = 0x6B
+        for j in lost_r:
+            d_r[b, j] = 0xB6
+    got = gpu_decode(ctx, dev, d_o, d_r, op, rp, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
+    classes = rs.last_decode_classes(ctx)
+    assert classes.get("window128", 0) > 0 and len([c for c, v in classes.items() if v and c != "window128"]) > 0, classes
 
 
 @pytest.mark.gpu
