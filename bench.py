@@ -14,7 +14,10 @@ launcher that starts N fresh rank processes before any GPU call and exits non-ze
 rank fails.  Each rank shards its own independent blocks (weak scaling, or --stream-blocks
 for BASELINE configs[4]'s one stream split over the GPUs); there is no data-path collective,
 the only collectives are the timing barrier, the max-over-ranks reduction and the gather of
-per-rank wall times reported in the line.
+per-rank wall times reported in the line.  With --gpus N > 1 (and no --stream-blocks) the
+same run then also times configs[4]'s 65 536 x 1 MiB stream split contiguously over the
+ranks and reports it as the `strong_stream` sub-line (value, per-rank walls and verdicts);
+`value` stays the weak-scaling figure, so the N = 1 line equals configs[1] + configs[2].
 
 Also printed in the JSON line: per-kernel HIP-event timings on the launch stream with the
 HBM roofline, a CPU baseline (the C oracle, a restatement of the reference algorithm, on a
@@ -46,6 +49,10 @@ def parse():
     ap.add_argument("--stream-blocks", type=int, default=0,
                     help="strong scaling: split one stream of this many blocks over the GPUs "
                          "(BASELINE configs[4]: 65536)")
+    ap.add_argument("--strong-stream", type=int, default=-1,
+                    help="after the main measurement, also time one stream of this many blocks split "
+                         "contiguously over the ranks and report it as `strong_stream` (BASELINE "
+                         "configs[4]); default: 65536 when --gpus > 1 without --stream-blocks, else off")
     ap.add_argument("--block-bytes", type=int, default=1 << 20)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--m", type=int, default=32)
@@ -70,7 +77,14 @@ def parse():
                          "steps are empty and the line reports no throughput (tests/test_dist.py)")
     ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--dry-verify-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
-    return ap.parse_args()
+    ap.add_argument("--dry-stream-verify-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    args = ap.parse_args()
+    if args.strong_stream < 0:
+        args.strong_stream = STREAM_BLOCKS if args.gpus > 1 and not args.stream_blocks else 0
+    return args
+
+
+STREAM_BLOCKS = 65536  # BASELINE configs[4]: a 64k-block stream batch-sharded one range per GPU
 
 
 def _free_port() -> int:
@@ -180,6 +194,18 @@ def _dry_main(args, world: int, rank: int, local: int) -> int:
     firsts = gather_over_ranks(plan.first, d)
     # a rank's "verification" here is only the flag the test asks for (--dry-verify-fail-rank)
     ok = None if args.no_verify else rank != args.dry_verify_fail_rank
+    sub = None
+    if args.strong_stream:
+        splan = RankPlan(rank, world, 0, args.strong_stream)
+        if d:
+            d.barrier()
+        t0 = time.perf_counter()
+        if d:
+            d.barrier()
+        swall = time.perf_counter() - t0
+        sok = None if args.no_verify else rank != args.dry_stream_verify_fail_rank
+        sub = _stream_line(args, splan, d, None, swall, sok, value=None, ms_per_step=None)
+        ok = _and_ok(ok, sok)
     line = None
     if rank == 0:
         line = {
@@ -191,6 +217,8 @@ def _dry_main(args, world: int, rank: int, local: int) -> int:
             "config": {"workload": _workload(args, world, plan.nblocks)},
             "verify": None,
         }
+        if sub is not None:
+            line["strong_stream"] = sub
     status = _finish(args, d, None, rank, line, ok)
     if d:
         d.destroy_process_group()
@@ -198,6 +226,38 @@ def _dry_main(args, world: int, rank: int, local: int) -> int:
 
 
 METRIC = "GiB/s device-resident RS shred encode+reconstruct, batched 1 MiB blocks"
+
+
+def _and_ok(a, b):
+    """Combine two verdicts (True / False / None = not verified)."""
+    if a is False or b is False:
+        return False
+    if a is None and b is None:
+        return None
+    return True
+
+
+def _stream_line(args, plan, d, dev, wall, ok, value, ms_per_step):
+    """The `strong_stream` sub-line (BASELINE configs[4]): every rank's timed wall, first
+    block and verdict gathered over the ranks (collectives: all ranks must call this).
+    Returns the dict on rank 0, None elsewhere."""
+    from alpenglow_amd.shard import gather_over_ranks, verify_over_ranks
+
+    walls = gather_over_ranks(wall, d, dev)
+    firsts = gather_over_ranks(plan.first, d, dev)
+    counts = gather_over_ranks(plan.nblocks, d, dev)
+    flags = verify_over_ranks(ok, d, dev)
+    if plan.rank != 0:
+        return None
+    failed = [r for r, f in enumerate(flags) if f is False]
+    return {
+        "value": value, "unit": "GiB/s", "scaling": "strong", "stream_blocks": plan.total,
+        "block_bytes": args.block_bytes, "steps": args.steps, "ms_per_step": ms_per_step,
+        "wall_s": walls, "first_block": [int(f) for f in firsts], "blocks_per_rank": [int(c) for c in counts],
+        "verify": None if all(f is None for f in flags) else {"per_rank": flags, "all_ranks_ok": not failed},
+        "workload": f"{plan.total} x {_size(args.block_bytes)} block stream split contiguously over "
+                    f"{plan.world} GPU(s), {args.k}:{args.m} encode + reconstruct",
+    }
 
 
 def _size(B):
@@ -308,6 +368,7 @@ def main():
     # full-size property check: zero the erased shards, reconstruct, compare with a fresh
     # regeneration of the data; and a 2-block bit-exact spot check of the parity vs oracle
     verify, ok = None, None
+    view = None
     if not args.no_verify:
         # zero every shred the decoder is told is absent (erased data AND lost coding), so a
         # decoder that read an absent shred could not pass
@@ -381,11 +442,95 @@ def main():
         if args.pcie and world == 1:
             line["pcie_inclusive"] = _pcie(args, ctx, cw, k, m, S, e, torch, dev)
             ok = ok is not False and line["pcie_inclusive"]["matches_device_result"]
+    if args.strong_stream:
+        # BASELINE configs[4]: the weak workload's buffers go first (the stream's codewords
+        # are strong_stream / world x (k + m) x S bytes per rank: 128 GiB at N = 1)
+        del cw, view
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+        sub, sok = _strong_stream(args, ctx, dist, dev, torch, stream, rank, world, k, m, S, e, lc)
+        ok = _and_ok(ok, sok)
+        if rank == 0:
+            line["strong_stream"] = sub
     status = _finish(args, dist, dev, rank, line, ok)
     ctx.close()
     if dist:
         dist.destroy_process_group()
     sys.exit(status)
+
+
+def _strong_stream(args, ctx, dist, dev, torch, stream, rank, world, k, m, S, e, lc):
+    """BASELINE configs[4]: one stream of args.strong_stream blocks split into contiguous
+    per-rank ranges (RankPlan strong), each rank encoding + reconstructing its range with no
+    data-path collective; the same step, warmup / settle, barrier-bracketed K steps and
+    max-over-ranks wall as the main measurement.  Verified afterwards on every rank (erased
+    and lost shards zeroed, reconstructed, compared with a fresh regeneration group by
+    group).  Returns (sub-line on rank 0 else None, this rank's verdict)."""
+    from alpenglow_amd import rs
+    from alpenglow_amd.shard import RankPlan, erasure_patterns, max_over_ranks
+
+    plan = RankPlan(rank, world, 0, args.strong_stream)
+    n, B, cw_stride = plan.nblocks, k * S, (k + m) * S
+    cw = torch.empty((n, cw_stride), dtype=torch.uint8, device=dev)
+    rs.fill_splitmix(ctx, cw, n, B, cw_stride, plan.seed_base)
+    data_ptr, par_ptr = cw.data_ptr(), cw.data_ptr() + B
+    opres, rpres = erasure_patterns(plan, k, m, e, lc, args.random_patterns)
+    opres_b, rpres_b = bytes(opres), bytes(rpres)
+    do_enc, do_dec = args.only in ("both", "encode"), args.only in ("both", "decode")
+
+    def encode():
+        rs.encode_batch(ctx, k, m, S, n, data_ptr, cw_stride, par_ptr, cw_stride)
+
+    def reconstruct():
+        rs.decode_batch(ctx, k, m, S, n, data_ptr, cw_stride, par_ptr, cw_stride, opres_b, rpres_b,
+                        mode=rs.DECODE_ANY_K)
+
+    def step():
+        if do_enc:
+            encode()
+        if do_dec:
+            reconstruct()
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    encode()
+    for _ in range(args.warmup):
+        step()
+    if not args.no_settle:
+        _settle(step, stream, torch, max_steps=50)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    wall = time.perf_counter() - t0
+    wall_max = max_over_ranks(wall, dist, dev)
+    ok = None
+    if not args.no_verify:
+        view = cw.view(n, k + m, S)
+        lost = torch.tensor(opres, dtype=torch.uint8).view(-1, k)[: n if args.random_patterns else 1] == 0
+        lost_r = torch.tensor(rpres, dtype=torch.uint8).view(-1, m)[: n if args.random_patterns else 1] == 0
+        view[:, :k][lost.to(dev).expand(n, k)] = 0
+        view[:, k:][lost_r.to(dev).expand(n, m)] = 0
+        reconstruct()
+        group = max(1, min(n, (4 << 30) // B))
+        ref = torch.empty((group, B), dtype=torch.uint8, device=dev)
+        ok = True
+        for g0 in range(0, n, group):
+            g = min(group, n - g0)
+            rs.fill_splitmix(ctx, ref, g, B, B, plan.seed_base + g0)
+            ok = ok and bool(torch.equal(cw[g0:g0 + g, :B], ref[:g]))
+        del ref, view
+    del cw
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    value = plan.processed_bytes(args.block_bytes, args.steps) / wall_max / GIB
+    sub = _stream_line(args, plan, dist, dev, wall, ok, value, wall_max * 1e3 / args.steps)
+    return sub, ok
 
 
 def _settle(step, stream, torch, max_steps=200, min_steps=3, tol=0.01, window=4):

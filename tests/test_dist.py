@@ -163,6 +163,41 @@ def test_bench_launcher_world2(extra, firsts):
     assert len(line["ranks"]["wall_s"]) == 2 and line["ranks"]["first_block"] == firsts
     assert line["scaling"] == ("strong" if extra else "weak")
     assert line["verify"]["per_rank"] == [True, True] and line["verify"]["all_ranks_ok"] is True
+    if extra:  # the main measurement already is the stream: no second one
+        assert "strong_stream" not in line
+    else:      # BASELINE configs[4] from the driver's own command: the 65536-block stream
+        sub = line["strong_stream"]
+        assert sub["scaling"] == "strong" and sub["stream_blocks"] == 65536
+        assert sub["first_block"] == [0, 32768] and sub["blocks_per_rank"] == [32768, 32768]
+        assert len(sub["wall_s"]) == 2
+        assert sub["verify"] == {"per_rank": [True, True], "all_ranks_ok": True}
+
+
+@pytest.mark.parametrize("bad", [0, 1])
+def test_bench_strong_stream_verify_fails_job(bad):
+    """A rank whose stream range fails verification makes the job exit 4, with the weak
+    measurement's verdicts intact and the stream's per-rank flags naming the rank."""
+    r = _bench("--gpus", "2", "--dry-device", "--steps", "1", "--dry-stream-verify-fail-rank", str(bad))
+    assert r.returncode == 4, (r.returncode, r.stderr)
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    assert line["strong_stream"]["verify"]["per_rank"] == [i != bad for i in range(2)]
+    assert line["strong_stream"]["verify"]["all_ranks_ok"] is False
+    assert line["verify"]["per_rank"] == [i != bad for i in range(2)]  # the job verdict folds it in
+
+
+def test_bench_strong_stream_flags():
+    """--strong-stream 0 turns the sub-line off; at one rank it is off by default and on
+    when asked (the driver's N = 1 line stays configs[1] + configs[2])."""
+    r = _bench("--gpus", "2", "--dry-device", "--steps", "1", "--strong-stream", "0")
+    assert r.returncode == 0, r.stderr
+    assert "strong_stream" not in json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    r = _bench("--gpus", "1", "--dry-device", "--steps", "1")
+    assert r.returncode == 0, r.stderr
+    assert "strong_stream" not in json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    r = _bench("--gpus", "1", "--dry-device", "--steps", "1", "--strong-stream", "1000")
+    assert r.returncode == 0, r.stderr
+    sub = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])["strong_stream"]
+    assert sub["first_block"] == [0] and sub["blocks_per_rank"] == [1000]
 
 
 @pytest.mark.parametrize("bad", [0, 1])
