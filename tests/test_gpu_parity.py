@@ -107,7 +107,7 @@ def test_fast_encode_many_blocks(ctx, dev, S, n):
 @pytest.mark.parametrize("S,n,kernel", [
     (32768, 40, "xform4"),   # the headline shape (1 MiB blocks), 320 tiles
     (4096, 300, "xform4"),   # one tile per block, 300 tiles
-    (65536, 9, "xform4"),    # 2 MiB blocks, 288 tiles
+    (65536, 18, "xform4"),   # 2 MiB shards (64 MiB blocks), 288 tiles
     (8192, 130, "xform8"),   # 256 KiB blocks: the measured 8 KiB-shard dispatch, 260 tiles
     (16384, 66, "xform8"),   # 512 KiB blocks: 16 KiB shards, 264 tiles
 ])
@@ -1229,8 +1229,10 @@ def test_window128_per_block_mixed_classes(ctx, dev, k, m):
         if kind == 0:    # W = 128: fewer than k survivors within the first 64 window positions
             if k == 64:  # HighRate 64:64: any lost coding shred with lost originals
                 lost_o, lost_r = set(rng.sample(range(k), 16)), set(rng.sample(range(m), 8))
-            else:        # LowRate 32:64: originals + first recovery chunk hold 24 < 32 survivors
-                lost_o, lost_r = set(rng.sample(range(k), 24)), set(rng.sample(range(32), 16))
+            else:        # LowRate 32:64: originals + first recovery chunk hold 24 < 32 survivors,
+                         # and the second chunk is incomplete (no single-chunk decode)
+                lost_o = set(rng.sample(range(k), 24))
+                lost_r = set(rng.sample(range(32), 16)) | set(rng.sample(range(32, 64), 2))
         elif kind == 1:  # nothing lost, or only originals with the whole recovery set present
             lost_o = set(rng.sample(range(k), k // 4)) if b % 2 else set()
             lost_r = set()
