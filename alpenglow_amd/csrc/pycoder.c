@@ -1,5 +1,6 @@
 /* CPython binding of the per-call coder entry points (ag_rs_coder_shred / _deshred) for
- * alpenglow_amd.rs.ReedSolomonCoder: the argument marshalling of the ctypes path (64 shred
+ * alpenglow_amd.rs.ReedSolomonCoder, and of the crate-API encoder / decoder calls for
+ * ReedSolomonEncoder / ReedSolomonDecoder: the argument marshalling of the ctypes path (64 shred
  * pointers, lengths and data flags built as ctypes arrays, three zero-filled result buffers,
  * 64 slices) cost more than the device round trip it wraps (tools/bench_latency.py).  Here one
  * C loop reads the shred list, the results are written straight into bytes objects of their
@@ -18,21 +19,139 @@
 typedef __typeof__(ag_rs_coder_shred)* shred_fn;
 typedef __typeof__(ag_rs_coder_deshred)* deshred_fn;
 typedef __typeof__(ag_rs_coder_num_coding)* num_coding_fn;
+typedef __typeof__(ag_rs_encoder_add_original_shard)* enc_add_fn;
+typedef __typeof__(ag_rs_encoder_encode)* enc_encode_fn;
+typedef __typeof__(ag_rs_encoder_recovery)* enc_recovery_fn;
+typedef __typeof__(ag_rs_decoder_add_original_shard)* dec_add_fn;
+typedef __typeof__(ag_rs_decoder_decode)* dec_decode_fn;
+typedef __typeof__(ag_rs_decoder_restored_original)* dec_restored_fn;
 
 static shred_fn g_shred;
 static deshred_fn g_deshred;
 static num_coding_fn g_num_coding;
+static enc_add_fn g_enc_add;
+static enc_encode_fn g_enc_encode;
+static enc_recovery_fn g_enc_recovery;
+static dec_add_fn g_dec_add_o, g_dec_add_r;
+static dec_decode_fn g_dec_decode;
+static dec_restored_fn g_dec_restored;
 
 enum { kTotal = AG_RS_TOTAL_SHREDS, kData = AG_RS_DATA_SHREDS };
 
+/* bind(shred, deshred, num_coding, encoder add / encode / recovery, decoder add original /
+ * add recovery / decode / restored_original): the library's entry points by address */
 static PyObject* bind(PyObject* self, PyObject* args) {
-  unsigned long long a, b, n;
+  unsigned long long a[10];
   (void)self;
-  if (!PyArg_ParseTuple(args, "KKK", &a, &b, &n)) return NULL;
-  g_shred = (shred_fn)(uintptr_t)a;
-  g_deshred = (deshred_fn)(uintptr_t)b;
-  g_num_coding = (num_coding_fn)(uintptr_t)n;
+  if (!PyArg_ParseTuple(args, "KKKKKKKKKK", &a[0], &a[1], &a[2], &a[3], &a[4], &a[5], &a[6], &a[7], &a[8], &a[9]))
+    return NULL;
+  g_shred = (shred_fn)(uintptr_t)a[0];
+  g_deshred = (deshred_fn)(uintptr_t)a[1];
+  g_num_coding = (num_coding_fn)(uintptr_t)a[2];
+  g_enc_add = (enc_add_fn)(uintptr_t)a[3];
+  g_enc_encode = (enc_encode_fn)(uintptr_t)a[4];
+  g_enc_recovery = (enc_recovery_fn)(uintptr_t)a[5];
+  g_dec_add_o = (dec_add_fn)(uintptr_t)a[6];
+  g_dec_add_r = (dec_add_fn)(uintptr_t)a[7];
+  g_dec_decode = (dec_decode_fn)(uintptr_t)a[8];
+  g_dec_restored = (dec_restored_fn)(uintptr_t)a[9];
   Py_RETURN_NONE;
+}
+
+/* ReedSolomonEncoder / ReedSolomonDecoder (INTEGRATION.md Route A) without ctypes marshalling:
+ * each crate call is one C call here, and the results come back as bytes objects in one loop.
+ * Every function returns the library status (0 = OK) or raises on malformed arguments. */
+static PyObject* enc_add(PyObject* self, PyObject* args) {
+  unsigned long long h;
+  Py_buffer b;
+  (void)self;
+  if (!g_enc_add) return PyErr_Format(PyExc_RuntimeError, "pycoder: bind() not called");
+  if (!PyArg_ParseTuple(args, "Ky*", &h, &b)) return NULL;
+  const int st = g_enc_add((ag_rs_encoder*)(uintptr_t)h, (const uint8_t*)b.buf, (size_t)b.len);
+  PyBuffer_Release(&b);
+  return PyLong_FromLong(st);
+}
+
+/* enc_encode(encoder, recovery_count) -> (status, [recovery shards]) */
+static PyObject* enc_encode(PyObject* self, PyObject* args) {
+  unsigned long long h;
+  Py_ssize_t m, j;
+  int st;
+  (void)self;
+  if (!g_enc_encode) return PyErr_Format(PyExc_RuntimeError, "pycoder: bind() not called");
+  if (!PyArg_ParseTuple(args, "Kn", &h, &m)) return NULL;
+  if (m < 0) return PyErr_Format(PyExc_ValueError, "recovery_count %zd < 0", m);
+  ag_rs_encoder* e = (ag_rs_encoder*)(uintptr_t)h;
+  Py_BEGIN_ALLOW_THREADS
+  st = g_enc_encode(e);
+  Py_END_ALLOW_THREADS
+  PyObject* out = PyList_New(0);
+  if (!out) return NULL;
+  for (j = 0; st == 0 && j < m; ++j) {
+    const uint8_t* p = NULL;
+    size_t len = 0;
+    if ((st = g_enc_recovery(e, (size_t)j, &p, &len)) != 0) break;
+    PyObject* b = PyBytes_FromStringAndSize((const char*)p, (Py_ssize_t)len);
+    if (!b || PyList_Append(out, b) < 0) {
+      Py_XDECREF(b);
+      Py_DECREF(out);
+      return NULL;
+    }
+    Py_DECREF(b);
+  }
+  return Py_BuildValue("(iN)", st, out);
+}
+
+/* dec_add(decoder, is_original, index, shard) -> status */
+static PyObject* dec_add(PyObject* self, PyObject* args) {
+  unsigned long long h;
+  int orig;
+  Py_ssize_t idx;
+  Py_buffer b;
+  (void)self;
+  if (!g_dec_add_o) return PyErr_Format(PyExc_RuntimeError, "pycoder: bind() not called");
+  if (!PyArg_ParseTuple(args, "Kpny*", &h, &orig, &idx, &b)) return NULL;
+  if (idx < 0) {
+    PyBuffer_Release(&b);
+    return PyErr_Format(PyExc_ValueError, "index %zd < 0", idx);
+  }
+  const int st = (orig ? g_dec_add_o : g_dec_add_r)((ag_rs_decoder*)(uintptr_t)h, (size_t)idx,
+                                                    (const uint8_t*)b.buf, (size_t)b.len);
+  PyBuffer_Release(&b);
+  return PyLong_FromLong(st);
+}
+
+/* dec_decode(decoder, original_count) -> (status, {index: restored original}) */
+static PyObject* dec_decode(PyObject* self, PyObject* args) {
+  unsigned long long h;
+  Py_ssize_t k, i;
+  int st;
+  (void)self;
+  if (!g_dec_decode) return PyErr_Format(PyExc_RuntimeError, "pycoder: bind() not called");
+  if (!PyArg_ParseTuple(args, "Kn", &h, &k)) return NULL;
+  if (k < 0) return PyErr_Format(PyExc_ValueError, "original_count %zd < 0", k);
+  ag_rs_decoder* d = (ag_rs_decoder*)(uintptr_t)h;
+  Py_BEGIN_ALLOW_THREADS
+  st = g_dec_decode(d);
+  Py_END_ALLOW_THREADS
+  PyObject* out = PyDict_New();
+  if (!out) return NULL;
+  for (i = 0; st == 0 && i < k; ++i) {
+    const uint8_t* p = NULL;
+    size_t len = 0;
+    if (g_dec_restored(d, (size_t)i, &p, &len) != 0) continue;  /* not restored (crate: None) */
+    PyObject* key = PyLong_FromSsize_t(i);
+    PyObject* b = PyBytes_FromStringAndSize((const char*)p, (Py_ssize_t)len);
+    if (!key || !b || PyDict_SetItem(out, key, b) < 0) {
+      Py_XDECREF(key);
+      Py_XDECREF(b);
+      Py_DECREF(out);
+      return NULL;
+    }
+    Py_DECREF(key);
+    Py_DECREF(b);
+  }
+  return Py_BuildValue("(iN)", st, out);
 }
 
 /* The library writes num_coding * S coding bytes whatever the caller says: the caller's count
@@ -176,7 +295,12 @@ done:
 }
 
 static PyMethodDef methods[] = {
-    {"bind", bind, METH_VARARGS, "bind(shred_addr, deshred_addr, num_coding_addr)"},
+    {"bind", bind, METH_VARARGS, "bind(shred, deshred, num_coding, enc_add, enc_encode, enc_recovery, dec_add_o, "
+                                 "dec_add_r, dec_decode, dec_restored)"},
+    {"enc_add", enc_add, METH_VARARGS, "enc_add(encoder, shard) -> status"},
+    {"enc_encode", enc_encode, METH_VARARGS, "enc_encode(encoder, recovery_count) -> (status, [recovery])"},
+    {"dec_add", dec_add, METH_VARARGS, "dec_add(decoder, is_original, index, shard) -> status"},
+    {"dec_decode", dec_decode, METH_VARARGS, "dec_decode(decoder, original_count) -> (status, {i: restored})"},
     {"shred", shred, METH_VARARGS, "shred(coder, payload, num_coding) -> (status, data, coding, S)"},
     {"deshred", deshred, METH_VARARGS, "deshred(coder, shreds, data_shreds, num_coding) -> (status, payload, data, coding, S)"},
     {NULL, NULL, 0, NULL}};

@@ -184,7 +184,6 @@ struct ag_rs_ctx {
   } slot[2];
   hipStream_t h2d = nullptr, d2h = nullptr;
   DevBuf one_in, one_out;                 // crate-API single codeword
-  PinBuf one_pin;                         // its pinned host staging
   // per-call server (latency_server_kernel): mailbox in mapped host memory, its own stream
   ag::LatencyMailbox* mb = nullptr;
   ag::LatencyMailbox* mb_dev = nullptr;
@@ -300,7 +299,6 @@ struct ag_rs_ctx {
                       &one_out, &d_pipe_few, &d_pipe_mask, &d_present})
       b->release();
     for (DevBuf& b : pipe) b.release();
-    one_pin.release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -1519,25 +1517,39 @@ int ag_aon_decrypt_batch(ag_rs_ctx* c, int scheme, size_t n, uint8_t* buffers, s
 // An object made by *_new_on_device owns its context (`owned`: created with it, destroyed by
 // its _free), so objects made that way share no state and may run on different threads at
 // once; *_new borrows the caller's context, shared with whatever else uses it.
+// Each encoder / decoder stages its codeword in its own mapped pinned buffer (the shards are
+// copied there by add_*_shard, the device reads and writes it in place, and the result
+// accessors point into it), so no call re-copies or re-zeroes a 64 KiB slice.
 struct ag_rs_encoder {
   ag_rs_ctx* ctx = nullptr;
   ag_rs_ctx* owned = nullptr;
   size_t k = 0, m = 0, S = 0;
   size_t received = 0;
   bool encoded = false;
-  std::vector<uint8_t> orig, rec;
-  ~ag_rs_encoder() { ag_rs_ctx_destroy(owned); }
+  PinBuf pin;  // originals [k * S] then recovery shards [m * S]
+  uint8_t* orig() const { return pin.as<uint8_t>(); }
+  uint8_t* rec() const { return pin.as<uint8_t>() + k * S; }
+  ~ag_rs_encoder() {
+    pin.release();
+    ag_rs_ctx_destroy(owned);
+  }
 };
 
 struct ag_rs_decoder {
   ag_rs_ctx* ctx = nullptr;
   ag_rs_ctx* owned = nullptr;
   size_t k = 0, m = 0, S = 0;
-  std::vector<uint8_t> orig, rec, opres, rpres;
+  std::vector<uint8_t> opres, rpres;
   size_t no = 0, nr = 0;
   bool decoded = false;
   std::vector<uint8_t> restored;  // 1 where original i was restored by the last decode
-  ~ag_rs_decoder() { ag_rs_ctx_destroy(owned); }
+  PinBuf pin;  // originals [k * S], recovery shards [m * S], re-encoded coding shards [m * S]
+  uint8_t* orig() const { return pin.as<uint8_t>(); }
+  uint8_t* rec() const { return pin.as<uint8_t>() + k * S; }
+  ~ag_rs_decoder() {
+    pin.release();
+    ag_rs_ctx_destroy(owned);
+  }
 };
 
 namespace {
@@ -1577,7 +1589,8 @@ ag::XformParams one_tile(const uint8_t* in, size_t in_stride, uint8_t* out, size
   p.total_columns = S / 64;
   return p;
 }
-int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t mask) {
+// `stage`: the pinned buffer the job reads and writes (abandoned on a timeout).
+int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t mask, PinBuf& stage) {
   if (!c->mb) {
     void* h = nullptr;
     AG_HIP(hipHostMalloc(&h, sizeof(ag::LatencyMailbox), hipHostMallocMapped | hipHostMallocCoherent));
@@ -1617,40 +1630,36 @@ int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t m
       c->server_broken = true;
       mb->kind = ag::kJobQuit;
       __atomic_store_n(&mb->doorbell, ++c->server_seq, __ATOMIC_RELEASE);
-      c->abandoned_pins.push_back(c->one_pin);
-      c->one_pin = PinBuf{};
+      c->abandoned_pins.push_back(stage);
+      stage = PinBuf{};
       return AG_RS_ERR_DEVICE;
     }
     __builtin_ia32_pause();
   }
 }
 
-int run_one_encode(ag_rs_ctx* c, size_t k, size_t m, size_t S, const uint8_t* orig, uint8_t* rec) {
+// One codeword staged in `pin` (originals at 0, recovery shards at k * S): the recovery shards
+// are computed in place.
+int run_one_encode(ag_rs_ctx* c, size_t k, size_t m, size_t S, PinBuf& pin) {
   int st;
   if ((st = c->enter())) return st;
   const size_t ob = k * S, rb = m * S;
-  if ((st = c->one_pin.ensure(ob + rb))) return st;
-  uint8_t* pin = c->one_pin.as<uint8_t>();
-  uint8_t* pd = c->one_pin.dev<uint8_t>();
-  std::memcpy(pin, orig, ob);
-  if (server_fits(c, k, m, S)) {
-    if ((st = server_job(c, ag::kJobEncode32, one_tile(pd, ob, pd + ob, rb, S), 0))) return st;
-  } else {
-    if ((st = encode_device(c, k, m, S, 1, pd, ob, pd + ob, rb))) return st;
-    if ((st = spin_sync(c))) return st;
-  }
-  std::memcpy(rec, pin + ob, rb);
-  return AG_RS_OK;
+  uint8_t* pd = pin.dev<uint8_t>();
+  if (server_fits(c, k, m, S)) return server_job(c, ag::kJobEncode32, one_tile(pd, ob, pd + ob, rb, S), 0, pin);
+  if ((st = encode_device(c, k, m, S, 1, pd, ob, pd + ob, rb))) return st;
+  return spin_sync(c);
 }
 
 // One codeword decoded on the device, zero-copy like run_one_encode: originals and recovery
-// shards in mapped pinned memory, decode in place (restored originals land in the original
-// region), and with `coding` the re-encode of every recovery shard from the completed
-// originals (ReedSolomonCoder::deshred's encode_coding_from_data, reed_solomon.rs:206).
-// EXACT runs as ANY_K when exactly k shards are present: k shards fix the codeword, so both
-// decoders return its originals for any input bytes.
-int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, uint8_t* orig, const uint8_t* rec,
-                   const uint8_t* opres, const uint8_t* rpres, int mode, uint8_t* coding) {
+// shards staged in `pin` (originals at 0, recovery at k * S), restored originals written in
+// place, and with `coding` the re-encode of every recovery shard from the completed originals
+// (ReedSolomonCoder::deshred's encode_coding_from_data, reed_solomon.rs:206) at (k + m) * S
+// -- or, when the received shards are exactly the m recovery shards, *coding_src points at
+// those (the re-encode reproduces them bit for bit).  EXACT runs as ANY_K when exactly k
+// shards are present: k shards fix the codeword, so both decoders return its originals for
+// any input bytes.
+int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, PinBuf& pin, const uint8_t* opres,
+                   const uint8_t* rpres, int mode, bool coding, const uint8_t** coding_src) {
   int st;
   if ((st = c->enter())) return st;
   const size_t ob = k * S, rb = m * S;
@@ -1659,16 +1668,13 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, uint8_t* orig, co
   for (size_t i = 0; i < m; ++i) present += rpres[i] != 0;
   if (present < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
   if (present == k) mode = AG_RS_DECODE_ANY_K;
-  if ((st = c->one_pin.ensure(ob + 2 * rb))) return st;
-  uint8_t* pin = c->one_pin.as<uint8_t>();
-  uint8_t* pd = c->one_pin.dev<uint8_t>();
-  std::memcpy(pin, orig, ob);
-  std::memcpy(pin + ob, rec, rb);
+  uint8_t* pd = pin.dev<uint8_t>();
   // exactly k shards, all of them recovery shards: the completed codeword passes through
   // them, so its re-encoded recovery shards are the received ones (bit for bit)
   size_t nr = 0;
   for (size_t i = 0; i < m; ++i) nr += rpres[i] != 0;
   const bool reuse = coding && present == k && nr == m;
+  if (coding_src) *coding_src = pin.as<uint8_t>() + (reuse ? ob : ob + rb);
   if (nr == m && (present == k || mode == AG_RS_DECODE_ANY_K) && server_fits(c, k, m, S)) {
     // the whole recovery set: the erased originals are one transform of it (the decode class
     // "none" route of decode_cols), run by the per-call server
@@ -1678,18 +1684,16 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, uint8_t* orig, co
     std::fill(std::begin(c->last_classes), std::end(c->last_classes), uint64_t{0});
     ++c->last_classes[mask ? 1 : 0];  // "transform" (or "none")
     if (mask && (st = server_job(c, (mask >> 16) ? ag::kJobDecode32 : ag::kJobDecode32Half,
-                                 one_tile(pd + ob, rb, pd, ob, S), mask)))
+                                 one_tile(pd + ob, rb, pd, ob, S), mask, pin)))
       return st;
-    if (coding && !reuse && (st = server_job(c, ag::kJobEncode32, one_tile(pd, ob, pd + ob + rb, rb, S), 0)))
+    if (coding && !reuse &&
+        (st = server_job(c, ag::kJobEncode32, one_tile(pd, ob, pd + ob + rb, rb, S), 0, pin)))
       return st;
-  } else {
-    if ((st = decode_device(c, k, m, S, 1, pd, ob, pd + ob, rb, opres, rpres, 1, mode))) return st;
-    if (coding && !reuse && (st = encode_device(c, k, m, S, 1, pd, ob, pd + ob + rb, rb))) return st;
-    if ((st = spin_sync(c))) return st;
+    return AG_RS_OK;
   }
-  std::memcpy(orig, pin, ob);
-  if (coding) std::memcpy(coding, reuse ? rec : pin + ob + rb, rb);
-  return AG_RS_OK;
+  if ((st = decode_device(c, k, m, S, 1, pd, ob, pd + ob, rb, opres, rpres, 1, mode))) return st;
+  if (coding && !reuse && (st = encode_device(c, k, m, S, 1, pd, ob, pd + ob + rb, rb))) return st;
+  return spin_sync(c);
 }
 }  // namespace
 
@@ -1697,15 +1701,15 @@ extern "C" {
 
 int ag_rs_encoder_reset(ag_rs_encoder* e, size_t k, size_t m, size_t S) {
   if (!e) return AG_RS_ERR_INVALID_ARGUMENT;
-  const int st = check_geometry(k, m, S);
+  int st = check_geometry(k, m, S);
   if (st) return st;
+  // the staging only grows; its bytes need no clearing (encode reads the k added originals)
+  if ((k + m) * S > e->pin.size && ((st = e->ctx->enter()) || (st = e->pin.ensure((k + m) * S)))) return st;
   e->k = k;
   e->m = m;
   e->S = S;
   e->received = 0;
   e->encoded = false;
-  e->orig.assign(k * S, 0);
-  e->rec.assign(m * S, 0);
   return AG_RS_OK;
 }
 
@@ -1746,7 +1750,7 @@ int ag_rs_encoder_add_original_shard(ag_rs_encoder* e, const uint8_t* shard, siz
   }
   if (e->received == e->k) return AG_RS_ERR_TOO_MANY_ORIGINAL_SHARDS;
   if (len != e->S) return AG_RS_ERR_DIFFERENT_SHARD_SIZE;
-  std::memcpy(e->orig.data() + e->received * e->S, shard, len);
+  std::memcpy(e->orig() + e->received * e->S, shard, len);
   ++e->received;
   return AG_RS_OK;
 }
@@ -1754,7 +1758,7 @@ int ag_rs_encoder_add_original_shard(ag_rs_encoder* e, const uint8_t* shard, siz
 int ag_rs_encoder_encode(ag_rs_encoder* e) {
   if (!e) return AG_RS_ERR_INVALID_ARGUMENT;
   if (e->received != e->k) return AG_RS_ERR_TOO_FEW_ORIGINAL_SHARDS;
-  const int st = run_one_encode(e->ctx, e->k, e->m, e->S, e->orig.data(), e->rec.data());
+  const int st = run_one_encode(e->ctx, e->k, e->m, e->S, e->pin);
   if (st) return st;
   e->encoded = true;
   return AG_RS_OK;
@@ -1763,7 +1767,7 @@ int ag_rs_encoder_encode(ag_rs_encoder* e) {
 int ag_rs_encoder_recovery(const ag_rs_encoder* e, size_t index, const uint8_t** shard, size_t* len) {
   if (!e || !shard || !len) return AG_RS_ERR_INVALID_ARGUMENT;
   if (!e->encoded || index >= e->m) return AG_RS_ERR_INVALID_ARGUMENT;
-  *shard = e->rec.data() + index * e->S;
+  *shard = e->rec() + index * e->S;
   *len = e->S;
   return AG_RS_OK;
 }
@@ -1772,13 +1776,13 @@ void ag_rs_encoder_free(ag_rs_encoder* e) { delete e; }
 
 int ag_rs_decoder_reset(ag_rs_decoder* d, size_t k, size_t m, size_t S) {
   if (!d) return AG_RS_ERR_INVALID_ARGUMENT;
-  const int st = check_geometry(k, m, S);
+  int st = check_geometry(k, m, S);
   if (st) return st;
+  if ((k + 2 * m) * S > d->pin.size && ((st = d->ctx->enter()) || (st = d->pin.ensure((k + 2 * m) * S))))
+    return st;
   d->k = k;
   d->m = m;
   d->S = S;
-  d->orig.assign(k * S, 0);
-  d->rec.assign(m * S, 0);
   d->opres.assign(k, 0);
   d->rpres.assign(m, 0);
   d->restored.assign(k, 0);
@@ -1831,7 +1835,7 @@ int ag_rs_decoder_add_original_shard(ag_rs_decoder* d, size_t index, const uint8
   if (index >= d->k) return AG_RS_ERR_INVALID_ORIGINAL_SHARD_INDEX;
   if (d->opres[index]) return AG_RS_ERR_DUPLICATE_ORIGINAL_SHARD_INDEX;
   if (len != d->S) return AG_RS_ERR_DIFFERENT_SHARD_SIZE;
-  std::memcpy(d->orig.data() + index * d->S, shard, len);
+  std::memcpy(d->orig() + index * d->S, shard, len);
   d->opres[index] = 1;
   ++d->no;
   return AG_RS_OK;
@@ -1843,7 +1847,7 @@ int ag_rs_decoder_add_recovery_shard(ag_rs_decoder* d, size_t index, const uint8
   if (index >= d->m) return AG_RS_ERR_INVALID_RECOVERY_SHARD_INDEX;
   if (d->rpres[index]) return AG_RS_ERR_DUPLICATE_RECOVERY_SHARD_INDEX;
   if (len != d->S) return AG_RS_ERR_DIFFERENT_SHARD_SIZE;
-  std::memcpy(d->rec.data() + index * d->S, shard, len);
+  std::memcpy(d->rec() + index * d->S, shard, len);
   d->rpres[index] = 1;
   ++d->nr;
   return AG_RS_OK;
@@ -1855,8 +1859,8 @@ int ag_rs_decoder_decode(ag_rs_decoder* d) {
   std::fill(d->restored.begin(), d->restored.end(), 0);
   if (d->no < d->k) {
     // exact crate semantics: decode from every present shard
-    const int st = run_one_decode(d->ctx, d->k, d->m, d->S, d->orig.data(), d->rec.data(), d->opres.data(),
-                                  d->rpres.data(), AG_RS_DECODE_EXACT, nullptr);
+    const int st = run_one_decode(d->ctx, d->k, d->m, d->S, d->pin, d->opres.data(), d->rpres.data(),
+                                  AG_RS_DECODE_EXACT, false, nullptr);
     if (st) return st;
     for (size_t i = 0; i < d->k; ++i) d->restored[i] = d->opres[i] ? 0 : 1;
   }
@@ -1867,7 +1871,7 @@ int ag_rs_decoder_decode(ag_rs_decoder* d) {
 int ag_rs_decoder_restored_original(const ag_rs_decoder* d, size_t index, const uint8_t** shard, size_t* len) {
   if (!d || !shard || !len) return AG_RS_ERR_INVALID_ARGUMENT;
   if (!d->decoded || index >= d->k || !d->restored[index]) return AG_RS_ERR_NOT_RESTORED;
-  *shard = d->orig.data() + index * d->S;
+  *shard = d->orig() + index * d->S;
   *len = d->S;
   return AG_RS_OK;
 }
@@ -1898,15 +1902,13 @@ constexpr size_t kTotalShreds = AG_RS_TOTAL_SHREDS;
 constexpr size_t kMaxAfterPadding = kDataShreds * AG_RS_MAX_DATA_PER_SHRED;
 constexpr size_t kMaxPayload = kMaxAfterPadding - 1;
 
-// encode_coding_from_data (reed_solomon.rs:211-231)
-int coder_encode(ag_rs_coder* c, const uint8_t* data, size_t S, uint8_t* coding) {
-  int st = ag_rs_encoder_reset(c->enc, kDataShreds, c->num_coding, S);
-  if (st) return st;
-  for (size_t i = 0; i < kDataShreds; ++i)
-    if ((st = ag_rs_encoder_add_original_shard(c->enc, data + i * S, S))) return st;
-  if ((st = ag_rs_encoder_encode(c->enc))) return st;
-  std::memcpy(coding, c->enc->rec.data(), c->num_coding * S);
-  return AG_RS_OK;
+// encode_coding_from_data (reed_solomon.rs:211-231) of the 32 data shards already staged in
+// the encoder's originals (S bytes each): the coding shards land in c->enc->rec()
+// (the caller reset the encoder to (32, num_coding, S) before staging them)
+int coder_encode_staged(ag_rs_coder* c) {
+  c->enc->received = kDataShreds;
+  c->enc->encoded = false;
+  return ag_rs_encoder_encode(c->enc);
 }
 }  // namespace
 
@@ -1959,14 +1961,16 @@ int ag_rs_coder_shred(ag_rs_coder* c, const uint8_t* payload, size_t len, uint8_
   // padding 0x80 00.. to a multiple of 2 * DATA_SHREDS (reed_solomon.rs:94-106)
   const size_t padding = 2 * kDataShreds - len % (2 * kDataShreds);
   const size_t S = (len + padding) / kDataShreds;
-  std::vector<uint8_t> padded(len + padding, 0);
-  if (len) std::memcpy(padded.data(), payload, len);
-  padded[len] = 0x80;
-  std::vector<uint8_t> coding(c->num_coding * S);
-  const int st = coder_encode(c, padded.data(), S, coding.data());
+  // padded payload straight into the encoder's pinned originals
+  int st = ag_rs_encoder_reset(c->enc, kDataShreds, c->num_coding, S);
   if (st) return st;
-  std::memcpy(data_out, padded.data(), padded.size());
-  std::memcpy(coding_out, coding.data(), coding.size());
+  uint8_t* padded = c->enc->orig();
+  if (len) std::memcpy(padded, payload, len);
+  padded[len] = 0x80;
+  std::memset(padded + len + 1, 0, padding - 1);
+  if ((st = coder_encode_staged(c))) return st;
+  std::memcpy(data_out, padded, len + padding);
+  std::memcpy(coding_out, c->enc->rec(), c->num_coding * S);
   *shred_bytes = S;
   return AG_RS_OK;
 }
@@ -2003,15 +2007,15 @@ int ag_rs_coder_deshred(ag_rs_coder* c, size_t data_shreds, const uint8_t* const
   ag_rs_decoder* dec = c->dec;
   if (dec->no + dec->nr < kDataShreds) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
   // decode and the re-encode of every coding shard (:206) in one device round trip; the
-  // completed originals (present ones as added, restored ones written back) are dec->orig
-  std::vector<uint8_t> coding(c->num_coding * S);
+  // completed originals (present ones as added, restored ones written back) are dec->orig()
+  const uint8_t* coding = nullptr;
   const bool coded = dec->no < kDataShreds;
-  if (coded && (st = run_one_decode(c->ctx, kDataShreds, c->num_coding, S, dec->orig.data(), dec->rec.data(),
-                                    dec->opres.data(), dec->rpres.data(), AG_RS_DECODE_EXACT, coding.data())))
+  if (coded && (st = run_one_decode(c->ctx, kDataShreds, c->num_coding, S, dec->pin, dec->opres.data(),
+                                    dec->rpres.data(), AG_RS_DECODE_EXACT, true, &coding)))
     return st;
   // concatenation with the TooMuchData bound of :169-188 (exceeded iff 32 S > 32 768)
   if (kDataShreds * S > kMaxAfterPadding) return AG_RS_ERR_TOO_MUCH_DATA;
-  const uint8_t* data = dec->orig.data();
+  const uint8_t* data = dec->orig();
   const size_t total = kDataShreds * S;
   // strip padding: trailing zeros then the 0x80 marker
   size_t zeros = 0;
@@ -2019,11 +2023,16 @@ int ag_rs_coder_deshred(ag_rs_coder* c, size_t data_shreds, const uint8_t* const
   const size_t padding = zeros + 1;
   if (padding > total || data[total - padding] != 0x80) return AG_RS_ERR_INVALID_PADDING;
   const size_t plen = total - padding;
-  if (!coded && (st = coder_encode(c, data, S, coding.data()))) return st;
+  if (!coded) {  // every data shred present: encode them (staged in the encoder)
+    if ((st = ag_rs_encoder_reset(c->enc, kDataShreds, c->num_coding, S))) return st;
+    std::memcpy(c->enc->orig(), data, total);
+    if ((st = coder_encode_staged(c))) return st;
+    coding = c->enc->rec();
+  }
   std::memcpy(payload_out, data, plen);
   *payload_len = plen;
   std::memcpy(data_out, data, total);
-  std::memcpy(coding_out, coding.data(), coding.size());
+  std::memcpy(coding_out, coding, c->num_coding * S);
   *shred_bytes = S;
   return AG_RS_OK;
 }
@@ -2668,7 +2677,10 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   c->xmask_host.clear();  // d_xmask / d_rows no longer hold decode_device's cached patterns
   c->xmask_w = 0;
   uint64_t* xm = c->d_xmask.as<uint64_t>();
-  if (ag::launch_pipe_patterns(d_present, n, xm, few, c->stream) != hipSuccess ||
+  // 1 KiB shreds (every maximum slice) decode on the packed window decoder, which also restores
+  // the absent coding shreds of exactly-k slices (few 2): the re-encode below skips those
+  const bool fuse = cps == 16;
+  if (ag::launch_pipe_patterns(d_present, n, xm, few, fuse, c->stream) != hipSuccess ||
       ag::launch_decode_rows(xm, xm + n, static_cast<uint32_t>(n), static_cast<uint32_t>(W), c->dtables(),
                              c->d_rows.as<uint32_t>(), true, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
@@ -2690,6 +2702,7 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   p.per_lane = 1;
   p.rows_w = static_cast<uint32_t>(W);
   p.any_k = 1;  // launch_pipe_patterns keeps exactly k survivors
+  p.fuse = fuse ? 1u : 0u;
   if (ag::launch_decode_x(static_cast<unsigned>(W), 0, p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   int64_t* strip = c->d_strip.as<int64_t>();
@@ -2709,6 +2722,7 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   xp.n_out = 32;
   xp.chunks_per_shard = static_cast<uint32_t>(cps);
   xp.total_columns = static_cast<uint64_t>(n) * cps;
+  xp.skip_idle = fuse ? 1u : 0u;  // tiles of fused slices only: nothing to re-encode
   if (ag::launch_xform(ag::XformKind::kEncode32, xp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   return pipe_coder_finish(c, n, strip, few, plen);
 }
@@ -2719,7 +2733,7 @@ int pipe_coder_finish(ag_rs_ctx* c, size_t n, const int64_t* strip, const uint8_
   AG_HIP(hipMemcpyAsync(hfew.data(), few, n, hipMemcpyDeviceToHost, c->stream));
   AG_HIP(hipStreamSynchronize(c->stream));
   for (size_t s = 0; s < n; ++s) {
-    if (hfew[s]) plen[s] = -AG_RS_ERR_NOT_ENOUGH_SHARDS;
+    if (hfew[s] & 1) plen[s] = -AG_RS_ERR_NOT_ENOUGH_SHARDS;  // bit 1: coding restored by the decode
     else if (plen[s] < 0) plen[s] = -AG_RS_ERR_INVALID_PADDING;
   }
   return AG_RS_OK;

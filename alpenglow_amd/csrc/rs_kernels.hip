@@ -37,6 +37,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
+  if (p.skip_idle) {  // per-block masks: a tile none of whose blocks stores anything exits
+    const uint64_t col = static_cast<uint64_t>(tile) * kXfLanes + lane;
+    const uint64_t m = col < p.total_columns ? p.out_mask[col / p.chunks_per_shard] : 0;
+    if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return;
+  }
   Regs8 ra;
   xf_load_raw(p, tile_io(p, tile, lane, p.in_block_stride), wave, ra);
   // Store-mask words, fetched now so their latency hides under the data loads.  With
@@ -851,7 +856,7 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
 // the cancellation programs this kernel's allocation spills (14 VGPRs).
 template <int OUTH>
 __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p) {
-  static_assert(OUTH == 0 || OUTH == 1, "the restored originals lie in one window half");
+  static_assert(OUTH >= -1 && OUTH <= 1, "OUTH: the restored positions' window half, -1 both");
   using LB = X8Lay<2, 1, 3, 4, 5>;
   using LC = X8Lay<2, 3, 1, 4, 5>;
   using LD = X8Lay<4, 3, 1, 2, 5>;
@@ -1011,7 +1016,10 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
   x8_layer_t<LE, 5, false, 0, 1>(wave, r);
   x8_layer_t<LE, 4, false, 0, 1>(wave, r);
   wait_readers(wave ^ 4, 5);
-  {
+  if constexpr (OUTH < 0) {
+    // restored positions in both halves (fused coding restore): every wave finishes the FFT
+    x8_swap<1, 2, 4 + D, 0xF, false>(wave, lane, lds, &flags, r);
+  } else {
     const int partner = wave ^ 4;
     if (((wave >> 2) & 1) != OUTH) {
       x8_wait_ge(&flags.done[partner], 3 + D);
@@ -1044,10 +1052,12 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
   h8_layer0<false, 0, 1>(wave, h, r);
   // 4. packed output products.  Every live wave's last swap read is done before any item
   // overwrites a region; items written, then every live wave's items visible before reads.
-  const int lw = wave & 3;  // live waves: wave bit 2 == OUTH
-  static_for<4>([&](auto Wv) {
+  constexpr int kLive = OUTH < 0 ? 8 : 4;     // live waves: all, or wave bit 2 == OUTH
+  constexpr int kHi = OUTH < 0 ? 0 : OUTH << 2;
+  const int lw = wave & (kLive - 1);
+  static_for<kLive>([&](auto Wv) {
     constexpr int w2 = decltype(Wv)::value;
-    x8_wait_ge(&flags.done[w2 | (OUTH << 2)], 6 + D);
+    x8_wait_ge(&flags.done[w2 | kHi], 6 + D);
   });
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
@@ -1061,15 +1071,16 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
     }
   });
   x8_signal(&flags.ready[wave], 7 + D, lane);
-  static_for<4>([&](auto Wv) {
+  static_for<kLive>([&](auto Wv) {
     constexpr int w2 = decltype(Wv)::value;
-    x8_wait_ge(&flags.ready[w2 | (OUTH << 2)], 7 + D);
+    x8_wait_ge(&flags.ready[w2 | kHi], 7 + D);
   });
-  // item o on row group o & 3 of slot (o >> 2) & 3 of live wave o >> 4
-  static_for<4>([&](auto U) {
+  // item o on row group o & 3 of slot (o >> 2) & (kPer / 4 - 1) of live wave o / kPer
+  constexpr int kPer = 64 / kLive;  // items per live wave
+  static_for<kPer / 4>([&](auto U) {
     constexpr int u = decltype(U)::value;
-    if (static_cast<uint32_t>(lw * 16 + u * 4) < nout) {  // wave-uniform
-      const uint32_t o = lw * 16 + u * 4 + row;
+    if (static_cast<uint32_t>(lw * kPer + u * 4) < nout) {  // wave-uniform
+      const uint32_t o = lw * kPer + u * 4 + row;
       if (o < nout) {
         const uint32_t sl = o < noA ? 0u : 1u;
         const uint32_t j = olist[sl][o - (sl ? noA : 0u)];
@@ -1905,6 +1916,7 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
     const bool packed = pl && p.any_k && p.chunks_per_shard == 16 && (p.low_rate || p.chunk == 32);
     if (packed) {
       if (p.low_rate) hipLaunchKernelGGL((decode_pk_kernel<0>), g32, dim3(512), 0, stream, p);
+      else if (p.fuse) hipLaunchKernelGGL((decode_pk_kernel<-1>), g32, dim3(512), 0, stream, p);
       else hipLaunchKernelGGL((decode_pk_kernel<1>), g32, dim3(512), 0, stream, p);
     } else if (!pl) AG_X16(0, 0, 0);
     else if (p.low_rate) AG_H8(0, 0, 0, 0);
@@ -2193,11 +2205,20 @@ hipError_t launch_coder_strip(const uint8_t* cw, uint64_t cw_stride, uint32_t da
 hipError_t launch_fill_splitmix(uint8_t* dst, uint64_t nblocks, uint64_t block_bytes, uint64_t dst_block_stride,
                                 uint64_t seed_base, hipStream_t stream) {
   if (block_bytes % 8) return hipErrorInvalidValue;
-  const uint64_t words = block_bytes / 8, pairs = (words + 1) / 2, n = nblocks * pairs;
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(fill_splitmix_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream, dst,
-                     nblocks, words, dst_block_stride, seed_base);
-  return hipGetLastError();
+  const uint64_t words = block_bytes / 8, pairs = (words + 1) / 2;
+  if (nblocks == 0 || pairs == 0) return hipSuccess;
+  if (pairs > (uint64_t{1} << 30)) return hipErrorInvalidValue;
+  // a dispatch's grid is at most 2^32 - 1 work-items (HSA packet): launches of at most 2^30
+  // threads' worth of whole blocks (BASELINE configs[4]'s 64 GiB stream at N = 1 is 2^32 pairs)
+  const uint64_t per = std::max<uint64_t>(1, (uint64_t{1} << 30) / pairs);
+  for (uint64_t b0 = 0; b0 < nblocks; b0 += per) {
+    const uint64_t nb = std::min(per, nblocks - b0), n = nb * pairs;
+    hipLaunchKernelGGL(fill_splitmix_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream,
+                       dst + b0 * dst_block_stride, nb, words, dst_block_stride, seed_base + b0);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace ag

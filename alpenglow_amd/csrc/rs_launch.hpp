@@ -24,6 +24,8 @@ struct XformParams {
   uint32_t chunks_per_shard;   // shard_bytes / 64
   uint64_t total_columns;         // nblocks * chunks_per_shard
   uint32_t out_low_half;          // decode: every stored shard is < N / 2 (pruned FFT)
+  uint32_t skip_idle;             // xform<4> with per-block masks: tiles whose blocks all have
+                                  // mask 0 exit before loading (re-encodes of a few slices)
 };
 
 enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };
@@ -192,6 +194,8 @@ struct DecodeXParams {
   uint64_t total_columns;  // batch blocks * chunks_per_shard
   uint32_t rows_w;         // constants per pattern in rows (W = 64: 64; W = 128: 128)
   uint32_t any_k;          // 1: every pattern loads at most k survivors (ANY_K; the packed kernel)
+  uint32_t fuse;           // packed kernel, HighRate: the restored set may include recovery positions
+                           // (every erased position of an exactly-k pattern: decode_pk<-1>)
 };
 // W = 32 / 64: pass 0.  W = 128: pass 1 (the other half's inputs, raw partial outputs), then
 // pass 2 (the output half's inputs, the partial added, output multiply); masks per pass.

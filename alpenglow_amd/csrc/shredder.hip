@@ -130,8 +130,16 @@ __device__ __forceinline__ uint64_t keep_lowest(uint64_t b, uint32_t budget) {
 }
 
 // ANY_K survivors of one slice's kept shreds in the W = 64 window (decode_device's rule).
+// fuse: slices with exactly k = 32 kept shreds (every successful deshred of the reference's
+// follower, slot_block_data.rs:343-355) also restore their absent coding shreds in the same
+// window decode (decode_pk<-1>): the 32 survivors fix the codeword, so the decoder's values at
+// the absent recovery positions are exactly the re-encode of the restored data
+// (reed_solomon.rs:206) -- few[s] bit 1 marks them, and the separate re-encode skips them.
+// Slices with surplus kept shreds keep the re-encode (present-but-unused recovery shreds are
+// rewritten only when the slice succeeds).  few[s] bit 0: fewer than k kept shreds.
 __global__ __launch_bounds__(256) void pipe_patterns_kernel(const uint64_t* __restrict__ present, uint64_t n,
-                                                            uint64_t* __restrict__ xm, uint8_t* __restrict__ few) {
+                                                            uint64_t* __restrict__ xm, uint8_t* __restrict__ few,
+                                                            uint32_t fuse) {
   const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (s >= n) return;
   const uint64_t pr = present[s];
@@ -139,16 +147,21 @@ __global__ __launch_bounds__(256) void pipe_patterns_kernel(const uint64_t* __re
   uint64_t rb = pr >> 32;
   const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(pr));
   uint64_t in = 0, out = 0, e = 0;
+  uint8_t f = cnt < kPipeData ? 1 : 0;
   if (cnt >= kPipeData && ob != 0xFFFFFFFFull) {
     rb = keep_lowest(rb, kPipeData - static_cast<uint32_t>(__builtin_popcountll(ob)));
     in = rb | (ob << 32);
     out = (~ob & 0xFFFFFFFFull) << 32;
     e = (~rb & 0xFFFFFFFFull) | out;
+    if (fuse && cnt == kPipeData) {  // no surplus: every erased position is an absent shred
+      out = e;
+      f = 2;
+    }
   }
   xm[s] = e;
   xm[n + 2 * s] = in;
   xm[n + 2 * s + 1] = out;
-  few[s] = cnt < kPipeData ? 1 : 0;
+  few[s] = f;
 }
 
 // ANY_K survivors of one CodingOnly slice (LowRate 32:64) in the W = 128 window, decode_device's
@@ -192,7 +205,7 @@ __global__ __launch_bounds__(256) void pipe_store_mask_kernel(const uint8_t* __r
                                                               uint64_t* __restrict__ mask) {
   const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (s >= n) return;
-  mask[s] = (!few[s] && strip[s] >= 0) ? ~uint64_t{0} : uint64_t{0};
+  mask[s] = (!few[s] && strip[s] >= 0) ? ~uint64_t{0} : uint64_t{0};  // few 2: restored by the decode
 }
 
 }  // namespace
@@ -243,10 +256,11 @@ hipError_t launch_pipe_merge_lens(const uint32_t* fresh, const uint64_t* present
   return hipGetLastError();
 }
 
-hipError_t launch_pipe_patterns(const uint64_t* present, uint64_t nslices, uint64_t* xm, uint8_t* few,
+hipError_t launch_pipe_patterns(const uint64_t* present, uint64_t nslices, uint64_t* xm, uint8_t* few, bool fuse,
                                 hipStream_t stream) {
   if (nslices == 0) return hipSuccess;
-  hipLaunchKernelGGL(pipe_patterns_kernel, grid256(nslices), dim3(256), 0, stream, present, nslices, xm, few);
+  hipLaunchKernelGGL(pipe_patterns_kernel, grid256(nslices), dim3(256), 0, stream, present, nslices, xm, few,
+                     fuse ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -91,7 +91,10 @@ hipError_t launch_pipe_merge_lens(const uint32_t* fresh, const uint64_t* present
 //   then recovery shards in index order up to 32), xm[n + 2 s + 1] = originals restored.
 // Slices with fewer than 32 kept shreds, or nothing to restore, get empty masks (no loads, no
 // stores); few[s] = 1 for the former (NotEnoughShreds, reed_solomon.rs:144).
-hipError_t launch_pipe_patterns(const uint64_t* present, uint64_t nslices, uint64_t* xm, uint8_t* few,
+// fuse (the packed window decoder, decode_pk<-1>): a slice with exactly 32 kept shreds also
+// restores its absent coding shreds in the decode (xm[n + 2 s + 1] = every erased position)
+// and gets few[s] = 2, so the re-encode's store mask skips it.
+hipError_t launch_pipe_patterns(const uint64_t* present, uint64_t nslices, uint64_t* xm, uint8_t* few, bool fuse,
                                 hipStream_t stream);
 // The same for CodingOnly slices (LowRate 32:64) in the W = 128 window of the two-pass decoder:
 // present[2 s] = data bits | coding 0..31 << 32, present[2 s + 1] = coding 32..63; xm =
@@ -101,7 +104,7 @@ hipError_t launch_pipe_patterns128(const uint64_t* present, uint64_t nslices, ui
                                    hipStream_t stream);
 // mask[s] = ~0 (store every coding shard of the re-encode) when the slice decoded and its
 // padding stripped (few[s] == 0 and strip[s] >= 0), else 0 (the coding shreds stay as they
-// are, like the reference's early returns).
+// are, like the reference's early returns; few[s] == 2: the decode restored them).
 hipError_t launch_pipe_store_masks(const uint8_t* few, const int64_t* strip, uint64_t nslices, uint64_t* mask,
                                    hipStream_t stream);
 

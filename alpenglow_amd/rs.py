@@ -228,7 +228,11 @@ def _coder_binding():
             spec.loader.exec_module(mod)
             L = load()
             addr = lambda f: ctypes.cast(f, ctypes.c_void_p).value  # noqa: E731
-            mod.bind(addr(L.ag_rs_coder_shred), addr(L.ag_rs_coder_deshred), addr(L.ag_rs_coder_num_coding))
+            mod.bind(*(addr(getattr(L, f)) for f in (
+                "ag_rs_coder_shred", "ag_rs_coder_deshred", "ag_rs_coder_num_coding",
+                "ag_rs_encoder_add_original_shard", "ag_rs_encoder_encode", "ag_rs_encoder_recovery",
+                "ag_rs_decoder_add_original_shard", "ag_rs_decoder_add_recovery_shard", "ag_rs_decoder_decode",
+                "ag_rs_decoder_restored_original")))
         _pycoder = mod
     return _pycoder or None
 
@@ -418,12 +422,21 @@ class ReedSolomonEncoder:
         self.recovery_count = recovery_count
 
     def add_original_shard(self, shard: bytes):
+        pc = _coder_binding()
+        if pc is not None:
+            _check(pc.enc_add(self.handle.value, shard), "add_original_shard")
+            return
         b = _buf(shard)
         _check(self._lib.ag_rs_encoder_add_original_shard(self.handle, b, len(shard)),
                "add_original_shard")
 
     def encode(self) -> list[bytes]:
         """encode() + EncoderResult::recovery_iter(), copied out (reed_solomon.rs:125)."""
+        pc = _coder_binding()
+        if pc is not None:
+            st, out = pc.enc_encode(self.handle.value, self.recovery_count)
+            _check(st, "ReedSolomonEncoder::encode")
+            return out
         _check(self._lib.ag_rs_encoder_encode(self.handle), "ReedSolomonEncoder::encode")
         out = []
         for j in range(self.recovery_count):
@@ -464,17 +477,30 @@ class ReedSolomonDecoder:
         self.original_count = original_count
 
     def add_original_shard(self, index: int, shard: bytes):
+        pc = _coder_binding()
+        if pc is not None:
+            _check(pc.dec_add(self.handle.value, True, index, shard), "add_original_shard")
+            return
         b = _buf(shard)
         _check(self._lib.ag_rs_decoder_add_original_shard(self.handle, index, b, len(shard)),
                "add_original_shard")
 
     def add_recovery_shard(self, index: int, shard: bytes):
+        pc = _coder_binding()
+        if pc is not None:
+            _check(pc.dec_add(self.handle.value, False, index, shard), "add_recovery_shard")
+            return
         b = _buf(shard)
         _check(self._lib.ag_rs_decoder_add_recovery_shard(self.handle, index, b, len(shard)),
                "add_recovery_shard")
 
     def decode(self) -> dict[int, bytes]:
         """decode() + DecoderResult::restored_original(i) for every i (None omitted)."""
+        pc = _coder_binding()
+        if pc is not None:
+            st, out = pc.dec_decode(self.handle.value, self.original_count)
+            _check(st, "ReedSolomonDecoder::decode")
+            return out
         _check(self._lib.ag_rs_decoder_decode(self.handle), "ReedSolomonDecoder::decode")
         out = {}
         for i in range(self.original_count):

@@ -233,7 +233,9 @@ int ag_rs_coder_shred_batch(ag_rs_ctx* ctx, size_t num_coding, size_t nslices, s
  * re-encodes all num_coding coding shards of every slice that succeeded (RawShreds of the
  * reference).  payload_len_out (HOST, nslices): the payload length (the payload is the
  * first len bytes of the slice's data region), or -AG_RS_ERR_NOT_ENOUGH_SHARDS /
- * -AG_RS_ERR_INVALID_PADDING for a slice whose coding shards are left untouched.  mode:
+ * -AG_RS_ERR_INVALID_PADDING for a slice whose received shards are left untouched (its absent
+ * shard slots hold unspecified bytes: a slice with exactly 32 kept 1 KiB shreds restores its
+ * absent data and coding shards in one decode, before the padding check).  mode:
  * AG_RS_DECODE_EXACT (crate semantics) or AG_RS_DECODE_ANY_K.  Synchronous.  Whole-call
  * errors: TOO_MUCH_DATA (S > 1024), INVALID_SHARD_SIZE. */
 int ag_rs_coder_deshred_batch(ag_rs_ctx* ctx, size_t num_coding, size_t nslices,

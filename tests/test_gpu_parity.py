@@ -767,12 +767,78 @@ def test_coder_deshred_batch(ctx, dev, S, mode, m):
             payload, raw = o.coder_deshred_indexed(orig_b, rec_b, m)
         except o.RSError as err:  # wrapper NotEnoughShreds maps to the crate status code
             assert res[b] == {"NotEnoughShreds": "NotEnoughShards"}.get(err.kind, err.kind), (b, res[b])
-            assert host[b, 32 * S:].tobytes() == damaged[b, 32 * S:].tobytes()  # coding untouched
+            for j in range(m):  # the received coding shreds untouched (absent ones unspecified)
+                if 32 + j in present[b]:
+                    assert host[b, (32 + j) * S:(33 + j) * S].tobytes() == damaged[b, (32 + j) * S:(33 + j) * S].tobytes()
             continue
         assert res[b] == len(payload), (b, res[b])
         assert host[b, :len(payload)].tobytes() == payload
         assert host[b, :32 * S].tobytes() == b"".join(raw.data)
         assert host[b, 32 * S:].tobytes() == b"".join(raw.coding)
+
+
+@pytest.mark.parametrize("mode", [rs.DECODE_ANY_K, rs.DECODE_EXACT])
+def test_coder_deshred_fused_coding_restore(ctx, dev, mode):
+    """The follower's deshred at exactly k = 32 kept shreds (slot_block_data.rs:343-355): the
+    packed window decoder restores the absent coding shreds in the same transform as the data
+    shreds (decode_pk<-1>, no re-encode pass), bit-exact against the oracle's re-encode
+    (o.encode of the restored data, reed_solomon.rs:206), mixed with slices that keep the
+    separate re-encode (surplus shreds; every data shred present), NotEnoughShreds and
+    InvalidPadding slices.  Every absent shred is overwritten with garbage first."""
+    rng = random.Random(0xF05E + mode)
+    n, S, m = 64, 1024, 32
+    stride = (32 + m) * S
+    lens = _payload_lens(rng, S, n)
+    cw = np.zeros((n, stride), np.uint8)
+    for b in range(n):
+        if b in (6, 40):  # random data without a padding marker: InvalidPadding
+            data = bytearray(o.splitmix64_bytes(900 + b, 32 * S))
+            data[-1] = 0x11
+            cw[b, :32 * S] = np.frombuffer(bytes(data), np.uint8)
+            cw[b, 32 * S:] = np.frombuffer(b"".join(o.encode([bytes(data[i * S:(i + 1) * S]) for i in range(32)], m)),
+                                           np.uint8)
+            continue
+        raw = o.coder_shred(o.splitmix64_bytes(3000 + b, lens[b]), m)
+        cw[b] = np.frombuffer(b"".join(raw.data) + b"".join(raw.coding), np.uint8)
+    present = []
+    for b in range(n):
+        if b == 1:
+            keep = set(range(32))                     # every data shred, no coding: re-encode
+        elif b == 2:
+            keep = set(range(32, 64))                 # every coding shred, no data
+        elif b == 3:
+            keep = set(rng.sample(range(64), 31))     # NotEnoughShreds
+        elif b % 9 == 5 and mode == rs.DECODE_ANY_K:
+            keep = set(rng.sample(range(64), 36))     # surplus: the separate re-encode
+        else:
+            keep = set(rng.sample(range(64), 32))     # random 32-of-64 arrival: fused
+        present.append(keep)
+    damaged = cw.copy()
+    for b in range(n):
+        for i in range(64):
+            if i not in present[b]:
+                damaged[b, i * S:(i + 1) * S] = (0x5A + i) & 0xFF
+    dp = [1 if i in present[b] else 0 for b in range(n) for i in range(32)]
+    cp = [1 if 32 + j in present[b] else 0 for b in range(n) for j in range(m)]
+    d_cw = to_dev(damaged, dev)
+    res = rs.coder_deshred_batch(ctx, m, n, S, d_cw, stride, dp, cp, mode)
+    host = d_cw.cpu().numpy()
+    ok = 0
+    for b in range(n):
+        orig_b = {i: cw[b, i * S:(i + 1) * S].tobytes() for i in range(32) if i in present[b]}
+        rec_b = {j: cw[b, (32 + j) * S:(33 + j) * S].tobytes() for j in range(m) if 32 + j in present[b]}
+        try:
+            payload, raw = o.coder_deshred_indexed(orig_b, rec_b, m)
+        except o.RSError as err:
+            assert res[b] == {"NotEnoughShreds": "NotEnoughShards"}.get(err.kind, err.kind), (b, res[b])
+            for i in present[b]:
+                assert host[b, i * S:(i + 1) * S].tobytes() == damaged[b, i * S:(i + 1) * S].tobytes(), (b, i)
+            continue
+        ok += 1
+        assert res[b] == len(payload), (b, res[b])
+        assert host[b, :32 * S].tobytes() == b"".join(raw.data), b
+        assert host[b, 32 * S:].tobytes() == b"".join(raw.coding), b
+    assert ok >= n - 4
 
 
 # --------------------------------------------------------- host-memory (PCIe) pipeline

@@ -6,6 +6,8 @@
 //   shred           payload -> 32 data + 32 coding shreds of 1 KiB
 //   deshred_coding  from the 32 coding shreds only (benches/shredder.rs:49-53's shape)
 //   deshred_random  from a random 32 of the 64 shreds (the follower's arrival)
+//   route_a_*       ReedSolomonEncoder / ReedSolomonDecoder (the facade's entry points): reset,
+//                   32 adds, encode / decode, 32 result reads copied out
 // Usage: latency_probe [calls]   (built by tools/latency/build.sh against the in-tree library)
 #include <algorithm>
 #include <chrono>
@@ -78,11 +80,63 @@ int main(int argc, char** argv) {
   if (plen != payload.size() || std::memcmp(pout.data(), payload.data(), plen) ||
       std::memcmp(cout.data(), coding.data(), 32 * S))
     return 4;
+  // Route A's own entry points in the Rust facade's call pattern: the crate's
+  // ReedSolomonEncoder / ReedSolomonDecoder as reed_solomon.rs drives them per slice --
+  // reset, 32 add_*_shard, encode / decode, 32 result reads (recovery_iter / restored_original)
+  ag_rs_encoder* enc = nullptr;
+  ag_rs_decoder* dec = nullptr;
+  if (ag_rs_encoder_new_on_device(0, 32, 32, S, &enc) || ag_rs_decoder_new_on_device(0, 32, 32, S, &dec)) return 5;
+  std::vector<uint8_t> sink(32 * S);
+  auto encoder = [&] {
+    int st = ag_rs_encoder_reset(enc, 32, 32, S);
+    for (int i = 0; i < 32 && !st; ++i) st = ag_rs_encoder_add_original_shard(enc, data.data() + i * S, S);
+    if (!st) st = ag_rs_encoder_encode(enc);
+    for (int j = 0; j < 32 && !st; ++j) {
+      const uint8_t* r = nullptr;
+      size_t len = 0;
+      st = ag_rs_encoder_recovery(enc, j, &r, &len);
+      if (!st) std::memcpy(sink.data() + j * S, r, len);  // the facade's .to_vec()
+    }
+    return st;
+  };
+  std::vector<int> keep;  // decoder: the follower's random 32 of 64
+  auto decoder = [&] {
+    int st = ag_rs_decoder_reset(dec, 32, 32, S);
+    for (int i : keep) {
+      if (st) break;
+      st = i < 32 ? ag_rs_decoder_add_original_shard(dec, i, data.data() + i * S, S)
+                  : ag_rs_decoder_add_recovery_shard(dec, i - 32, coding.data() + (i - 32) * S, S);
+    }
+    if (!st) st = ag_rs_decoder_decode(dec);
+    for (int i = 0; i < 32 && !st; ++i) {
+      const uint8_t* r = nullptr;
+      size_t len = 0;
+      if (ag_rs_decoder_restored_original(dec, i, &r, &len) == 0) std::memcpy(sink.data() + i * S, r, len);
+    }
+    return st;
+  };
+  const Stat s_enc = time(encoder);
+  if (std::memcmp(sink.data(), coding.data(), 32 * S)) return 6;
+  keep.assign(coding_only.begin(), coding_only.end());
+  const Stat s_dec_c = time(decoder);
+  if (std::memcmp(sink.data(), data.data(), 32 * S)) return 7;
+  keep.assign(all.begin(), all.end());
+  const Stat s_dec_r = time(decoder);
+  for (int i = 0; i < 32; ++i)
+    if (std::find(keep.begin(), keep.end(), i) == keep.end() && std::memcmp(sink.data() + i * S, data.data() + i * S, S))
+      return 8;
   std::printf("{\"unit\": \"us per call\", \"caller\": \"C++ through the C ABI\", \"calls\": %d, "
               "\"shred\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
               "\"deshred_coding_only\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
-              "\"deshred_random_32_of_64\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}}\n",
-              calls, s_shred.med, s_shred.p90, s_shred.min, s_dc.med, s_dc.p90, s_dc.min, s_dr.med, s_dr.p90, s_dr.min);
+              "\"deshred_random_32_of_64\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
+              "\"route_a_encoder\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
+              "\"route_a_decoder_coding_only\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
+              "\"route_a_decoder_random_32_of_64\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}}\n",
+              calls, s_shred.med, s_shred.p90, s_shred.min, s_dc.med, s_dc.p90, s_dc.min, s_dr.med, s_dr.p90, s_dr.min,
+              s_enc.med, s_enc.p90, s_enc.min, s_dec_c.med, s_dec_c.p90, s_dec_c.min, s_dec_r.med, s_dec_r.p90,
+              s_dec_r.min);
+  ag_rs_encoder_free(enc);
+  ag_rs_decoder_free(dec);
   ag_rs_coder_free(coder);
   return 0;
 }
