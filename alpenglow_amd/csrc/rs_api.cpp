@@ -16,6 +16,7 @@
 #include <cstddef>
 #include <cstdlib>
 #include <cstring>
+#include <immintrin.h>
 #include <memory>
 #include <new>
 #include <vector>
@@ -172,6 +173,8 @@ struct ag_rs_ctx {
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
   DevBuf d_pipe_few, d_pipe_mask;           // composed deshred: too-few flags, re-encode store masks
   DevBuf d_present;                         // coder batches: per-slice present masks
+  PinBuf h_present;                         // their pinned host staging
+  hipEvent_t present_ev = nullptr;          // recorded after its upload
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
   static constexpr int kPipeBufs = 25;
   DevBuf pipe[kPipeBufs];                   // composed shredder scratch (ag_shredder_*_batch)
@@ -299,6 +302,11 @@ struct ag_rs_ctx {
                       &one_out, &d_pipe_few, &d_pipe_mask, &d_present})
       b->release();
     for (DevBuf& b : pipe) b.release();
+    if (present_ev) {
+      (void)hipEventSynchronize(present_ev);
+      (void)hipEventDestroy(present_ev);
+    }
+    h_present.release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -2067,6 +2075,44 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
 }  // namespace
 
 namespace {
+// Per-slice present words of ag_rs_coder_deshred_batch's device-pattern path: word 0 = data
+// flags | coding 0..31 << 32 (and word 1 = coding 32..63 when m = 64).  Returns whether any
+// slice keeps more than 32 shreds.  The flag bytes are 4 MiB per 65 536 slices: compared 32
+// at a time with AVX2 where the host has it (the 8-byte multiply trick of pack_flags took
+// ~0.5 ms of the call).
+__attribute__((target("avx2"))) uint32_t nonzero_mask32_avx2(const uint8_t* f) {
+  const __m256i x = _mm256_loadu_si256(reinterpret_cast<const __m256i*>(f));
+  return ~static_cast<uint32_t>(_mm256_movemask_epi8(_mm256_cmpeq_epi8(x, _mm256_setzero_si256())));
+}
+// (a macro body, not a template: this part of the file has C linkage)
+#define AG_PACK_PRESENT(MASK32)                                                   \
+  const size_t wps = m == kDataShreds ? 1 : 2;                                    \
+  bool surplus = false;                                                           \
+  for (size_t b = 0; b < n; ++b) {                                                \
+    uint64_t* q = pres + wps * b;                                                 \
+    q[0] = uint64_t{MASK32(dpres + b * kDataShreds)} | (uint64_t{MASK32(cpres + b * m)} << 32); \
+    int cnt = __builtin_popcountll(q[0]);                                         \
+    if (wps == 2) {                                                               \
+      q[1] = MASK32(cpres + b * m + 32);                                          \
+      cnt += __builtin_popcountll(q[1]);                                          \
+    }                                                                             \
+    surplus |= cnt > static_cast<int>(kDataShreds);                               \
+  }                                                                               \
+  return surplus;
+__attribute__((target("avx2"))) bool pack_present_avx2(const uint8_t* dpres, const uint8_t* cpres, size_t m, size_t n,
+                                                       uint64_t* pres) {
+  AG_PACK_PRESENT(nonzero_mask32_avx2)
+}
+uint32_t nonzero_mask32(const uint8_t* f) { return static_cast<uint32_t>(pack_flags(f, 32)); }
+bool pack_present_scalar(const uint8_t* dpres, const uint8_t* cpres, size_t m, size_t n, uint64_t* pres) {
+  AG_PACK_PRESENT(nonzero_mask32)
+}
+#undef AG_PACK_PRESENT
+bool pack_present_words(const uint8_t* dpres, const uint8_t* cpres, size_t m, size_t n, uint64_t* pres) {
+  static const bool avx2 = __builtin_cpu_supports("avx2");
+  return avx2 ? pack_present_avx2(dpres, cpres, m, n, pres) : pack_present_scalar(dpres, cpres, m, n, pres);
+}
+
 // ag_rs_coder_deshred_batch when every slice has the same present shreds (pattern = slice 0's).
 int coder_deshred_uniform(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
                           const uint8_t* dpres, const uint8_t* cpres, int mode, int64_t* out) {
@@ -2133,19 +2179,18 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   // CodingOnlyShredder's 32:64 (LowRate) takes the same path with the W = 128 window.
   if ((m == kDataShreds || m == 2 * kDataShreds) && S % 64 == 0 && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
     const size_t wps = m == kDataShreds ? 1 : 2;  // present words per slice
-    std::vector<uint64_t> pres(wps * n);
+    // packed straight into pinned staging, so the upload is one DMA with no pageable bounce
+    // (once the previous call's upload of it has completed)
+    if (c->present_ev) AG_HIP(hipEventSynchronize(c->present_ev));
+    else AG_HIP(hipEventCreateWithFlags(&c->present_ev, hipEventDisableTiming));
+    if ((st = c->h_present.ensure(wps * n * 8))) return st;
+    uint64_t* pres = c->h_present.as<uint64_t>();
     // (uniform batches returned above)
-    bool surplus = false;
-    for (size_t b = 0; b < n; ++b) {
-      const uint64_t* q = &pres[wps * b];
-      pres[wps * b] = pack_flags(dpres + b * kDataShreds, kDataShreds) | (pack_flags(cpres + b * m, 32) << 32);
-      if (wps == 2) pres[wps * b + 1] = pack_flags(cpres + b * m + 32, 32);
-      surplus = surplus ||
-                __builtin_popcountll(q[0]) + (wps == 2 ? __builtin_popcountll(q[1]) : 0) > static_cast<int>(kDataShreds);
-    }
+    const bool surplus = pack_present_words(dpres, cpres, m, n, pres);
     if (mode == AG_RS_DECODE_ANY_K || !surplus) {
       if ((st = c->d_present.ensure(wps * n * 8, c->stream))) return st;
-      AG_HIP(hipMemcpyAsync(c->d_present.ptr, pres.data(), wps * n * 8, hipMemcpyHostToDevice, c->stream));
+      AG_HIP(hipMemcpyAsync(c->d_present.ptr, pres, wps * n * 8, hipMemcpyHostToDevice, c->stream));
+      AG_HIP(hipEventRecord(c->present_ev, c->stream));
       return pipe_coder_deshred(c, n, S, cw, cw_stride, c->d_present.as<uint64_t>(), out, m);  // synchronous
     }
   }

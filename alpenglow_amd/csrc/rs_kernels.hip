@@ -1567,33 +1567,42 @@ __global__ __launch_bounds__(1024) void locator_kernel(const uint8_t* erased, ui
 // Data region of slice b (32 * S bytes at cw + b * cw_stride) := payload || 0x80 || 0...
 // (payload == null: the payload already sits in the data region; only the padding is
 // written).  One thread per 16 output bytes.
+// One workgroup per slice, its threads striding over the slice's 16-byte pieces: with a
+// payload source every piece is copied (the tail piece merged with 0x80 00..); in place
+// (payload null) only the pieces from the one holding byte `len` are written -- a maximum
+// slice's padding is one piece, where the earlier one-thread-per-piece grid read every
+// piece's length word and divided for it (0.3 ms per 65 536 slices for one byte each).
 __global__ __launch_bounds__(256) void coder_pad_kernel(const uint8_t* __restrict__ payload, uint64_t payload_stride,
                                                         const uint32_t* __restrict__ lens, uint8_t* cw,
                                                         uint64_t cw_stride, uint32_t data_bytes, uint64_t nslices) {
-  const uint64_t per = data_bytes / 16;
-  const uint64_t tid = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (tid >= nslices * per) return;
-  const uint64_t b = tid / per;
-  const uint32_t j = static_cast<uint32_t>(tid - b * per) * 16;
+  const uint64_t b = blockIdx.x;
+  const uint32_t per = data_bytes / 16;
   const uint32_t len = lens[b];
-  uint8_t* dst = cw + b * cw_stride + j;
-  if (j + 16 <= len) {
-    if (payload) {
-      const uint8_t* src = payload + b * payload_stride + j;
-      if ((reinterpret_cast<uintptr_t>(src) & 15) == 0) {
-        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src);
+  uint8_t* base = cw + b * cw_stride;
+  const uint8_t* src = payload ? payload + b * payload_stride : nullptr;
+  const bool a16 = src && (reinterpret_cast<uintptr_t>(src) & 15) == 0;
+  for (uint32_t piece = (src ? 0u : len / 16) + threadIdx.x; piece < per; piece += blockDim.x) {
+    const uint32_t j = piece * 16;
+    uint8_t* dst = base + j;
+    if (j + 16 <= len) {  // whole payload piece (only with a source)
+      if (a16) {
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(src + j);
       } else {
-        for (int i = 0; i < 16; ++i) dst[i] = src[i];
+        for (int i = 0; i < 16; ++i) dst[i] = src[j + i];
       }
+      continue;
     }
-    return;
+    if (j >= len + 1) {  // padding zeros only
+      *reinterpret_cast<uint4*>(dst) = make_uint4(0, 0, 0, 0);
+      continue;
+    }
+    uint8_t v[16];
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t pos = j + i;
+      v[i] = pos < len ? (src ? src[pos] : dst[i]) : (pos == len ? 0x80 : 0);
+    }
+    for (int i = 0; i < 16; ++i) dst[i] = v[i];
   }
-  uint8_t v[16];
-  for (int i = 0; i < 16; ++i) {
-    const uint32_t pos = j + i;
-    v[i] = pos < len ? (payload ? payload[b * payload_stride + pos] : dst[i]) : (pos == len ? 0x80 : 0);
-  }
-  for (int i = 0; i < 16; ++i) dst[i] = v[i];
 }
 
 // Shard restride for shard sizes that are not whole 64-byte chunks (the
@@ -1792,36 +1801,44 @@ __global__ __launch_bounds__(256) void unpack_tail_kernel(const RestrideParams p
 // Padding strip (reed_solomon.rs:191-203): the last non-zero byte of the data region must
 // be 0x80.  The padding sits at the end, so the workgroup scans 4 KiB windows backwards
 // with 16-byte loads and stops at the first window holding a non-zero byte.
+// Padding strip (reed_solomon.rs:189-202): the last nonzero byte of the slice's data region
+// must be the 0x80 marker.  One wave per slice scans back from the end in 1 KiB windows (one
+// 16-byte piece per lane, a ballot picks the highest lane with a nonzero byte): a maximum
+// slice's marker lies in its last shred, so the wave reads 1 KiB and never synchronises.
 __global__ __launch_bounds__(256) void coder_strip_kernel(const uint8_t* __restrict__ cw, uint64_t cw_stride,
-                                                          uint32_t data_bytes, int64_t* out) {
-  __shared__ int32_t best;
-  const uint8_t* d = cw + static_cast<uint64_t>(blockIdx.x) * cw_stride;
+                                                          uint32_t data_bytes, uint64_t nslices, int64_t* out) {
+  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (b >= nslices) return;  // wave-uniform
+  const uint8_t* d = cw + b * cw_stride;
   const bool a16 = ((reinterpret_cast<uintptr_t>(cw) | cw_stride) & 15) == 0;
-  int32_t found = -1;
-  for (int64_t hi = data_bytes; hi > 0 && found < 0; hi -= 4096) {
-    const int64_t lo = hi > 4096 ? hi - 4096 : 0;
-    if (threadIdx.x == 0) best = -1;
-    __syncthreads();
-    const int64_t i0 = lo + 16 * static_cast<int64_t>(threadIdx.x);
-    int32_t last = -1;
-    if (i0 < hi) {  // data_bytes % 16 == 0: whole 16-byte pieces
-      uint8_t v[16];
+  int64_t found = -1;
+  for (int64_t hi = data_bytes; hi > 0 && found < 0; hi -= 1024) {  // data_bytes % 16 == 0
+    const int64_t i0 = hi - 1024 + 16 * static_cast<int64_t>(lane);
+    int32_t last = -1;  // highest nonzero byte of this lane's piece
+    if (i0 >= 0) {
+      uint32_t w[4];
       if (a16) {
         const uint4 x = *reinterpret_cast<const uint4*>(d + i0);
-        const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-        for (int i = 0; i < 16; ++i) v[i] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+        w[0] = x.x;
+        w[1] = x.y;
+        w[2] = x.z;
+        w[3] = x.w;
       } else {
-        for (int i = 0; i < 16; ++i) v[i] = d[i0 + i];
+        for (int q = 0; q < 4; ++q)
+          w[q] = d[i0 + 4 * q] | d[i0 + 4 * q + 1] << 8 | d[i0 + 4 * q + 2] << 16 | static_cast<uint32_t>(d[i0 + 4 * q + 3]) << 24;
       }
-      for (int i = 0; i < 16; ++i)
-        if (v[i]) last = static_cast<int32_t>(i0 + i);
+      for (int q = 0; q < 4; ++q)
+        if (w[q]) last = 4 * q + (31 - __builtin_clz(w[q])) / 8;
     }
-    if (last >= 0) atomicMax(&best, last);
-    __syncthreads();
-    found = best;
-    __syncthreads();
+    const uint64_t any = __builtin_amdgcn_ballot_w64(last >= 0);
+    if (any) {
+      const int top = 63 - __builtin_clzll(any);
+      const int32_t l = __shfl(last, top);
+      found = hi - 1024 + 16 * top + l;
+    }
   }
-  if (threadIdx.x == 0) out[blockIdx.x] = (found < 0 || d[found] != 0x80) ? -1 : found;
+  if (lane == 0) out[b] = (found < 0 || d[found] != 0x80) ? -1 : found;
 }
 
 // =====================================================================================
@@ -2154,10 +2171,10 @@ hipError_t launch_locator(const uint8_t* erased, uint32_t npatterns, uint32_t W,
 hipError_t launch_coder_pad(const uint8_t* payload, uint64_t payload_stride, const uint32_t* lens, uint8_t* cw,
                             uint64_t cw_stride, uint32_t data_bytes, uint64_t nslices, hipStream_t stream) {
   if (data_bytes % 16) return hipErrorInvalidValue;
-  const uint64_t n = nslices * (data_bytes / 16);
-  if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(coder_pad_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream, payload,
-                     payload_stride, lens, cw, cw_stride, data_bytes, nslices);
+  if (nslices == 0 || data_bytes == 0) return hipSuccess;
+  if (nslices > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(coder_pad_kernel, dim3(static_cast<unsigned>(nslices)), dim3(payload ? 256 : 64), 0, stream,
+                     payload, payload_stride, lens, cw, cw_stride, data_bytes, nslices);
   return hipGetLastError();
 }
 
@@ -2196,9 +2213,11 @@ hipError_t launch_restride(const uint8_t* src, uint64_t src_block_stride, uint64
 hipError_t launch_coder_strip(const uint8_t* cw, uint64_t cw_stride, uint32_t data_bytes, uint64_t nslices,
                               int64_t* out, hipStream_t stream) {
   if (nslices == 0) return hipSuccess;
-  if (nslices > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(coder_strip_kernel, dim3(static_cast<unsigned>(nslices)), dim3(256), 0, stream, cw, cw_stride,
-                     data_bytes, out);
+  if (data_bytes % 16) return hipErrorInvalidValue;
+  const uint64_t groups = (nslices + 3) / 4;  // one wave per slice
+  if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(coder_strip_kernel, dim3(static_cast<unsigned>(groups)), dim3(256), 0, stream, cw, cw_stride,
+                     data_bytes, nslices, out);
   return hipGetLastError();
 }
 
