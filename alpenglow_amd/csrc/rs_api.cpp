@@ -175,6 +175,8 @@ struct ag_rs_ctx {
   DevBuf d_present;                         // coder batches: per-slice present masks
   PinBuf h_present;                         // their pinned host staging
   hipEvent_t present_ev = nullptr;          // recorded after its upload
+  PinBuf h_lens;                            // coder shred batches: pinned staging of the lengths
+  hipEvent_t lens_ev = nullptr;             // recorded after its upload
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
   static constexpr int kPipeBufs = 25;
   DevBuf pipe[kPipeBufs];                   // composed shredder scratch (ag_shredder_*_batch)
@@ -307,6 +309,11 @@ struct ag_rs_ctx {
       (void)hipEventDestroy(present_ev);
     }
     h_present.release();
+    if (lens_ev) {
+      (void)hipEventSynchronize(lens_ev);
+      (void)hipEventDestroy(lens_ev);
+    }
+    h_lens.release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -440,6 +447,27 @@ int encode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
   return AG_RS_OK;
 }
 
+// 32-point encodes of shards ending in a split tail chunk (S % 64 != 0, S even): one launch of
+// the TAIL transform reads and writes the tail in place (rs_xform.hpp tile_io_g), no restride
+int encode_tail32(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig, size_t ostride,
+                  uint8_t* rec, size_t rstride) {
+  const size_t cps = padded_shard(S) / 64;
+  ag::XformParams p{};
+  p.in = orig;
+  p.in_block_stride = ostride;
+  p.in_shard_stride = S;
+  p.out = rec;
+  p.out_block_stride = rstride;
+  p.out_shard_stride = S;
+  p.n_in = static_cast<uint32_t>(k);
+  p.n_out = static_cast<uint32_t>(m);
+  p.chunks_per_shard = static_cast<uint32_t>(cps);
+  p.total_columns = static_cast<uint64_t>(nblocks) * cps;
+  p.tail_bytes = static_cast<uint32_t>(S % 64);
+  c->last_encode_kernels |= ag::encode32_kernel(p);
+  return ag::launch_xform(ag::XformKind::kEncode32, p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
 int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
                   size_t ostride, uint8_t* rec, size_t rstride) {
   if (nblocks == 0) return AG_RS_OK;
@@ -448,6 +476,8 @@ int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
     if (odd_layout(orig, rec, ostride, rstride))
       return encode_restrided(c, k, m, S, S, 0, nblocks, orig, ostride, rec, rstride);
     const size_t full = S / 64 * 64, tail = S - full;
+    if (tail >= 16 && xform_points(k, m, Sp) == 32)  // (tail windows are 16 bytes of the tail itself)
+      return encode_tail32(c, k, m, S, nblocks, orig, ostride, rec, rstride);
     int st;
     if (full && (st = encode_cols(c, k, m, full, S, nblocks, orig, ostride, rec, rstride))) return st;
     if (tail && (st = encode_restrided(c, k, m, tail, S, full, nblocks, orig, ostride, rec, rstride))) return st;
@@ -538,6 +568,50 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   return st;
 }
 
+// The 32-point full-recovery reconstruct (decode class "transform") of shards ending in a split
+// tail chunk: xform8's TAIL variant restores the erased originals, tail included, in place.
+int decode_tail32(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
+                  const uint8_t* rec, size_t rstride, const uint8_t* opres, size_t npat) {
+  if (npat > 1) {
+    bool same = true;
+    for (size_t p = 1; p < npat && same; ++p) same = std::memcmp(opres, opres + p * k, k) == 0;
+    if (same) npat = 1;
+  }
+  std::vector<uint64_t> mask(npat);
+  const uint64_t kmask = (uint64_t{1} << k) - 1;  // k <= 32
+  bool any = false;
+  for (size_t p = 0; p < npat; ++p) {
+    mask[p] = ~pack_flags(opres + p * k, k) & kmask;
+    ++c->last_classes[mask[p] ? 1 : 0];
+    any = any || mask[p];
+  }
+  if (!any) return AG_RS_OK;
+  int st;
+  if (mask != c->mask_host) {
+    AG_HIP(hipStreamSynchronize(c->stream));  // a pending upload may still read mask_host
+    if ((st = c->d_mask.ensure(mask.size() * 8, c->stream))) return st;
+    c->mask_host = mask;
+    AG_HIP(hipMemcpyAsync(c->d_mask.ptr, c->mask_host.data(), mask.size() * 8, hipMemcpyHostToDevice, c->stream));
+  }
+  const size_t cps = padded_shard(S) / 64;
+  ag::XformParams p{};
+  p.in = rec;
+  p.in_block_stride = rstride;
+  p.in_shard_stride = S;
+  p.out = orig;
+  p.out_block_stride = ostride;
+  p.out_shard_stride = S;
+  p.out_mask = c->d_mask.as<uint64_t>();
+  p.pattern_per_block = npat > 1 ? 1u : 0u;
+  p.n_in = static_cast<uint32_t>(m);
+  p.n_out = static_cast<uint32_t>(k);
+  p.chunks_per_shard = static_cast<uint32_t>(cps);
+  p.total_columns = static_cast<uint64_t>(nblocks) * cps;
+  p.tail_bytes = static_cast<uint32_t>(S % 64);
+  p.out_low_half = std::all_of(mask.begin(), mask.end(), [](uint64_t w) { return (w >> 16) == 0; });
+  return ag::launch_xform(ag::XformKind::kDecode32, p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
 int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
                        const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
                        int mode) {
@@ -550,6 +624,13 @@ int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblock
     if (xform_points(k, m, Sp) || mc_chunk(k, m, Sp) || lowrate_chunk(k, m, Sp) || xw == 32 || xw == 64) {
       if (odd) return decode_restrided(c, k, m, S, S, 0, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
       const size_t full = S / 64 * 64, tail = S - full;
+      // every pattern restores from the full 32-point recovery set (or restores nothing): the
+      // TAIL transform decodes the whole shards, tail included, in place in one launch
+      if (tail >= 16 && xform_points(k, m, Sp) == 32 && m == 32 && mode == AG_RS_DECODE_ANY_K) {
+        bool all_full = true;
+        for (size_t p = 0; p < npat && all_full; ++p) all_full = count_flags(rpres + p * m, m) == m;
+        if (all_full) return decode_tail32(c, k, m, S, nblocks, orig, ostride, rec, rstride, opres, npat);
+      }
       int st;
       if (full && (st = decode_cols(c, k, m, full, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode)))
         return st;
@@ -2059,10 +2140,16 @@ int ag_rs_coder_shred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, const ui
   if (n == 0) return AG_RS_OK;
   int st = c->enter();
   if (st) return st;
-  // d_lens may still be read by a previous call's pad kernel
-  AG_HIP(hipStreamSynchronize(c->stream));
+  // the lengths go up through pinned staging on the context stream (ordered after a previous
+  // call's pad kernel, which may still read d_lens); the staging is rewritten once its last
+  // upload has completed -- no stream synchronisation before the call's work is enqueued
+  if (c->lens_ev) AG_HIP(hipEventSynchronize(c->lens_ev));
+  else AG_HIP(hipEventCreateWithFlags(&c->lens_ev, hipEventDisableTiming));
+  if ((st = c->h_lens.ensure(n * 4))) return st;
+  std::memcpy(c->h_lens.ptr, lens, n * 4);
   if ((st = c->d_lens.ensure(n * 4, c->stream))) return st;
-  AG_HIP(hipMemcpy(c->d_lens.ptr, lens, n * 4, hipMemcpyHostToDevice));
+  AG_HIP(hipMemcpyAsync(c->d_lens.ptr, c->h_lens.ptr, n * 4, hipMemcpyHostToDevice, c->stream));
+  AG_HIP(hipEventRecord(c->lens_ev, c->stream));
   if (ag::launch_coder_pad(payloads, payload_stride, c->d_lens.as<uint32_t>(), cw, cw_stride,
                            static_cast<uint32_t>(kDataShreds * S), n, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
@@ -2682,7 +2769,7 @@ int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, si
   }
   int64_t* strip = c->d_strip.as<int64_t>();
   if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(k * S), n, strip, c->stream) != hipSuccess ||
-      ag::launch_pipe_store_masks(few, strip, n, c->d_pipe_mask.as<uint64_t>(), c->stream) != hipSuccess)
+      ag::launch_pipe_store_masks(few, strip, d_present, 2, n, c->d_pipe_mask.as<uint64_t>(), c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   for (unsigned j = 0; j * 32 < m;) {  // the recovery chunks, two per launch (encode_cols' LowRate loop)
     ag::XformParams xp{};
@@ -2692,7 +2779,7 @@ int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, si
     xp.out = cw + (k + 32 * j) * S;
     xp.out_block_stride = cw_stride;
     xp.out_shard_stride = S;
-    xp.out_mask = c->d_pipe_mask.as<uint64_t>();  // all or none of a slice's coding shreds
+    xp.out_mask = c->d_pipe_mask.as<uint64_t>();  // the slice's absent coding shreds, all, or none
     xp.pattern_per_block = 1;
     xp.n_in = static_cast<uint32_t>(k);
     xp.chunks_per_shard = static_cast<uint32_t>(cps);
@@ -2752,7 +2839,7 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
     return AG_RS_ERR_DEVICE;
   int64_t* strip = c->d_strip.as<int64_t>();
   if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(k * S), n, strip, c->stream) != hipSuccess ||
-      ag::launch_pipe_store_masks(few, strip, n, c->d_pipe_mask.as<uint64_t>(), c->stream) != hipSuccess)
+      ag::launch_pipe_store_masks(few, strip, d_present, 1, n, c->d_pipe_mask.as<uint64_t>(), c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   ag::XformParams xp{};
   xp.in = cw;

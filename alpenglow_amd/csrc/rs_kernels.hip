@@ -31,7 +31,8 @@ using dev::static_for;
 
 // One 64-chunk tile per workgroup of NW waves.  N = 32: 64 KiB LDS, two workgroups per
 // CU; N = 64: 128 KiB LDS, one workgroup (8 waves) per CU.
-template <int NW, int DIN, int DOUT>
+// TAIL: shards end in the crate's split tail chunk (XformParams::tail_bytes, rs_xform.hpp).
+template <int NW, int DIN, int DOUT, bool TAIL = false>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const XformParams p) {
   __shared__ uint4 lds[4 * NW * 4 * kXfLanes];
   const int lane = threadIdx.x & 63;
@@ -43,7 +44,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
     if (__builtin_amdgcn_ballot_w64(m != 0) == 0) return;
   }
   Regs8 ra;
-  xf_load_raw(p, tile_io(p, tile, lane, p.in_block_stride), wave, ra);
+  xf_load_raw<TAIL>(p, tile_io<TAIL>(p, tile, lane, p.in_block_stride), wave, ra);
   // Store-mask words, fetched now so their latency hides under the data loads.  With
   // one pattern for the batch the word is wave-uniform (scalar load).
   uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
@@ -60,6 +61,10 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
     }
   }
 
+  if constexpr (TAIL) {
+    const TileIO in_io = tile_io<TAIL>(p, tile, lane, p.in_block_stride);
+    static_for<8>([&](auto T) { tail_fix_all<TAIL>(in_io, ra[decltype(T)::value]); });
+  }
   static_for<8>([&](auto T) {
     swap_halves(ra[decltype(T)::value]);
     dev::planes_from_raw(ra[decltype(T)::value]);
@@ -72,7 +77,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
 
   // pass C only where some lane of the wave stores one of its 8 shards (a decode restores
   // only the erased originals)
-  const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
+  const TileIO out_io = tile_io<TAIL>(p, tile, lane, p.out_block_stride);
   const uint32_t qall = qmask_all<8>(out_io, mask, 8 * wave, p.n_out);  // 32 bits: 8 shards x 4 pieces
   if (__builtin_amdgcn_ballot_w64(qall != 0) == 0) return;
   xf_pass_c<NW, DOUT>(wave, ra);
@@ -81,7 +86,8 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
     const uint32_t s = 8 * wave + t;  // wave-uniform
     const uint32_t q = (qall >> (4 * t)) & 15u;
     // a slot no lane stores skips its planes -> bytes conversion (a decode restores a subset)
-    if (s < p.n_out && __builtin_amdgcn_ballot_w64(q != 0) != 0) store_shard(p.out + s * p.out_shard_stride, out_io, q, ra[t]);
+    if (s < p.n_out && __builtin_amdgcn_ballot_w64(q != 0) != 0)
+      store_shard<false, TAIL>(p.out + s * p.out_shard_stride, out_io, q, ra[t]);
   });
 }
 
@@ -95,11 +101,11 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
 //   H0 slots p4 p0 | waves p1 p2 p3   FFT b0, store shards 2w, 2w + 1
 // One tile (flags zeroed by the caller, every wave of the 512-thread workgroup calls it):
 // xform8_kernel's grid and the per-call server's jobs (latency_server_kernel).
-template <int DIN, int DOUT, bool HALF = false>
+template <int DIN, int DOUT, bool HALF = false, bool TAIL = false>
 __device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile, uint4* lds, X8Flags* fl) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const TileIO io = tile_io(p, tile, lane, p.in_block_stride);
+  const TileIO io = tile_io<TAIL>(p, tile, lane, p.in_block_stride);
   Regs4 r;
   // a tile past the batch's last column (one slice per call: 16 of 64 columns) loads only
   // its existing pieces -- over PCIe from mapped host memory, the idle re-reads were 3/4 of
@@ -113,7 +119,7 @@ __device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile,
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
         uint4 x = make_uint4(0, 0, 0, 0);
-        if (whole || ((io.valid >> q) & 1)) x = ld_piece(base + io.off[q]);
+        if (whole || ((io.valid >> q) & 1)) x = ld_piece_io<TAIL>(base, io, q);
         r[t][4 * q] = x.x;
         r[t][4 * q + 1] = x.y;
         r[t][4 * q + 2] = x.z;
@@ -124,6 +130,7 @@ __device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile,
     }
   });
   static_for<4>([&](auto T) {
+    tail_fix_all<TAIL>(io, r[decltype(T)::value]);
     swap_halves(r[decltype(T)::value]);
     dev::planes_from_raw(r[decltype(T)::value]);
   });
@@ -148,7 +155,7 @@ __device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile,
     x8_swap<1, 1, 5, 0x5>(wave, lane, lds, fl, r);
     x8_layer_lay<H1, 1, DOUT, 0x5>(wave, r);
     x8_swap<1, 0, 6, 0x5>(wave, lane, lds, fl, r);
-    const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
+    const TileIO out_io = tile_io<TAIL>(p, tile, lane, p.out_block_stride);
     uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
     if (p.out_mask) {
       if (!p.pattern_per_block) {
@@ -165,7 +172,7 @@ __device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile,
     static_for<2>([&](auto U) {
       constexpr int t = 2 * decltype(U)::value;
       const uint32_t sh = 2 * wave + (t >> 1);  // H0 position of live slot t
-      if (sh < p.n_out) store_shard(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * (t >> 1))) & 15u, r[t]);
+      if (sh < p.n_out) store_shard<false, TAIL>(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * (t >> 1))) & 15u, r[t]);
     });
     return;
   }
@@ -178,7 +185,7 @@ __device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile,
   x8_layer<1, 1, false, DOUT>(wave, r);
   x8_swap<0, 0, 6>(wave, lane, lds, fl, r);
   // store masks fetched only now: live across the transform they cost registers (spills)
-  const TileIO out_io = tile_io(p, tile, lane, p.out_block_stride);
+  const TileIO out_io = tile_io<TAIL>(p, tile, lane, p.out_block_stride);
   uint64_t mask[4] = {~0ull, ~0ull, ~0ull, ~0ull};
   if (p.out_mask) {
     if (!p.pattern_per_block) {
@@ -208,17 +215,17 @@ __device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile,
     constexpr int t = decltype(T)::value;
     const uint32_t sh = 4 * wave + t;  // wave-uniform
     if (((need >> t) & 1u) && sh < p.n_out)
-      store_shard(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, r[t]);
+      store_shard<false, TAIL>(p.out + sh * p.out_shard_stride, out_io, (qall >> (4 * t)) & 15u, r[t]);
   });
 }
 
-template <int DIN, int DOUT, bool HALF = false>
+template <int DIN, int DOUT, bool HALF = false, bool TAIL = false>
 __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
   __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
   __shared__ X8Flags flags;
   if (threadIdx.x < 16) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x] = 0;
   __syncthreads();
-  xform8_tile<DIN, DOUT, HALF>(p, dev::xcd_tile(blockIdx.x, gridDim.x), lds, &flags);
+  xform8_tile<DIN, DOUT, HALF, TAIL>(p, dev::xcd_tile(blockIdx.x, gridDim.x), lds, &flags);
 }
 
 // =====================================================================================
@@ -1112,13 +1119,19 @@ __global__ __launch_bounds__(64) void decode_rows_kernel(const uint64_t* __restr
                                                          uint32_t poly) {
   const uint64_t pat = blockIdx.x;
   const uint32_t x = threadIdx.x;
-  if (x >= W) return;
   const uint64_t e = emask[pat], in = pmask[2 * pat], out = pmask[2 * pat + 1];
+  // W <= 64 = the wave: lane x holds log[x], and log[x ^ y] is lane x ^ y's (a lane shuffle
+  // per erased position instead of a dependent table load)
+  const uint32_t lx = x < W ? log_t[x] : 0u;
+  uint32_t acc = 0;
+  for (uint64_t em = W >= 64 ? e : e & ((uint64_t{1} << W) - 1); em; em &= em - 1) {  // erased positions < W
+    const uint32_t y = static_cast<uint32_t>(__builtin_ctzll(em));
+    const uint32_t ly = static_cast<uint32_t>(__shfl_xor(static_cast<int>(lx), static_cast<int>(y)));
+    if (y != x) acc = dev::add_mod(acc, ly);
+  }
+  if (x >= W) return;
   const bool is_in = (in >> x) & 1, is_out = (out >> x) & 1;
   if (!is_in && !is_out) return;
-  uint32_t acc = 0;
-  for (uint32_t y = 0; y < W; ++y)
-    if (((e >> y) & 1) && y != x) acc = dev::add_mod(acc, log_t[x ^ y]);
   const uint16_t lg = is_in ? static_cast<uint16_t>(acc) : static_cast<uint16_t>(65535 - acc);
   if (poly) {
     rows[pat * W + x] = dev::to_poly(exp_t[lg]);  // exp[lg] = the constant (lg < 65535)
@@ -2116,6 +2129,13 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
     // reconstructs (half the exposed arithmetic per wave: -8% time), with the pruned FFT when
     // every restored original is < 16.
     case XformKind::kEncode32:
+      if (p.tail_bytes) {  // shards ending in a split tail chunk: the TAIL kernels, same dispatch
+        if (encode32_kernel(p) == kEkXform8)
+          hipLaunchKernelGGL((xform8_kernel<32, 0, false, true>), grid, dim3(512), 0, stream, p);
+        else
+          hipLaunchKernelGGL((xform_kernel<4, 32, 0, true>), grid, dim3(256), 0, stream, p);
+        break;
+      }
       // batches of fewer tiles than CUs (a single slice per call: one tile) are latency-bound:
       // xform8 spreads a tile's transform over 8 waves of 4 slots, half xform<4>'s instruction
       // stream per wave.  Shards of 8 and 16 KiB (2 or 4 tiles per shard) also take xform8:
@@ -2131,6 +2151,13 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
     case XformKind::kDecode32:
       // (xform<4> with the same skipped conversions: random-16 reconstruct 5.37 TB/s against
       // xform8's 5.43-5.51, one box)
+      if (p.tail_bytes) {
+        if (p.out_low_half)
+          hipLaunchKernelGGL((xform8_kernel<0, 32, true, true>), grid, dim3(512), 0, stream, p);
+        else
+          hipLaunchKernelGGL((xform8_kernel<0, 32, false, true>), grid, dim3(512), 0, stream, p);
+        break;
+      }
       if (p.out_low_half)
         hipLaunchKernelGGL((xform8_kernel<0, 32, true>), grid, dim3(512), 0, stream, p);
       else

@@ -26,6 +26,9 @@ struct XformParams {
   uint32_t out_low_half;          // decode: every stored shard is < N / 2 (pruned FFT)
   uint32_t skip_idle;             // xform<4> with per-block masks: tiles whose blocks all have
                                   // mask 0 exit before loading (re-encodes of a few slices)
+  uint32_t tail_bytes;            // T = S mod 64 (even), TAIL kernels: chunk chunks_per_shard - 1 of
+                                  // every shard is the crate's split tail (T/2 low bytes, then T/2
+                                  // high bytes), read and written in place
 };
 
 enum class XformKind { kEncode32, kDecode32, kEncode64, kDecode64 };

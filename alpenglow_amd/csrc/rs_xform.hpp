@@ -176,13 +176,40 @@ struct TileIO {
   uint64_t off[4];  // byte offset of this lane's 16-byte piece of shard 0, per instruction q
   uint64_t blk[4];  // block of chunk q (for the per-block store mask)
   uint32_t valid;   // bit q: chunk q exists (idle pieces re-read the last chunk, never store)
+  uint32_t tailq;   // bit q: chunk q is its shard's tail chunk (TAIL kernels)
+  uint32_t tlen;    // bytes of this lane's run in a tail chunk (0..16)
+  uint32_t tsh;     // its run's start within the lane's 16-byte tail window (off[q] = the window)
+  uint32_t tlen_h;  // h = T / 2 (uniform)
 };
+// Tail chunks (shard bytes S with T = S mod 64 != 0): the crate stores the last T bytes as T/2
+// low bytes then T/2 high bytes, i.e. a 64-byte chunk whose symbols h..31
+// (h = T/2) are zero.  The four quarter lanes of a chunk (low bytes of symbols 0-15 / 16-31,
+// high bytes of 0-15 / 16-31) own the runs [0, 16) [16, h) [h, h + 16) [h + 16, T) of the
+// tail (for h >= 16; for 8 <= h < 16: [0, h) and [h, T), quarters 1 and 3 empty).  Each lane
+// moves one whole 16-byte window of the tail that contains its run -- [0, 16), [h - 16, h),
+// [h, h + 16), [T - 16, T); for h < 16: [0, 16) and [T - 16, T) -- so tail pieces load and
+// store with the same instructions as every other piece (T >= 16: every window lies inside the
+// tail).  A loaded window is shifted down to its run (tail_fix_all); a stored window is
+// completed with the neighbouring run's bytes from the partner lane (tail_window), so the
+// bytes two lanes both write are equal.
 __device__ __forceinline__ TileIO tile_io_g(uint64_t total_columns, uint32_t chunks_per_shard, uint64_t tile, int lane,
-                                           uint64_t block_stride) {
+                                           uint64_t block_stride, uint32_t tail = 0) {
   TileIO io;
   io.valid = 0;
+  io.tailq = 0;
   const uint32_t quarter = ((lane >> 5) << 1) | (lane & 1);
-  // the tile's first chunk once per wave (scalar division); lanes add < 64 chunks to its
+  const uint32_t h = tail / 2;
+  io.tlen_h = h;
+  uint32_t win;  // window start in the tail
+  if (h >= 16) {
+    win = quarter == 0 ? 0 : quarter == 1 ? h - 16 : quarter == 2 ? h : tail - 16;
+    io.tsh = (quarter & 1) ? 32 - h : 0;
+    io.tlen = (quarter & 1) ? h - 16 : 16;
+  } else {
+    win = quarter < 2 ? 0 : tail - 16;
+    io.tsh = quarter == 2 ? 16 - h : 0;
+    io.tlen = (quarter & 1) ? 0 : h;
+  }  // the tile's first chunk once per wave (scalar division); lanes add < 64 chunks to its
   // in-block index, so a lane crosses at most one block boundary when C >= 64 (the 64-bit
   // division per lane and piece cost ~10 % of a reconstruct's VALU)
   const uint32_t C = chunks_per_shard;
@@ -204,13 +231,133 @@ __device__ __forceinline__ TileIO tile_io_g(uint64_t total_columns, uint32_t chu
       rem = c - d * C;
     }
     io.blk[q] = b0 + d;
-    io.off[q] = base + d * block_stride + static_cast<uint64_t>(rem) * 64 + 16 * quarter;
+    const bool tq = tail != 0 && rem == C - 1;
+    io.off[q] = base + d * block_stride + static_cast<uint64_t>(rem) * 64 + (tq ? win : 16 * quarter);
     io.valid |= ok ? (1u << q) : 0u;
+    io.tailq |= tq ? (1u << q) : 0u;
   });
   return io;
 }
+template <bool TAIL = false>
 __device__ __forceinline__ TileIO tile_io(const XformParams& p, uint64_t tile, int lane, uint64_t block_stride) {
-  return tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, block_stride);
+  return tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, block_stride, TAIL ? p.tail_bytes : 0u);
+}
+
+// 128-bit shifts of v[0..3] by a byte count (0..16) as two 64-bit halves
+__device__ __forceinline__ void shr128(uint32_t* v, uint32_t bytes) {
+  const uint32_t sh = 8 * bytes;
+  uint64_t lo = v[0] | static_cast<uint64_t>(v[1]) << 32, hi = v[2] | static_cast<uint64_t>(v[3]) << 32;
+  if (sh >= 64) {
+    lo = sh >= 128 ? 0 : hi >> (sh - 64);
+    hi = 0;
+  } else if (sh != 0) {
+    lo = (lo >> sh) | (hi << (64 - sh));
+    hi >>= sh;
+  }
+  v[0] = static_cast<uint32_t>(lo);
+  v[1] = static_cast<uint32_t>(lo >> 32);
+  v[2] = static_cast<uint32_t>(hi);
+  v[3] = static_cast<uint32_t>(hi >> 32);
+}
+__device__ __forceinline__ void shl128(uint32_t* v, uint32_t bytes) {
+  const uint32_t sh = 8 * bytes;
+  uint64_t lo = v[0] | static_cast<uint64_t>(v[1]) << 32, hi = v[2] | static_cast<uint64_t>(v[3]) << 32;
+  if (sh >= 64) {
+    hi = sh >= 128 ? 0 : lo << (sh - 64);
+    lo = 0;
+  } else if (sh != 0) {
+    hi = (hi << sh) | (lo >> (64 - sh));
+    lo <<= sh;
+  }
+  v[0] = static_cast<uint32_t>(lo);
+  v[1] = static_cast<uint32_t>(lo >> 32);
+  v[2] = static_cast<uint32_t>(hi);
+  v[3] = static_cast<uint32_t>(hi >> 32);
+}
+// keep the low `len` bytes (0..16)
+__device__ __forceinline__ void keep128(uint32_t* v, uint32_t len) {
+  static_for<4>([&](auto K) {
+    constexpr int k = decltype(K)::value;
+    const int keep = static_cast<int>(len) - 4 * k;
+    v[k] = keep >= 4 ? v[k] : keep <= 0 ? 0u : (v[k] & ((1u << (8 * keep)) - 1));
+  });
+}
+// piece q of shard `base` (a tail piece is its lane's whole window: tail_fix_all after the
+// tile's loads, so no load waits on the others)
+template <bool TAIL>
+__device__ __forceinline__ uint4 ld_piece_io(const uint8_t* base, const TileIO& io, int q) {
+  return ld_piece(base + io.off[q]);
+}
+// the loaded tail windows of one slot (registers 4 q .. 4 q + 3 = piece q) -> their runs at
+// byte 0, zeros above (the transform then sees symbols h..31 as zero).  Shift and length
+// depend only on h (uniform) and the lane's quarter, so the shifts take scalar amounts.
+template <bool TAIL>
+__device__ __forceinline__ void tail_fix_all(const TileIO& io, uint32_t* v) {
+  if constexpr (TAIL) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t h = io.tlen_h;
+    static_for<4>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      if (__builtin_amdgcn_ballot_w64((io.tailq >> q) & 1) != 0) {  // wave-uniform
+        uint32_t* x = v + 4 * q;
+        uint32_t t[4] = {x[0], x[1], x[2], x[3]};
+        const bool tl = (io.tailq >> q) & 1;
+        if (h >= 16) {  // quarters 1 / 3: window [h - 16, h) / [T - 16, T), run at 32 - h
+          shr128(t, 32 - h);
+          keep128(t, h - 16);
+          if (tl && (lane & 1)) static_for<4>([&](auto K) { x[decltype(K)::value] = t[decltype(K)::value]; });
+        } else {  // quarter 0: run [0, h) at 0; quarter 2: window [T - 16, T), run at 16 - h; 1 / 3 empty
+          shr128(t, 16 - h);
+          keep128(t, h);
+          uint32_t u[4] = {x[0], x[1], x[2], x[3]};
+          keep128(u, h);
+          if (tl) {
+            static_for<4>([&](auto K) {
+              constexpr int k = decltype(K)::value;
+              x[k] = (lane & 1) ? 0u : lane >= 32 ? t[k] : u[k];
+            });
+          }
+        }
+      }
+    });
+  }
+}
+// The window a tail lane stores, from its run (bytes 0..tlen-1 of v, zeros above) and the
+// partner run's bytes: quarters 1 / 3 take quarter 0 / 2 (the lane below, quad permute);
+// with h < 16 quarters 0 / 2 take each other (lanes l, l + 32).  Wave-wide: every lane runs
+// the exchanges; the caller stores the result on tail lanes only.  h is uniform.
+__device__ __forceinline__ void tail_window(uint32_t* v, int lane, uint32_t h) {
+  if (h >= 16) {
+    uint32_t lo[4];  // the lane below's run (quarter 0 / 2 of the chunk)
+    static_for<4>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      lo[k] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v[k]), 0xA0 /* quad_perm 0,0,2,2 */, 0xF,
+                                                             0xF, false));
+    });
+    if (lane & 1) {  // window [h - 16, h) = lo[h - 16, 16) ++ own[0, h - 16)
+      shr128(lo, h - 16);
+      shl128(v, 32 - h);
+      static_for<4>([&](auto K) { v[decltype(K)::value] |= lo[decltype(K)::value]; });
+    }
+  } else {
+    uint32_t pr[4];  // the partner half's run: quarter 0 <-> 2
+    static_for<4>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      pr[k] = __builtin_amdgcn_permlane32_swap(v[k], v[k], false, false)[0];
+    });
+    if (lane >= 32) {  // quarter 2: window [T - 16, T) = q0[2h - 16, h) ++ own[0, h)
+      shr128(pr, 2 * h - 16);
+      shl128(v, 16 - h);
+    } else {  // quarter 0: window [0, 16) = own[0, h) ++ q2[0, 16 - h)
+      shl128(pr, h);
+    }
+    static_for<4>([&](auto K) { v[decltype(K)::value] |= pr[decltype(K)::value]; });
+  }
+}
+template <bool TAIL>
+__device__ __forceinline__ void st_piece_io(uint8_t* base, const TileIO& io, int q, uint32_t a, uint32_t b, uint32_t c,
+                                            uint32_t d) {
+  st_piece(base + io.off[q], a, b, c, d);
 }
 
 // lanes l and l + 32 exchange register halves (see TileIO); an involution
@@ -224,6 +371,7 @@ __device__ __forceinline__ void swap_halves(uint32_t* v) {
 }
 
 // Raw 16-byte pieces of this wave's pass-A shards 8*wave + t (before swap / transpose).
+template <bool TAIL = false>
 __device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& io, int wave, Regs8& raw) {
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
@@ -232,7 +380,7 @@ __device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& 
       const uint8_t* base = p.in + s * p.in_shard_stride;
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(base + io.off[q]);
+        const uint4 x = ld_piece_io<TAIL>(base, io, q);
         raw[t][4 * q] = x.x;
         raw[t][4 * q + 1] = x.y;
         raw[t][4 * q + 2] = x.z;
@@ -246,7 +394,7 @@ __device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& 
 
 // Planes -> bytes -> lane-linear pieces, stored where the input pieces were read.  ACC: XOR
 // into the bytes already there (a partial result stored by an earlier pass).
-template <bool ACC = false>
+template <bool ACC = false, bool TAIL = false>
 __device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const TileIO& io, uint32_t qmask,
                                             const uint32_t* planes) {
   uint32_t v[16];
@@ -257,14 +405,33 @@ __device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const Ti
   dev::transpose8(v);
   dev::transpose8(v + 8);
   swap_halves(v);
+  if constexpr (TAIL) {
+    // tail pieces: the run (symbols >= h are zero: the inputs there were zero) completed to
+    // the lane's window; lanes with an empty run (tlen 0) store nothing
+    const int lane = threadIdx.x & 63;
+    static_for<4>([&](auto Q) {
+      constexpr int q = decltype(Q)::value;
+      if (__builtin_amdgcn_ballot_w64((io.tailq >> q) & 1) != 0) {  // wave-uniform
+        // (bytes past the run are zero: outputs at symbols >= h come from zero inputs)
+        uint32_t w[4] = {v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]};
+        tail_window(w, lane, io.tlen_h);
+        if ((io.tailq >> q) & 1) {
+          static_for<4>([&](auto K) { v[4 * q + decltype(K)::value] = w[decltype(K)::value]; });
+          if (io.tlen == 0) qmask &= ~(1u << q);
+        }
+      }
+    });
+  }
   static_for<4>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
     if (qmask & (1u << q)) {
       if constexpr (ACC) {
-        const uint4 o = ld_piece(base + io.off[q]);
-        st_piece(base + io.off[q], v[4 * q] ^ o.x, v[4 * q + 1] ^ o.y, v[4 * q + 2] ^ o.z, v[4 * q + 3] ^ o.w);
+        static_assert(!TAIL, "accumulating stores of tail windows are not supported");
+        const uint4 x = ld_piece_io<TAIL>(base, io, q);
+        uint32_t o[4] = {x.x, x.y, x.z, x.w};
+        st_piece_io<TAIL>(base, io, q, v[4 * q] ^ o[0], v[4 * q + 1] ^ o[1], v[4 * q + 2] ^ o[2], v[4 * q + 3] ^ o[3]);
       } else {
-        st_piece(base + io.off[q], v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+        st_piece_io<TAIL>(base, io, q, v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
       }
     }
   });

@@ -201,11 +201,21 @@ __global__ __launch_bounds__(256) void pipe_patterns128_kernel(const uint64_t* _
 }
 
 __global__ __launch_bounds__(256) void pipe_store_mask_kernel(const uint8_t* __restrict__ few,
-                                                              const int64_t* __restrict__ strip, uint64_t n,
-                                                              uint64_t* __restrict__ mask) {
+                                                              const int64_t* __restrict__ strip,
+                                                              const uint64_t* __restrict__ present, uint32_t wps,
+                                                              uint64_t n, uint64_t* __restrict__ mask) {
   const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (s >= n) return;
-  mask[s] = (!few[s] && strip[s] >= 0) ? ~uint64_t{0} : uint64_t{0};  // few 2: restored by the decode
+  uint64_t m = 0;
+  if (!few[s] && strip[s] >= 0) {  // few 2: restored by the decode
+    // exactly k kept shreds fix the codeword: the received coding shreds are its own, so only
+    // the absent ones are written; with surplus shreds every coding shred is re-encoded
+    const uint64_t p0 = present[wps * s], p1 = wps == 2 ? present[wps * s + 1] : 0;
+    const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(p0) + __builtin_popcountll(p1));
+    const uint64_t coding = (p0 >> 32) | (p1 << 32);  // coding shreds 0..63 present
+    m = cnt == kPipeData ? ~coding : ~uint64_t{0};
+  }
+  mask[s] = m;
 }
 
 }  // namespace
@@ -271,10 +281,11 @@ hipError_t launch_pipe_patterns128(const uint64_t* present, uint64_t nslices, ui
   return hipGetLastError();
 }
 
-hipError_t launch_pipe_store_masks(const uint8_t* few, const int64_t* strip, uint64_t nslices, uint64_t* mask,
-                                   hipStream_t stream) {
+hipError_t launch_pipe_store_masks(const uint8_t* few, const int64_t* strip, const uint64_t* present, uint32_t wps,
+                                   uint64_t nslices, uint64_t* mask, hipStream_t stream) {
   if (nslices == 0) return hipSuccess;
-  hipLaunchKernelGGL(pipe_store_mask_kernel, grid256(nslices), dim3(256), 0, stream, few, strip, nslices, mask);
+  hipLaunchKernelGGL(pipe_store_mask_kernel, grid256(nslices), dim3(256), 0, stream, few, strip, present, wps, nslices,
+                     mask);
   return hipGetLastError();
 }
 

@@ -105,7 +105,10 @@ hipError_t launch_pipe_patterns128(const uint64_t* present, uint64_t nslices, ui
 // mask[s] = ~0 (store every coding shard of the re-encode) when the slice decoded and its
 // padding stripped (few[s] == 0 and strip[s] >= 0), else 0 (the coding shreds stay as they
 // are, like the reference's early returns; few[s] == 2: the decode restored them).
-hipError_t launch_pipe_store_masks(const uint8_t* few, const int64_t* strip, uint64_t nslices, uint64_t* mask,
+// present: the kept-shred words (wps per slice, launch_pipe_patterns / 128): a slice with
+// exactly 32 kept shreds re-encodes only its absent coding shreds (bit j: coding shred j).
+hipError_t launch_pipe_store_masks(const uint8_t* few, const int64_t* strip, const uint64_t* present, uint32_t wps,
+                                   uint64_t nslices, uint64_t* mask,
                                    hipStream_t stream);
 
 }  // namespace ag

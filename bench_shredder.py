@@ -35,6 +35,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--arrived", type=int, default=32, help="datagrams received per slice before deshred (32..64)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -132,8 +133,89 @@ def main():
         "deshred_slices_per_s": n * steps / t_de,
         "verify": {"roundtrip_restores_everything": ok, "datagrams_match_oracle": bool(spot)},
     }
+    if not args.no_cpu_baseline:
+        line["cpu_baseline"] = _cpu_baseline(args, data, slots, sidx, last, cw, pkts, D, S)
     print(json.dumps(line), flush=True)
     ctx.close()
+
+
+def _host_cpus():
+    n = len(os.sched_getaffinity(0))
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
+def _cpu_baseline(args, data, slots, sidx, last, cw, pkts, D, S):
+    """The composed RegularShredder on this host's CPU (oracle/shredder_cpu.c, a port: the
+    crate's Avx2 RS engine restated, OpenSSL's SHA-256 and Ed25519), on a bounded sample of
+    the same slices: shred (RS + Merkle tree + signature + proofs), the reference bench's
+    deshred from the 32 coding shreds (RS decode + re-encode + Merkle check + parse + proofs;
+    benches/shredder.rs:19-61) and the receive-side validation the device deshred also does
+    (each shred's root from its path, one signature verified per slice).  1 thread and every
+    host CPU; its coding shreds and signatures are compared with the device's."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import numpy as np
+
+    import ed25519_oracle as ed
+    import shredder_cpu as sc
+
+    seed = bytes(range(32))
+    pk = ed.secret_to_public(seed)
+    nall = _host_cpus()
+    n = min(data.shape[0], max(64, nall * 64))
+    framed = np.zeros((n, 32 * S), np.uint8)
+    framed[:, 1:9] = np.frombuffer(int(D).to_bytes(8, "little"), np.uint8)
+    framed[:, 9:9 + D] = data[:n, :D].cpu().numpy()
+    lens = np.full(n, D + 9, np.uint32)
+    sl, si, ls = slots[:n].cpu().numpy(), sidx[:n].cpu().numpy(), last[:n].cpu().numpy()
+
+    def rate(what, threads, cnt):
+        t = time.perf_counter()
+        st, *_ = sc.run(what, threads, framed[:cnt], lens[:cnt], sl[:cnt], si[:cnt], ls[:cnt], seed, pk)
+        dt = time.perf_counter() - t
+        if st:
+            raise RuntimeError(f"shredder_cpu failed ({st})")
+        return cnt / dt
+
+    out = {"unit": "slices/s", "kind": "port", "cores": nall, "cpu": _cpu_model()}
+    # device comparison: the first 8 slices' coding shreds and slice signatures
+    st, coding, _, sigs = sc.run(sc.SHRED, 1, framed[:8], lens[:8], sl[:8], si[:8], ls[:8], seed, pk, outputs=True)
+    gc = cw[:8, 32 * S:64 * S].cpu().numpy().reshape(8, 32, S)
+    gsig = pkts.view(-1, 64, pkts.shape[1])[:8, 0, 37 + S:37 + S + 64].cpu().numpy()
+    out["gpu_matches_cpu"] = bool(st == 0 and np.array_equal(coding, gc) and np.array_equal(sigs, gsig))
+    for threads in (1, nall):
+        cnt = min(n, 64 * threads)
+        r_sh = rate(sc.SHRED, threads, cnt)
+        r_bench = rate(sc.SHRED | sc.DESHRED, threads, cnt)
+        r_all = rate(sc.SHRED | sc.DESHRED | sc.RECEIVE, threads, cnt)
+        t_sh, t_de, t_rx = 1 / r_sh, 1 / r_bench - 1 / r_sh, 1 / r_all - 1 / r_bench
+        out[f"threads_{threads}"] = {
+            "slices": cnt, "threads": threads,
+            "shred_slices_per_s": r_sh, "deshred_slices_per_s": 1 / t_de,
+            "receive_slices_per_s": 1 / t_rx,
+            "reference_bench_roundtrip_slices_per_s": r_bench,
+            "device_shape_roundtrip_slices_per_s": r_all,
+        }
+    out["value"] = out[f"threads_{nall}"]["device_shape_roundtrip_slices_per_s"]
+    out["sample"] = (f"{n} of the same maximum slices (framed 32 767-byte payloads), shred + receive validation + "
+                     f"deshred from the 32 coding shreds, one slice per task; RS by oracle/rs_cpu_avx2.c, SHA-256 "
+                     f"and Ed25519 by OpenSSL libcrypto")
+    return out
+
+
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 if __name__ == "__main__":

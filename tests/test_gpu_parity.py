@@ -1082,6 +1082,39 @@ def test_tail_chunk_encode_decode(ctx, dev, k, m, S):
             assert np.array_equal(got, blocks), (per_block, mode)
 
 
+@pytest.mark.parametrize("S,n", [(1000, 1040), (1022, 1030), (62, 16400), (2, 40), (66, 8200), (126, 9000),
+                                 (1000, 9), (574, 2000), (84, 300), (48, 6000), (110, 500)])
+@pytest.mark.parametrize("k", [32, 25])
+def test_tail_chunks_in_kernel(ctx, dev, S, n, k):
+    """32-point geometries whose shards end in the crate's split tail chunk (S mod 64 != 0):
+    encode and the full-recovery reconstruct read and write the tail in place (the TAIL
+    transforms: xform<4> at >= 256 tiles, xform8 below; rs_xform.hpp tile_io_g), no restride
+    (tails under 16 bytes still restride).
+    Tails of T = 2..62 bytes (odd and even halves), against the C oracle and the originals;
+    per-block random erasures (and erasures confined to shards 0..15: the pruned FFT)."""
+    m = 32
+    blocks = _blocks(7300 + S + k, n, k, S)
+    rec = gpu_encode(ctx, dev, blocks, m)
+    kern = rs.last_encode_kernels(ctx)
+    if S % 64 >= 16:  # tails under 16 bytes keep the restride (a 16-byte tail window would leave the tail)
+        assert "restride" not in kern and kern <= {"xform4", "xform8"}, kern
+    assert np.array_equal(rec, ro_c.encode_blocks(blocks, m, threads=8))
+    rng = random.Random(S * 7 + n + k)
+    for low in (False, True):
+        op = []
+        for b in range(n):
+            lost = set(rng.sample(range(min(k, 16) if low else k), rng.randint(1, min(k, 16) if low else k)))
+            op += [0 if i in lost else 1 for i in range(k)]
+        d_o = blocks.copy()
+        for b in range(n):
+            for i in range(k):
+                if not op[b * k + i]:
+                    d_o[b, i] = 0x5C
+        got = gpu_decode(ctx, dev, d_o, rec, op, [1] * (m * n), rs.DECODE_ANY_K)
+        assert np.array_equal(got, blocks), low
+        assert set(rs.last_decode_classes(ctx)) <= {"transform", "none"}
+
+
 @pytest.mark.parametrize("k,m,S", [(32, 64, 1024), (32, 33, 2048), (20, 40, 128), (32, 64, 4096), (25, 33, 192)])
 def test_lowrate_window_decode(ctx, dev, k, m, S):
     """LowRate (CodingOnly 32:64, PETS 32:33, shredder.rs:362-446) with mixed losses and no
