@@ -103,30 +103,40 @@ static size_t commitment(uint64_t slot, uint64_t slice_index, int is_last, const
 /* ---- per-thread state ---- */
 typedef struct {
   EVP_PKEY *sk, *pk;
-  EVP_MD_CTX *md;
+  EVP_MD_CTX *md, *sign_tmpl, *verify_tmpl;
   uint8_t cw[TOTAL * S_MAX];            /* 32 data then 32 coding shards */
   uint8_t nodes[NODES][32];
   uint8_t proofs[TOTAL][HEIGHT][32];    /* the output shreds' Merkle paths */
 } worker_t;
 
+/* OpenSSL 3 fetches the signature implementation on every EVP_Digest{Sign,Verify}Init under a
+ * process-wide lock (16 threads signed slower than one); each worker initialises one signing
+ * and one verifying context once and copies them per call. */
 static int worker_init(worker_t *w, const uint8_t seed[32], const uint8_t pk[32]) {
   w->sk = EVP_PKEY_new_raw_private_key(EVP_PKEY_ED25519, NULL, seed, 32);
   w->pk = EVP_PKEY_new_raw_public_key(EVP_PKEY_ED25519, NULL, pk, 32);
   w->md = EVP_MD_CTX_new();
-  return w->sk && w->pk && w->md ? 0 : -1;
+  w->sign_tmpl = EVP_MD_CTX_new();
+  w->verify_tmpl = EVP_MD_CTX_new();
+  if (!w->sk || !w->pk || !w->md || !w->sign_tmpl || !w->verify_tmpl) return -1;
+  if (EVP_DigestSignInit(w->sign_tmpl, NULL, NULL, NULL, w->sk) != 1) return -1;
+  if (EVP_DigestVerifyInit(w->verify_tmpl, NULL, NULL, NULL, w->pk) != 1) return -1;
+  return 0;
 }
 static void worker_free(worker_t *w) {
   EVP_PKEY_free(w->sk);
   EVP_PKEY_free(w->pk);
   EVP_MD_CTX_free(w->md);
+  EVP_MD_CTX_free(w->sign_tmpl);
+  EVP_MD_CTX_free(w->verify_tmpl);
 }
 static int ed_sign(worker_t *w, const uint8_t *msg, size_t len, uint8_t sig[64]) {
   size_t sl = 64;
-  if (EVP_DigestSignInit(w->md, NULL, NULL, NULL, w->sk) != 1) return -1;
+  if (EVP_MD_CTX_copy_ex(w->md, w->sign_tmpl) != 1) return -1;
   return EVP_DigestSign(w->md, sig, &sl, msg, len) == 1 && sl == 64 ? 0 : -1;
 }
 static int ed_verify(worker_t *w, const uint8_t *msg, size_t len, const uint8_t sig[64]) {
-  if (EVP_DigestVerifyInit(w->md, NULL, NULL, NULL, w->pk) != 1) return -1;
+  if (EVP_MD_CTX_copy_ex(w->md, w->verify_tmpl) != 1) return -1;
   return EVP_DigestVerify(w->md, sig, 64, msg, len) == 1 ? 0 : -1;
 }
 
