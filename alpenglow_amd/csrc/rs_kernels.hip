@@ -915,7 +915,27 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
     return is_rec ? p.rec + (g - rpos) * p.rec_shard_stride + blk * p.rec_block_stride + col * 64
                   : p.orig + (g - opos) * p.orig_shard_stride + blk * p.orig_block_stride + col * 64;
   };
-  // 2. packed input products: item i on row group i & 3 of slot (i >> 2) & 1 of wave i >> 3
+  // 2. packed input products: item i on row group i & 3 of slot (i >> 2) & 1 of wave i >> 3.
+  // Both items' loads are issued before either product (one HBM round trip per wave, not two)
+  uint32_t v[2][16];
+  static_for<2>([&](auto U) {
+    constexpr int u = decltype(U)::value;
+    const uint32_t i = wave * 8 + u * 4 + row;
+    if (i < nin) {
+      const uint32_t sl = i < nA ? 0u : 1u;
+      const uint8_t* src = src_of(sl, ilist[sl][i - (sl ? nA : 0u)]);
+      static_for<4>([&](auto Q) {
+        constexpr int q = decltype(Q)::value;
+        const uint4 x = ld_piece(src + 16 * q);
+        v[u][4 * q] = x.x;
+        v[u][4 * q + 1] = x.y;
+        v[u][4 * q + 2] = x.z;
+        v[u][4 * q + 3] = x.w;
+      });
+    } else {
+      static_for<16>([&](auto P) { v[u][decltype(P)::value] = 0; });
+    }
+  });
   static_for<2>([&](auto U) {
     constexpr int u = decltype(U)::value;
     if (static_cast<uint32_t>(wave * 8 + u * 4) < nin) {  // wave-uniform
@@ -923,26 +943,12 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
       const bool ok = i < nin;
       const uint32_t sl = i < nA ? 0u : 1u;
       const uint32_t j = ok ? ilist[sl][i - (sl ? nA : 0u)] : 0u;
-      uint32_t v[16];
-      if (ok) {
-        const uint8_t* src = src_of(sl, j);
-        static_for<4>([&](auto Q) {
-          constexpr int q = decltype(Q)::value;
-          const uint4 x = ld_piece(src + 16 * q);
-          v[4 * q] = x.x;
-          v[4 * q + 1] = x.y;
-          v[4 * q + 2] = x.z;
-          v[4 * q + 3] = x.w;
-        });
-      } else {
-        static_for<16>([&](auto P) { v[decltype(P)::value] = 0; });
-      }
-      dev::planes_from_raw(v);
-      dev::mul_rt_poly(v, lcoef[sl * W + j]);
+      dev::planes_from_raw(v[u]);
+      dev::mul_rt_poly(v[u], lcoef[sl * W + j]);
       if (ok) {
         static_for<4>([&](auto Q) {
           constexpr int q = decltype(Q)::value;
-          lds[(i * 4 + q) * kSl + col] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+          lds[(i * 4 + q) * kSl + col] = make_uint4(v[u][4 * q], v[u][4 * q + 1], v[u][4 * q + 2], v[u][4 * q + 3]);
         });
       }
     }
