@@ -447,8 +447,20 @@ int encode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
   return AG_RS_OK;
 }
 
-// 32-point encodes of shards ending in a split tail chunk (S % 64 != 0, S even): one launch of
-// the TAIL transform reads and writes the tail in place (rs_xform.hpp tile_io_g), no restride
+// A 32-point transform over shards that end in a split tail chunk, one launch on the caller's
+// buffers (no restride): chunks_per_shard = ceil(S / 64), the last chunk of every shard read
+// and written as 16-byte windows of its tail (rs_xform.hpp tile_io_g).  (Two launches -- the
+// whole chunks with the tails skipped, then the tails alone -- measured slower: 3.76 / 4.06
+// TB/s at S = 1000 against 3.8-4.0 / 4.2-4.4; the whole-chunk pass alone ran at 4.35 TB/s,
+// its shards' last 64-byte sectors left partial for the second pass to complete,
+// profiles/r05_tail_split_kernel_stats.csv.)
+int launch_tail(ag_rs_ctx* c, ag::XformKind kind, const ag::XformParams& p, bool encode) {
+  if (encode) c->last_encode_kernels |= ag::encode32_kernel(p);
+  return ag::launch_xform(kind, p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+}
+
+// 32-point encodes of shards ending in a split tail chunk (S % 64 != 0, S even): the TAIL
+// transforms read and write the tail in place (launch_tail), no restride
 int encode_tail32(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig, size_t ostride,
                   uint8_t* rec, size_t rstride) {
   const size_t cps = padded_shard(S) / 64;
@@ -464,8 +476,7 @@ int encode_tail32(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, co
   p.chunks_per_shard = static_cast<uint32_t>(cps);
   p.total_columns = static_cast<uint64_t>(nblocks) * cps;
   p.tail_bytes = static_cast<uint32_t>(S % 64);
-  c->last_encode_kernels |= ag::encode32_kernel(p);
-  return ag::launch_xform(ag::XformKind::kEncode32, p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+  return launch_tail(c, ag::XformKind::kEncode32, p, true);
 }
 
 int encode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, const uint8_t* orig,
@@ -609,7 +620,7 @@ int decode_tail32(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
   p.total_columns = static_cast<uint64_t>(nblocks) * cps;
   p.tail_bytes = static_cast<uint32_t>(S % 64);
   p.out_low_half = std::all_of(mask.begin(), mask.end(), [](uint64_t w) { return (w >> 16) == 0; });
-  return ag::launch_xform(ag::XformKind::kDecode32, p, c->stream) == hipSuccess ? AG_RS_OK : AG_RS_ERR_DEVICE;
+  return launch_tail(c, ag::XformKind::kDecode32, p, false);
 }
 
 int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,

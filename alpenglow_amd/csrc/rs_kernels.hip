@@ -31,8 +31,8 @@ using dev::static_for;
 
 // One 64-chunk tile per workgroup of NW waves.  N = 32: 64 KiB LDS, two workgroups per
 // CU; N = 64: 128 KiB LDS, one workgroup (8 waves) per CU.
-// TAIL: shards end in the crate's split tail chunk (XformParams::tail_bytes, rs_xform.hpp).
-template <int NW, int DIN, int DOUT, bool TAIL = false>
+// TAIL 1: shards end in the crate's split tail chunk (XformParams::tail_bytes, rs_xform.hpp).
+template <int NW, int DIN, int DOUT, int TAIL = 0>
 __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const XformParams p) {
   __shared__ uint4 lds[4 * NW * 4 * kXfLanes];
   const int lane = threadIdx.x & 63;
@@ -61,7 +61,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
     }
   }
 
-  if constexpr (TAIL) {
+  if constexpr (TAIL == 1) {
     const TileIO in_io = tile_io<TAIL>(p, tile, lane, p.in_block_stride);
     static_for<8>([&](auto T) { tail_fix_all<TAIL>(in_io, ra[decltype(T)::value]); });
   }
@@ -101,7 +101,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
 //   H0 slots p4 p0 | waves p1 p2 p3   FFT b0, store shards 2w, 2w + 1
 // One tile (flags zeroed by the caller, every wave of the 512-thread workgroup calls it):
 // xform8_kernel's grid and the per-call server's jobs (latency_server_kernel).
-template <int DIN, int DOUT, bool HALF = false, bool TAIL = false>
+template <int DIN, int DOUT, bool HALF = false, int TAIL = 0>
 __device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile, uint4* lds, X8Flags* fl) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -219,7 +219,7 @@ __device__ __forceinline__ void xform8_tile(const XformParams& p, uint32_t tile,
   });
 }
 
-template <int DIN, int DOUT, bool HALF = false, bool TAIL = false>
+template <int DIN, int DOUT, bool HALF = false, int TAIL = 0>
 __global__ __launch_bounds__(512, 4) void xform8_kernel(const XformParams p) {
   __shared__ uint4 lds[16 * 4 * kXfLanes];  // 8 waves x 2 slots x 4 KiB
   __shared__ X8Flags flags;
@@ -2137,9 +2137,9 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
     case XformKind::kEncode32:
       if (p.tail_bytes) {  // shards ending in a split tail chunk: the TAIL kernels, same dispatch
         if (encode32_kernel(p) == kEkXform8)
-          hipLaunchKernelGGL((xform8_kernel<32, 0, false, true>), grid, dim3(512), 0, stream, p);
+          hipLaunchKernelGGL((xform8_kernel<32, 0, false, 1>), grid, dim3(512), 0, stream, p);
         else
-          hipLaunchKernelGGL((xform_kernel<4, 32, 0, true>), grid, dim3(256), 0, stream, p);
+          hipLaunchKernelGGL((xform_kernel<4, 32, 0, 1>), grid, dim3(256), 0, stream, p);
         break;
       }
       // batches of fewer tiles than CUs (a single slice per call: one tile) are latency-bound:
@@ -2159,9 +2159,9 @@ hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream
       // xform8's 5.43-5.51, one box)
       if (p.tail_bytes) {
         if (p.out_low_half)
-          hipLaunchKernelGGL((xform8_kernel<0, 32, true, true>), grid, dim3(512), 0, stream, p);
+          hipLaunchKernelGGL((xform8_kernel<0, 32, true, 1>), grid, dim3(512), 0, stream, p);
         else
-          hipLaunchKernelGGL((xform8_kernel<0, 32, false, true>), grid, dim3(512), 0, stream, p);
+          hipLaunchKernelGGL((xform8_kernel<0, 32, false, 1>), grid, dim3(512), 0, stream, p);
         break;
       }
       if (p.out_low_half)

@@ -238,7 +238,7 @@ __device__ __forceinline__ TileIO tile_io_g(uint64_t total_columns, uint32_t chu
   });
   return io;
 }
-template <bool TAIL = false>
+template <int TAIL = 0>
 __device__ __forceinline__ TileIO tile_io(const XformParams& p, uint64_t tile, int lane, uint64_t block_stride) {
   return tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, block_stride, TAIL ? p.tail_bytes : 0u);
 }
@@ -284,16 +284,16 @@ __device__ __forceinline__ void keep128(uint32_t* v, uint32_t len) {
 }
 // piece q of shard `base` (a tail piece is its lane's whole window: tail_fix_all after the
 // tile's loads, so no load waits on the others)
-template <bool TAIL>
+template <int TAIL>
 __device__ __forceinline__ uint4 ld_piece_io(const uint8_t* base, const TileIO& io, int q) {
   return ld_piece(base + io.off[q]);
 }
 // the loaded tail windows of one slot (registers 4 q .. 4 q + 3 = piece q) -> their runs at
 // byte 0, zeros above (the transform then sees symbols h..31 as zero).  Shift and length
 // depend only on h (uniform) and the lane's quarter, so the shifts take scalar amounts.
-template <bool TAIL>
+template <int TAIL>
 __device__ __forceinline__ void tail_fix_all(const TileIO& io, uint32_t* v) {
-  if constexpr (TAIL) {
+  if constexpr (TAIL == 1) {
     const int lane = threadIdx.x & 63;
     const uint32_t h = io.tlen_h;
     static_for<4>([&](auto Q) {
@@ -354,7 +354,7 @@ __device__ __forceinline__ void tail_window(uint32_t* v, int lane, uint32_t h) {
     static_for<4>([&](auto K) { v[decltype(K)::value] |= pr[decltype(K)::value]; });
   }
 }
-template <bool TAIL>
+template <int TAIL>
 __device__ __forceinline__ void st_piece_io(uint8_t* base, const TileIO& io, int q, uint32_t a, uint32_t b, uint32_t c,
                                             uint32_t d) {
   st_piece(base + io.off[q], a, b, c, d);
@@ -371,7 +371,7 @@ __device__ __forceinline__ void swap_halves(uint32_t* v) {
 }
 
 // Raw 16-byte pieces of this wave's pass-A shards 8*wave + t (before swap / transpose).
-template <bool TAIL = false>
+template <int TAIL = 0>
 __device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& io, int wave, Regs8& raw) {
   static_for<8>([&](auto T) {
     constexpr int t = decltype(T)::value;
@@ -394,7 +394,7 @@ __device__ __forceinline__ void xf_load_raw(const XformParams& p, const TileIO& 
 
 // Planes -> bytes -> lane-linear pieces, stored where the input pieces were read.  ACC: XOR
 // into the bytes already there (a partial result stored by an earlier pass).
-template <bool ACC = false, bool TAIL = false>
+template <bool ACC = false, int TAIL = 0>
 __device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const TileIO& io, uint32_t qmask,
                                             const uint32_t* planes) {
   uint32_t v[16];
@@ -405,7 +405,7 @@ __device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const Ti
   dev::transpose8(v);
   dev::transpose8(v + 8);
   swap_halves(v);
-  if constexpr (TAIL) {
+  if constexpr (TAIL == 1) {
     // tail pieces: the run (symbols >= h are zero: the inputs there were zero) completed to
     // the lane's window; lanes with an empty run (tlen 0) store nothing
     const int lane = threadIdx.x & 63;
@@ -426,7 +426,7 @@ __device__ __forceinline__ void store_shard(uint8_t* __restrict__ base, const Ti
     constexpr int q = decltype(Q)::value;
     if (qmask & (1u << q)) {
       if constexpr (ACC) {
-        static_assert(!TAIL, "accumulating stores of tail windows are not supported");
+        static_assert(TAIL != 1, "accumulating stores of tail windows are not supported");
         const uint4 x = ld_piece_io<TAIL>(base, io, q);
         uint32_t o[4] = {x.x, x.y, x.z, x.w};
         st_piece_io<TAIL>(base, io, q, v[4 * q] ^ o[0], v[4 * q + 1] ^ o[1], v[4 * q + 2] ^ o[2], v[4 * q + 3] ^ o[3]);
