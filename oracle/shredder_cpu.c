@@ -53,13 +53,18 @@ static void hash_leaf(const uint8_t *data, size_t len, uint8_t out[32]) {
   SHA256_Update(&c, data, len);
   SHA256_Final(out, &c);
 }
+/* (the low-level SHA256_* calls: OpenSSL 3's one-shot SHA256() goes through an EVP fetch under a
+ * process-wide lock, which serialised the threads) */
 static void hash_pair(const uint8_t l[32], const uint8_t r[32], uint8_t out[32]) {
   uint8_t buf[128];
   memcpy(buf, LEFT_LABEL, 32);
   memcpy(buf + 32, l, 32);
   memcpy(buf + 64, RIGHT_LABEL, 32);
   memcpy(buf + 96, r, 32);
-  SHA256(buf, sizeof buf, out);
+  SHA256_CTX c;
+  SHA256_Init(&c);
+  SHA256_Update(&c, buf, sizeof buf);
+  SHA256_Final(out, &c);
 }
 /* nodes[0..63] leaves, then 32, 16, 8, 4, 2, 1: a power-of-two leaf count never pairs with
  * an EMPTY_ROOTS entry; nodes[126] is the root */
