@@ -177,6 +177,7 @@ struct ag_rs_ctx {
   hipEvent_t present_ev = nullptr;          // recorded after its upload
   PinBuf h_lens;                            // coder shred batches: pinned staging of the lengths
   hipEvent_t lens_ev = nullptr;             // recorded after its upload
+  PinBuf h_strip;                           // coder deshred batches: pinned staging of the results
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
   static constexpr int kPipeBufs = 25;
   DevBuf pipe[kPipeBufs];                   // composed shredder scratch (ag_shredder_*_batch)
@@ -314,6 +315,7 @@ struct ag_rs_ctx {
       (void)hipEventDestroy(lens_ev);
     }
     h_lens.release();
+    h_strip.release();
     if (own_stream) (void)hipStreamDestroy(own_stream);
   }
 };
@@ -2284,6 +2286,9 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
     if ((st = c->h_present.ensure(wps * n * 8))) return st;
     uint64_t* pres = c->h_present.as<uint64_t>();
     // (uniform batches returned above)
+    // ANY_K always takes the device path; EXACT when no slice keeps more than 32 shreds (both
+    // decoders agree then).  (Packing a first ~1/8 range and the rest behind its decode
+    // measured even with one whole-batch range, profiles/r05_ab_coder_ranges.jsonl.)
     const bool surplus = pack_present_words(dpres, cpres, m, n, pres);
     if (mode == AG_RS_DECODE_ANY_K || !surplus) {
       if ((st = c->d_present.ensure(wps * n * 8, c->stream))) return st;
@@ -2739,23 +2744,49 @@ namespace {
 // 32-point encode rewrites the coding shreds of the slices that decoded and stripped (store
 // masks per slice; the others keep theirs).  plen[s] as ag_rs_coder_deshred_batch: the
 // payload length, or -NotEnoughShreds / -InvalidPadding.
-int pipe_coder_finish(ag_rs_ctx* c, size_t n, const int64_t* strip, const uint8_t* few, int64_t* plen);
+//
+// pipe_coder_enqueue runs slices s0 .. s0 + n of a batch whose scratch pipe_coder_reserve
+// sized (cw / d_present already at slice s0); pipe_coder_finish reads the results back.  The
+// store-mask kernel writes each slice's final result (length or error) into the strip words.
+int pipe_coder_reserve(ag_rs_ctx* c, size_t ntot, size_t m) {
+  int st;
+  if ((st = c->ensure_tables()) || (st = c->d_pipe_few.ensure(ntot, c->stream)) ||
+      (st = c->d_pipe_mask.ensure(8 * ntot, c->stream)) || (st = c->d_strip.ensure(8 * ntot, c->stream)))
+    return st;
+  if (m == 2 * kDataShreds)
+    return (st = c->d_x128.ensure(10 * ntot * 8, c->stream)) ? st : c->d_rows128.ensure(ntot * 128 * 4, c->stream);
+  if ((st = c->d_xmask.ensure(3 * ntot * 8, c->stream)) || (st = c->d_rows.ensure(ntot * 64 * 4, c->stream))) return st;
+  c->xmask_host.clear();  // d_xmask / d_rows no longer hold decode_device's cached patterns
+  c->xmask_w = 0;
+  return AG_RS_OK;
+}
+int pipe_coder_finish(ag_rs_ctx* c, size_t n, int64_t* plen);
+int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
+                       const uint64_t* d_present, size_t m);
+// The whole batch in one range (the composed deshred's coder stage).
+int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
+                       int64_t* plen, size_t m) {
+  int st;
+  if ((st = pipe_coder_reserve(c, n, m)) || (st = pipe_coder_enqueue(c, 0, n, S, cw, cw_stride, d_present, m)))
+    return st;
+  return pipe_coder_finish(c, n, plen);
+}
 // The same for CodingOnlyShredder's coder (LowRate 32:64, shredder.rs:362-395): every slice
 // decodes in the W = 128 window as the two per-lane decode_x16 passes (the class-8 patterns of
 // decode_device, built on the device by launch_pipe_patterns128), then the strip, and the
 // LowRate re-encode of both 32-shard recovery chunks under the per-slice store masks.
 // present: two words per slice (launch_pipe_patterns128).
-int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
-                               const uint64_t* d_present, int64_t* plen) {
+int pipe_coder_enqueue_lowrate(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
+                               const uint64_t* d_present) {
   constexpr size_t k = kDataShreds, m = 2 * kDataShreds;
   const size_t cps = S / 64;
-  int st;
-  if ((st = c->d_x128.ensure(10 * n * 8, c->stream)) || (st = c->d_rows128.ensure(n * 128 * 4, c->stream))) return st;
-  uint64_t* xm = c->d_x128.as<uint64_t>();
-  uint8_t* few = c->d_pipe_few.as<uint8_t>();
+  uint64_t* xm = c->d_x128.as<uint64_t>() + 10 * s0;
+  uint32_t* rows = c->d_rows128.as<uint32_t>() + 128 * s0;
+  uint8_t* few = c->d_pipe_few.as<uint8_t>() + s0;
+  uint64_t* mask = c->d_pipe_mask.as<uint64_t>() + s0;
+  int64_t* strip = c->d_strip.as<int64_t>() + s0;
   if (ag::launch_pipe_patterns128(d_present, n, xm, few, c->stream) != hipSuccess ||
-      ag::launch_decode_rows128(xm, static_cast<uint32_t>(n), c->dtables(), c->d_rows128.as<uint32_t>(), c->stream) !=
-          hipSuccess)
+      ag::launch_decode_rows128(xm, static_cast<uint32_t>(n), c->dtables(), rows, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   ag::DecodeXParams p{};
   p.rec = cw + k * S;
@@ -2764,7 +2795,7 @@ int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, si
   p.orig = cw;
   p.orig_block_stride = cw_stride;
   p.orig_shard_stride = S;
-  p.rows = c->d_rows128.as<uint32_t>();
+  p.rows = rows;
   p.rows_w = 128;
   p.k = static_cast<uint32_t>(k);
   p.m = 32;  // recovery shards per window half (the kernel addresses the rest from p.rec)
@@ -2778,9 +2809,9 @@ int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, si
     if (ag::launch_decode_x(128, pass, p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
       return AG_RS_ERR_DEVICE;
   }
-  int64_t* strip = c->d_strip.as<int64_t>();
   if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(k * S), n, strip, c->stream) != hipSuccess ||
-      ag::launch_pipe_store_masks(few, strip, d_present, 2, n, c->d_pipe_mask.as<uint64_t>(), c->stream) != hipSuccess)
+      ag::launch_pipe_store_masks(few, strip, d_present, 2, n, mask, -AG_RS_ERR_NOT_ENOUGH_SHARDS,
+                                  -AG_RS_ERR_INVALID_PADDING, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   for (unsigned j = 0; j * 32 < m;) {  // the recovery chunks, two per launch (encode_cols' LowRate loop)
     ag::XformParams xp{};
@@ -2790,7 +2821,7 @@ int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, si
     xp.out = cw + (k + 32 * j) * S;
     xp.out_block_stride = cw_stride;
     xp.out_shard_stride = S;
-    xp.out_mask = c->d_pipe_mask.as<uint64_t>();  // the slice's absent coding shreds, all, or none
+    xp.out_mask = mask;  // the slice's absent coding shreds, all, or none
     xp.pattern_per_block = 1;
     xp.n_in = static_cast<uint32_t>(k);
     xp.chunks_per_shard = static_cast<uint32_t>(cps);
@@ -2802,30 +2833,27 @@ int pipe_coder_deshred_lowrate(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, si
       return AG_RS_ERR_DEVICE;
     j += pair ? 2 : 1;
   }
-  return pipe_coder_finish(c, n, strip, few, plen);
+  return AG_RS_OK;
 }
 
-int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
-                       int64_t* plen, size_t m) {
+int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
+                       const uint64_t* d_present, size_t m) {
   constexpr size_t k = kDataShreds;
   const size_t cps = S / 64;
-  int st;
-  if ((st = c->ensure_tables()) || (st = c->d_pipe_few.ensure(n, c->stream)) ||
-      (st = c->d_pipe_mask.ensure(8 * n, c->stream)) || (st = c->d_strip.ensure(8 * n, c->stream)))
-    return st;
-  uint8_t* few = c->d_pipe_few.as<uint8_t>();
-  if (m == 2 * kDataShreds) return pipe_coder_deshred_lowrate(c, n, S, cw, cw_stride, d_present, plen);
+  if (n == 0) return AG_RS_OK;
+  if (m == 2 * kDataShreds) return pipe_coder_enqueue_lowrate(c, s0, n, S, cw, cw_stride, d_present);
   constexpr size_t W = 64;
-  if ((st = c->d_xmask.ensure(3 * n * 8, c->stream)) || (st = c->d_rows.ensure(n * W * 4, c->stream))) return st;
-  c->xmask_host.clear();  // d_xmask / d_rows no longer hold decode_device's cached patterns
-  c->xmask_w = 0;
-  uint64_t* xm = c->d_xmask.as<uint64_t>();
+  uint64_t* xm = c->d_xmask.as<uint64_t>() + 3 * s0;
+  uint32_t* rows = c->d_rows.as<uint32_t>() + W * s0;
+  uint8_t* few = c->d_pipe_few.as<uint8_t>() + s0;
+  uint64_t* mask = c->d_pipe_mask.as<uint64_t>() + s0;
+  int64_t* strip = c->d_strip.as<int64_t>() + s0;
   // 1 KiB shreds (every maximum slice) decode on the packed window decoder, which also restores
   // the absent coding shreds of exactly-k slices (few 2): the re-encode below skips those
   const bool fuse = cps == 16;
   if (ag::launch_pipe_patterns(d_present, n, xm, few, fuse, c->stream) != hipSuccess ||
-      ag::launch_decode_rows(xm, xm + n, static_cast<uint32_t>(n), static_cast<uint32_t>(W), c->dtables(),
-                             c->d_rows.as<uint32_t>(), true, c->stream) != hipSuccess)
+      ag::launch_decode_rows(xm, xm + n, static_cast<uint32_t>(n), static_cast<uint32_t>(W), c->dtables(), rows, true,
+                             c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   ag::DecodeXParams p{};
   p.rec = cw + k * S;
@@ -2835,7 +2863,7 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   p.orig_block_stride = cw_stride;
   p.orig_shard_stride = S;
   p.pmask = xm + n;
-  p.rows = c->d_rows.as<uint32_t>();
+  p.rows = rows;
   p.k = static_cast<uint32_t>(k);
   p.m = 32;
   p.chunk = 32;
@@ -2848,9 +2876,9 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   p.fuse = fuse ? 1u : 0u;
   if (ag::launch_decode_x(static_cast<unsigned>(W), 0, p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
-  int64_t* strip = c->d_strip.as<int64_t>();
   if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(k * S), n, strip, c->stream) != hipSuccess ||
-      ag::launch_pipe_store_masks(few, strip, d_present, 1, n, c->d_pipe_mask.as<uint64_t>(), c->stream) != hipSuccess)
+      ag::launch_pipe_store_masks(few, strip, d_present, 1, n, mask, -AG_RS_ERR_NOT_ENOUGH_SHARDS,
+                                  -AG_RS_ERR_INVALID_PADDING, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   ag::XformParams xp{};
   xp.in = cw;
@@ -2859,7 +2887,7 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   xp.out = cw + k * S;
   xp.out_block_stride = cw_stride;
   xp.out_shard_stride = S;
-  xp.out_mask = c->d_pipe_mask.as<uint64_t>();
+  xp.out_mask = mask;
   xp.pattern_per_block = 1;
   xp.n_in = static_cast<uint32_t>(k);
   xp.n_out = 32;
@@ -2867,18 +2895,16 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
   xp.total_columns = static_cast<uint64_t>(n) * cps;
   xp.skip_idle = fuse ? 1u : 0u;  // tiles of fused slices only: nothing to re-encode
   if (ag::launch_xform(ag::XformKind::kEncode32, xp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
-  return pipe_coder_finish(c, n, strip, few, plen);
+  return AG_RS_OK;
 }
-// plen from the strip results and the too-few flags (synchronous)
-int pipe_coder_finish(ag_rs_ctx* c, size_t n, const int64_t* strip, const uint8_t* few, int64_t* plen) {
-  std::vector<uint8_t> hfew(n);
-  AG_HIP(hipMemcpyAsync(plen, strip, 8 * n, hipMemcpyDeviceToHost, c->stream));
-  AG_HIP(hipMemcpyAsync(hfew.data(), few, n, hipMemcpyDeviceToHost, c->stream));
+// plen[0 .. n) from the store-mask kernels' results (synchronous): read back through pinned
+// staging (a pageable destination would take the runtime's bounce path)
+int pipe_coder_finish(ag_rs_ctx* c, size_t n, int64_t* plen) {
+  int st;
+  if ((st = c->h_strip.ensure(8 * n))) return st;
+  AG_HIP(hipMemcpyAsync(c->h_strip.ptr, c->d_strip.ptr, 8 * n, hipMemcpyDeviceToHost, c->stream));
   AG_HIP(hipStreamSynchronize(c->stream));
-  for (size_t s = 0; s < n; ++s) {
-    if (hfew[s] & 1) plen[s] = -AG_RS_ERR_NOT_ENOUGH_SHARDS;  // bit 1: coding restored by the decode
-    else if (plen[s] < 0) plen[s] = -AG_RS_ERR_INVALID_PADDING;
-  }
+  std::memcpy(plen, c->h_strip.ptr, 8 * n);
   return AG_RS_OK;
 }
 // Step 6b of ag_shredder_deshred_batch for slice s: its datagram rows are parsed again into

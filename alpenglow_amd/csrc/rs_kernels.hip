@@ -1074,7 +1074,10 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
   });
   static_for<4>([&](auto T) {
     constexpr int t = decltype(T)::value;
-    const uint32_t j = posA(t);
+    // recomputed here: otherwise layout A's rank masks stay live across the transform and
+    // the fused variant (kLive 8) spills them
+    uint32_t j = posA(t);
+    __asm__ volatile("" : "+v"(j));
     if ((out_mask >> j) & 1) {
       const uint32_t o = static_cast<uint32_t>(__builtin_popcountll(out_mask & ((uint64_t{1} << j) - 1))) + (lsl ? noA : 0u);
       static_for<4>([&](auto Q) {
@@ -1118,29 +1121,68 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
 // eval_poly over the window up to one constant factor, which cancels between the input
 // multiply (present x: exp(loc)) and the output multiply (restored x: exp(-loc)).
 // poly: one word per position instead -- the constant in the polynomial basis (mul_rt_poly).
-__global__ __launch_bounds__(64) void decode_rows_kernel(const uint64_t* __restrict__ emask,
-                                                         const uint64_t* __restrict__ pmask, uint32_t W,
-                                                         const uint16_t* __restrict__ log_t,
-                                                         const uint16_t* __restrict__ exp_t, uint32_t* rows,
-                                                         uint32_t poly) {
-  const uint64_t pat = blockIdx.x;
-  const uint32_t x = threadIdx.x;
+//
+// loc is the XOR convolution of L(z) = log z (L(0) = 0, which drops e = x; log[0] = 65535 is
+// the same residue) with the erasure indicator, so it comes out of Walsh-Hadamard transforms
+// over Z/65535 (the crate's own error-locator route, on the window instead of the field):
+// loc = H(H(L) * H(I)) / N.  The window's L is zero past W, so an N-point transform
+// (N = 64, or 128 with two positions per lane) serves every W <= N.  One wave per pattern,
+// lane-shuffle stages, no loop over the erased positions; exp depends only on the residue
+// (exp[65535] = exp[0]), so the constants are the loop form's bit for bit.
+namespace {
+__device__ __forceinline__ uint32_t m65535_add(uint32_t a, uint32_t b) {
+  const uint32_t s = a + b;
+  return s >= 65535u ? s - 65535u : s;
+}
+__device__ __forceinline__ uint32_t m65535_sub(uint32_t a, uint32_t b) { return a >= b ? a - b : a + 65535u - b; }
+__device__ __forceinline__ uint32_t m65535_mul(uint32_t a, uint32_t b) {  // canonical a, b < 65535
+  const uint32_t p = a * b;
+  uint32_t s = (p & 0xFFFFu) + (p >> 16);  // 2^16 = 1 (mod 65535)
+  s = (s & 0xFFFFu) + (s >> 16);
+  return s >= 65535u ? s - 65535u : s;
+}
+// the unnormalised Walsh transform over the 64 lanes (one residue per lane)
+__device__ __forceinline__ uint32_t walsh64(uint32_t v, int lane) {
+  static_for<6>([&](auto B) {
+    constexpr int d = 1 << decltype(B)::value;
+    const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
+    v = (lane & d) ? m65535_sub(o, v) : m65535_add(v, o);
+  });
+  return v;
+}
+// 128 points: position lane in v0, lane + 64 in v1
+__device__ __forceinline__ void walsh128(uint32_t& v0, uint32_t& v1, int lane) {
+  v0 = walsh64(v0, lane);
+  v1 = walsh64(v1, lane);
+  const uint32_t a = v0;
+  v0 = m65535_add(a, v1);
+  v1 = m65535_sub(a, v1);
+}
+__device__ __forceinline__ uint16_t locator_log(uint32_t loc, bool in) {  // exp of +loc (present), -loc (restored)
+  return static_cast<uint16_t>(in ? loc : 65535u - loc);
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void decode_rows_kernel(const uint64_t* __restrict__ emask,
+                                                          const uint64_t* __restrict__ pmask, uint32_t npat,
+                                                          uint32_t W, const uint16_t* __restrict__ log_t,
+                                                          const uint16_t* __restrict__ exp_t, uint32_t* rows,
+                                                          uint32_t poly) {
+  const uint64_t pat = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (pat >= npat) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
+  const uint32_t x = static_cast<uint32_t>(lane);
   const uint64_t e = emask[pat], in = pmask[2 * pat], out = pmask[2 * pat + 1];
-  // W <= 64 = the wave: lane x holds log[x], and log[x ^ y] is lane x ^ y's (a lane shuffle
-  // per erased position instead of a dependent table load)
-  const uint32_t lx = x < W ? log_t[x] : 0u;
-  uint32_t acc = 0;
-  for (uint64_t em = W >= 64 ? e : e & ((uint64_t{1} << W) - 1); em; em &= em - 1) {  // erased positions < W
-    const uint32_t y = static_cast<uint32_t>(__builtin_ctzll(em));
-    const uint32_t ly = static_cast<uint32_t>(__shfl_xor(static_cast<int>(lx), static_cast<int>(y)));
-    if (y != x) acc = dev::add_mod(acc, ly);
-  }
+  // H(L) / 64 (64^-1 = 1024: 2^16 = 1)
+  const uint32_t hl = m65535_mul(walsh64(x && x < W ? log_t[x] : 0u, lane), 1024u);
+  const uint32_t hi = walsh64(x < W ? static_cast<uint32_t>((e >> x) & 1) : 0u, lane);
+  const uint32_t acc = walsh64(m65535_mul(hl, hi), lane);
   if (x >= W) return;
   const bool is_in = (in >> x) & 1, is_out = (out >> x) & 1;
   if (!is_in && !is_out) return;
-  const uint16_t lg = is_in ? static_cast<uint16_t>(acc) : static_cast<uint16_t>(65535 - acc);
+  const uint16_t lg = locator_log(acc, is_in);
   if (poly) {
-    rows[pat * W + x] = dev::to_poly(exp_t[lg]);  // exp[lg] = the constant (lg < 65535)
+    rows[pat * W + x] = dev::to_poly(exp_t[lg]);  // exp[lg] = the constant
     return;
   }
   uint32_t* dst = rows + (pat * W + x) * 16;
@@ -1991,34 +2033,42 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
 
 // W = 128 windows: m6[pat] = {erased lo, hi, present lo, hi, restored lo, hi} (position bits
 // 0..63, 64..127); rows [pat][128] polynomial-basis constants (decode_rows poly form).
-__global__ __launch_bounds__(128) void decode_rows128_kernel(const uint64_t* __restrict__ m6,
+__global__ __launch_bounds__(256) void decode_rows128_kernel(const uint64_t* __restrict__ m6, uint32_t npat,
                                                             const uint16_t* __restrict__ log_t,
                                                             const uint16_t* __restrict__ exp_t, uint32_t* rows) {
-  const uint64_t pat = blockIdx.x;
-  const uint32_t x = threadIdx.x;
+  const uint64_t pat = static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (pat >= npat) return;  // wave-uniform
+  const int lane = threadIdx.x & 63;
   const uint64_t* m = m6 + 6 * pat;
-  const uint32_t h = x >> 6, xl = x & 63;
-  const bool is_in = (m[2 + h] >> xl) & 1, is_out = (m[4 + h] >> xl) & 1;
-  if (!is_in && !is_out) return;
-  uint32_t acc = 0;
-  for (uint32_t y = 0; y < 128; ++y)
-    if (((m[y >> 6] >> (y & 63)) & 1) && y != x) acc = dev::add_mod(acc, log_t[x ^ y]);
-  const uint16_t lg = is_in ? static_cast<uint16_t>(acc) : static_cast<uint16_t>(65535 - acc);
-  rows[pat * 128 + x] = dev::to_poly(exp_t[lg]);
+  // decode_rows' Walsh route at N = 128: positions lane (v0) and lane + 64 (v1)
+  uint32_t l0 = lane ? log_t[lane] : 0u, l1 = log_t[lane + 64];
+  walsh128(l0, l1, lane);
+  l0 = m65535_mul(l0, 512u);  // 128^-1 = 512
+  l1 = m65535_mul(l1, 512u);
+  uint32_t i0 = static_cast<uint32_t>((m[0] >> lane) & 1), i1 = static_cast<uint32_t>((m[1] >> lane) & 1);
+  walsh128(i0, i1, lane);
+  uint32_t a0 = m65535_mul(l0, i0), a1 = m65535_mul(l1, i1);
+  walsh128(a0, a1, lane);
+  static_for<2>([&](auto H) {
+    constexpr int h = decltype(H)::value;
+    const bool is_in = (m[2 + h] >> lane) & 1, is_out = (m[4 + h] >> lane) & 1;
+    if (is_in || is_out) rows[pat * 128 + h * 64 + lane] = dev::to_poly(exp_t[locator_log(h ? a1 : a0, is_in)]);
+  });
 }
 
 hipError_t launch_decode_rows128(const uint64_t* m6, uint32_t npat, const GfDeviceTables& t, uint32_t* rows,
                                  hipStream_t stream) {
   if (npat == 0) return hipSuccess;
-  hipLaunchKernelGGL(decode_rows128_kernel, dim3(npat), dim3(128), 0, stream, m6, t.log, t.exp, rows);
+  hipLaunchKernelGGL(decode_rows128_kernel, dim3((npat + 3) / 4), dim3(256), 0, stream, m6, npat, t.log, t.exp, rows);
   return hipGetLastError();
 }
 
 hipError_t launch_decode_rows(const uint64_t* emask, const uint64_t* pmask, uint32_t npat, uint32_t W,
                               const GfDeviceTables& t, uint32_t* rows, bool poly, hipStream_t stream) {
   if (npat == 0) return hipSuccess;
-  hipLaunchKernelGGL(decode_rows_kernel, dim3(npat), dim3(64), 0, stream, emask, pmask, W, t.log, t.exp, rows,
-                     poly ? 1u : 0u);
+  if (W > 64) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(decode_rows_kernel, dim3((npat + 3) / 4), dim3(256), 0, stream, emask, pmask, npat, W, t.log, t.exp,
+                     rows, poly ? 1u : 0u);
   return hipGetLastError();
 }
 

@@ -243,43 +243,37 @@ __device__ __forceinline__ TileIO tile_io(const XformParams& p, uint64_t tile, i
   return tile_io_g(p.total_columns, p.chunks_per_shard, tile, lane, block_stride, TAIL ? p.tail_bytes : 0u);
 }
 
-// 128-bit shifts of v[0..3] by a byte count (0..16) as two 64-bit halves
-__device__ __forceinline__ void shr128(uint32_t* v, uint32_t bytes) {
-  const uint32_t sh = 8 * bytes;
-  uint64_t lo = v[0] | static_cast<uint64_t>(v[1]) << 32, hi = v[2] | static_cast<uint64_t>(v[3]) << 32;
-  if (sh >= 64) {
-    lo = sh >= 128 ? 0 : hi >> (sh - 64);
-    hi = 0;
-  } else if (sh != 0) {
-    lo = (lo >> sh) | (hi << (64 - sh));
-    hi >>= sh;
-  }
-  v[0] = static_cast<uint32_t>(lo);
-  v[1] = static_cast<uint32_t>(lo >> 32);
-  v[2] = static_cast<uint32_t>(hi);
-  v[3] = static_cast<uint32_t>(hi >> 32);
+// Byte funnels on 16-byte windows with a wave-uniform byte count j (0..16): out = bytes
+// [j, j + 16) of the 32-byte little-endian value lo ++ hi.  One scalar branch on j / 4 picks
+// the word offset, then four v_alignbyte_b32 (the 64-bit shift pairs and their selects of a
+// per-lane form cost ~2x the VALU and a branch per shift).
+template <int W>
+__device__ __forceinline__ void funnel_w(const uint32_t* lo, const uint32_t* hi, uint32_t b, uint32_t* out) {
+  const uint32_t c[9] = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3], 0u};
+  static_for<4>([&](auto I) {
+    constexpr int i = decltype(I)::value;
+    out[i] = __builtin_amdgcn_alignbyte(c[i + W + 1], c[i + W], b);
+  });
 }
-__device__ __forceinline__ void shl128(uint32_t* v, uint32_t bytes) {
-  const uint32_t sh = 8 * bytes;
-  uint64_t lo = v[0] | static_cast<uint64_t>(v[1]) << 32, hi = v[2] | static_cast<uint64_t>(v[3]) << 32;
-  if (sh >= 64) {
-    hi = sh >= 128 ? 0 : lo << (sh - 64);
-    lo = 0;
-  } else if (sh != 0) {
-    hi = (hi << sh) | (lo >> (64 - sh));
-    lo <<= sh;
+__device__ __forceinline__ void funnel16(const uint32_t* lo, const uint32_t* hi, uint32_t j, uint32_t* out) {
+  j = __builtin_amdgcn_readfirstlane(j);
+  const uint32_t b = j & 3;
+  switch (j >> 2) {
+    case 0: funnel_w<0>(lo, hi, b, out); break;
+    case 1: funnel_w<1>(lo, hi, b, out); break;
+    case 2: funnel_w<2>(lo, hi, b, out); break;
+    case 3: funnel_w<3>(lo, hi, b, out); break;
+    default: funnel_w<4>(lo, hi, b, out); break;
   }
-  v[0] = static_cast<uint32_t>(lo);
-  v[1] = static_cast<uint32_t>(lo >> 32);
-  v[2] = static_cast<uint32_t>(hi);
-  v[3] = static_cast<uint32_t>(hi >> 32);
 }
-// keep the low `len` bytes (0..16)
-__device__ __forceinline__ void keep128(uint32_t* v, uint32_t len) {
+// keep the low `len` bytes (0..16, uniform): word masks from scalar arithmetic
+__device__ __forceinline__ void keep16(uint32_t* v, uint32_t len) {
+  len = __builtin_amdgcn_readfirstlane(len);
   static_for<4>([&](auto K) {
     constexpr int k = decltype(K)::value;
     const int keep = static_cast<int>(len) - 4 * k;
-    v[k] = keep >= 4 ? v[k] : keep <= 0 ? 0u : (v[k] & ((1u << (8 * keep)) - 1));
+    const uint32_t m = keep >= 4 ? ~0u : keep <= 0 ? 0u : (1u << (8 * keep)) - 1;
+    v[k] &= m;
   });
 }
 // piece q of shard `base` (a tail piece is its lane's whole window: tail_fix_all after the
@@ -290,32 +284,31 @@ __device__ __forceinline__ uint4 ld_piece_io(const uint8_t* base, const TileIO& 
 }
 // the loaded tail windows of one slot (registers 4 q .. 4 q + 3 = piece q) -> their runs at
 // byte 0, zeros above (the transform then sees symbols h..31 as zero).  Shift and length
-// depend only on h (uniform) and the lane's quarter, so the shifts take scalar amounts.
+// depend only on h (uniform) and the lane's quarter.
 template <int TAIL>
 __device__ __forceinline__ void tail_fix_all(const TileIO& io, uint32_t* v) {
   if constexpr (TAIL == 1) {
     const int lane = threadIdx.x & 63;
-    const uint32_t h = io.tlen_h;
+    const uint32_t h = __builtin_amdgcn_readfirstlane(io.tlen_h);
+    const uint32_t zero[4] = {0u, 0u, 0u, 0u};
     static_for<4>([&](auto Q) {
       constexpr int q = decltype(Q)::value;
       if (__builtin_amdgcn_ballot_w64((io.tailq >> q) & 1) != 0) {  // wave-uniform
         uint32_t* x = v + 4 * q;
-        uint32_t t[4] = {x[0], x[1], x[2], x[3]};
         const bool tl = (io.tailq >> q) & 1;
+        uint32_t t[4];
         if (h >= 16) {  // quarters 1 / 3: window [h - 16, h) / [T - 16, T), run at 32 - h
-          shr128(t, 32 - h);
-          keep128(t, h - 16);
+          funnel16(x, zero, 32 - h, t);
+          keep16(t, h - 16);
           if (tl && (lane & 1)) static_for<4>([&](auto K) { x[decltype(K)::value] = t[decltype(K)::value]; });
         } else {  // quarter 0: run [0, h) at 0; quarter 2: window [T - 16, T), run at 16 - h; 1 / 3 empty
-          shr128(t, 16 - h);
-          keep128(t, h);
-          uint32_t u[4] = {x[0], x[1], x[2], x[3]};
-          keep128(u, h);
+          funnel16(x, zero, 16 - h, t);
           if (tl) {
             static_for<4>([&](auto K) {
               constexpr int k = decltype(K)::value;
-              x[k] = (lane & 1) ? 0u : lane >= 32 ? t[k] : u[k];
+              x[k] = (lane & 1) ? 0u : lane >= 32 ? t[k] : x[k];
             });
+            keep16(x, h);
           }
         }
       }
@@ -327,6 +320,8 @@ __device__ __forceinline__ void tail_fix_all(const TileIO& io, uint32_t* v) {
 // with h < 16 quarters 0 / 2 take each other (lanes l, l + 32).  Wave-wide: every lane runs
 // the exchanges; the caller stores the result on tail lanes only.  h is uniform.
 __device__ __forceinline__ void tail_window(uint32_t* v, int lane, uint32_t h) {
+  h = __builtin_amdgcn_readfirstlane(h);
+  const uint32_t zero[4] = {0u, 0u, 0u, 0u};
   if (h >= 16) {
     uint32_t lo[4];  // the lane below's run (quarter 0 / 2 of the chunk)
     static_for<4>([&](auto K) {
@@ -334,24 +329,27 @@ __device__ __forceinline__ void tail_window(uint32_t* v, int lane, uint32_t h) {
       lo[k] = static_cast<uint32_t>(__builtin_amdgcn_mov_dpp(static_cast<int>(v[k]), 0xA0 /* quad_perm 0,0,2,2 */, 0xF,
                                                              0xF, false));
     });
-    if (lane & 1) {  // window [h - 16, h) = lo[h - 16, 16) ++ own[0, h - 16)
-      shr128(lo, h - 16);
-      shl128(v, 32 - h);
-      static_for<4>([&](auto K) { v[decltype(K)::value] |= lo[decltype(K)::value]; });
-    }
+    // window [h - 16, h) = lo[h - 16, 16) ++ own[0, h - 16): bytes h - 16 .. h + 15 of lo ++ own
+    uint32_t w[4];
+    funnel16(lo, v, h - 16, w);
+    if (lane & 1) static_for<4>([&](auto K) { v[decltype(K)::value] = w[decltype(K)::value]; });
   } else {
     uint32_t pr[4];  // the partner half's run: quarter 0 <-> 2
     static_for<4>([&](auto K) {
       constexpr int k = decltype(K)::value;
       pr[k] = __builtin_amdgcn_permlane32_swap(v[k], v[k], false, false)[0];
     });
-    if (lane >= 32) {  // quarter 2: window [T - 16, T) = q0[2h - 16, h) ++ own[0, h)
-      shr128(pr, 2 * h - 16);
-      shl128(v, 16 - h);
-    } else {  // quarter 0: window [0, 16) = own[0, h) ++ q2[0, 16 - h)
-      shl128(pr, h);
-    }
-    static_for<4>([&](auto K) { v[decltype(K)::value] |= pr[decltype(K)::value]; });
+    // quarter 2: window [T - 16, T) = q0[2h - 16, h) ++ own[0, h) (pr is zero from byte h on);
+    // quarter 0: window [0, 16) = own[0, h) ++ q2[0, 16 - h)
+    uint32_t a[4], b[4];
+    funnel16(pr, zero, 2 * h - 16, a);  // q0's bytes from 2h - 16 down to 0
+    funnel16(zero, v, h, b);            // own run moved up by 16 - h
+    uint32_t c[4];
+    funnel16(zero, pr, 16 - h, c);      // q2's run moved up by h
+    static_for<4>([&](auto K) {
+      constexpr int k = decltype(K)::value;
+      v[k] = lane >= 32 ? (a[k] | b[k]) : (v[k] | c[k]);
+    });
   }
 }
 template <int TAIL>

@@ -201,21 +201,26 @@ __global__ __launch_bounds__(256) void pipe_patterns128_kernel(const uint64_t* _
 }
 
 __global__ __launch_bounds__(256) void pipe_store_mask_kernel(const uint8_t* __restrict__ few,
-                                                              const int64_t* __restrict__ strip,
+                                                              int64_t* __restrict__ strip,
                                                               const uint64_t* __restrict__ present, uint32_t wps,
-                                                              uint64_t n, uint64_t* __restrict__ mask) {
+                                                              uint64_t n, uint64_t* __restrict__ mask,
+                                                              int64_t err_few, int64_t err_padding) {
   const uint64_t s = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (s >= n) return;
   uint64_t m = 0;
-  if (!few[s] && strip[s] >= 0) {  // few 2: restored by the decode
+  const int64_t len = strip[s];
+  if (!(few[s] & 1) && len >= 0) {
     // exactly k kept shreds fix the codeword: the received coding shreds are its own, so only
-    // the absent ones are written; with surplus shreds every coding shred is re-encoded
+    // the absent ones are written (none when the decode restored them: few 2); with surplus
+    // shreds every coding shred is re-encoded
     const uint64_t p0 = present[wps * s], p1 = wps == 2 ? present[wps * s + 1] : 0;
     const uint32_t cnt = static_cast<uint32_t>(__builtin_popcountll(p0) + __builtin_popcountll(p1));
     const uint64_t coding = (p0 >> 32) | (p1 << 32);  // coding shreds 0..63 present
-    m = cnt == kPipeData ? ~coding : ~uint64_t{0};
+    m = few[s] ? 0 : cnt == kPipeData ? ~coding : ~uint64_t{0};
   }
   mask[s] = m;
+  // the slice's result in place: payload length, or the crate's error (too few shreds first)
+  strip[s] = (few[s] & 1) ? err_few : len < 0 ? err_padding : len;
 }
 
 }  // namespace
@@ -281,11 +286,12 @@ hipError_t launch_pipe_patterns128(const uint64_t* present, uint64_t nslices, ui
   return hipGetLastError();
 }
 
-hipError_t launch_pipe_store_masks(const uint8_t* few, const int64_t* strip, const uint64_t* present, uint32_t wps,
-                                   uint64_t nslices, uint64_t* mask, hipStream_t stream) {
+hipError_t launch_pipe_store_masks(const uint8_t* few, int64_t* strip, const uint64_t* present, uint32_t wps,
+                                   uint64_t nslices, uint64_t* mask, int64_t err_few, int64_t err_padding,
+                                   hipStream_t stream) {
   if (nslices == 0) return hipSuccess;
   hipLaunchKernelGGL(pipe_store_mask_kernel, grid256(nslices), dim3(256), 0, stream, few, strip, present, wps, nslices,
-                     mask);
+                     mask, err_few, err_padding);
   return hipGetLastError();
 }
 

@@ -107,8 +107,10 @@ hipError_t launch_pipe_patterns128(const uint64_t* present, uint64_t nslices, ui
 // are, like the reference's early returns; few[s] == 2: the decode restored them).
 // present: the kept-shred words (wps per slice, launch_pipe_patterns / 128): a slice with
 // exactly 32 kept shreds re-encodes only its absent coding shreds (bit j: coding shred j).
-hipError_t launch_pipe_store_masks(const uint8_t* few, const int64_t* strip, const uint64_t* present, uint32_t wps,
-                                   uint64_t nslices, uint64_t* mask,
+// strip[s] then becomes the slice's result: its payload length, err_few (fewer than 32 kept
+// shreds) or err_padding (the strip failed).
+hipError_t launch_pipe_store_masks(const uint8_t* few, int64_t* strip, const uint64_t* present, uint32_t wps,
+                                   uint64_t nslices, uint64_t* mask, int64_t err_few, int64_t err_padding,
                                    hipStream_t stream);
 
 }  // namespace ag
