@@ -53,7 +53,7 @@ __global__ __launch_bounds__(64 * NW, NW == 4 ? 2 : 1) void xform_kernel(const X
       const uint64_t m = p.out_mask[0];
       mask[0] = mask[1] = mask[2] = mask[3] = m;
     } else {
-      const TileIO io = tile_io(p, tile, lane, p.out_block_stride);
+      const TileIO io = tile_io<TAIL>(p, tile, lane, p.out_block_stride);  // the stores' column order
       static_for<4>([&](auto Q) {
         constexpr int q = decltype(Q)::value;
         mask[q] = p.out_mask[io.blk[q]];
