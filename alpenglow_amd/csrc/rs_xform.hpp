@@ -218,10 +218,19 @@ __device__ __forceinline__ TileIO tile_io_g(uint64_t total_columns, uint32_t chu
   const uint32_t r0 = static_cast<uint32_t>(g0 - b0 * C);
   const uint64_t base = b0 * block_stride;
   const uint32_t lc = (lane & 31) >> 1;
+  // Tail kernels with 16 or 32 chunks per shard and T % 8 == 0 (a tile is 64 / C whole shard
+  // rows): instruction q takes chunks [q C/4, (q + 1) C/4) of each row -- runs of C/4 chunks
+  // instead of one 16-chunk run -- so every tail chunk falls in instruction 3 and the window
+  // fix-ups run for one of the four pieces of each slot.  Measured against the 16-chunk runs
+  // (profiles/r05_ab_tail_runs.jsonl, one box): S = 1000 3.90 -> 4.37 / 4.37 -> 4.65 TB/s
+  // encode / reconstruct, S = 2000 4.31 -> 4.68 / 4.77 -> 4.95; but S = 1022 (2-byte aligned
+  // shards) 3.85 -> 3.57 encode and C = 8 (128-byte runs) 3.51 -> 2.77: those keep 16-chunk runs
+  const uint32_t R = (tail != 0 && tail % 8 == 0 && (C == 16 || C == 32)) ? C / 4 : 16;
   static_for<4>([&](auto Q) {
     constexpr int q = decltype(Q)::value;
-    const bool ok = g0 + 16 * q + lc < total_columns;
-    const uint32_t c = ok ? r0 + 16 * q + lc : r0;  // idle pieces re-read the tile's first chunk, never store
+    const uint32_t cl = R == 16 ? 16 * q + lc : (lc / R) * C + q * R + lc % R;
+    const bool ok = g0 + cl < total_columns;
+    const uint32_t c = ok ? r0 + cl : r0;  // idle pieces re-read the tile's first chunk, never store
     uint32_t d, rem;
     if (C >= kXfLanes) {
       d = c >= C ? 1u : 0u;

@@ -1083,7 +1083,8 @@ def test_tail_chunk_encode_decode(ctx, dev, k, m, S):
 
 
 @pytest.mark.parametrize("S,n", [(1000, 1040), (1022, 1030), (62, 16400), (2, 40), (66, 8200), (126, 9000),
-                                 (1000, 9), (574, 2000), (84, 300), (48, 6000), (110, 500)])
+                                 (1000, 9), (574, 2000), (84, 300), (48, 6000), (110, 500), (2040, 600),
+                                 (2000, 20)])
 @pytest.mark.parametrize("k", [32, 25])
 def test_tail_chunks_in_kernel(ctx, dev, S, n, k):
     """32-point geometries whose shards end in the crate's split tail chunk (S mod 64 != 0):
@@ -1091,7 +1092,9 @@ def test_tail_chunks_in_kernel(ctx, dev, S, n, k):
     transforms: xform<4> at >= 256 tiles, xform8 below; rs_xform.hpp tile_io_g), no restride
     (tails under 16 bytes still restride).
     Tails of T = 2..62 bytes (odd and even halves), against the C oracle and the originals;
-    per-block random erasures (and erasures confined to shards 0..15: the pruned FFT)."""
+    per-block random erasures (and erasures confined to shards 0..15: the pruned FFT).  S =
+    1000, 2000, 2040: 16 / 32 chunks per shard with T % 8 == 0, the tile order of C/4-chunk runs
+    (tile_io_g); S = 1022 and the rest: 16-chunk runs."""
     m = 32
     blocks = _blocks(7300 + S + k, n, k, S)
     rec = gpu_encode(ctx, dev, blocks, m)
