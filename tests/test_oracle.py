@@ -149,6 +149,43 @@ def test_locator_fwht_equals_direct_product():
         assert int(exp[int(loc[x]) % 65535]) == acc
 
 
+def _walsh_mod(v):
+    """Unnormalised Walsh-Hadamard transform over Z/65535 (the kernels' lane-shuffle stages)."""
+    v = v.copy()
+    d = 1
+    while d < len(v):
+        for i in range(len(v)):
+            if not i & d:
+                a, b = v[i], v[i | d]
+                v[i], v[i | d] = (a + b) % 65535, (a - b) % 65535
+        d <<= 1
+    return v
+
+
+@pytest.mark.parametrize("N,W", [(64, 64), (64, 32), (64, 16), (128, 128)])
+def test_window_locator_walsh_route(N, W):
+    """decode_rows / decode_rows128 (rs_kernels.hip): loc(x) = sum_{e erased, e != x} log(x ^ e)
+    mod 65535 as the XOR convolution of L (L(z) = log z, L(0) = 0, zero past W) with the
+    erasure indicator, i.e. H(H(L) * H(I)) / N over Z/65535 (N^-1 = 1024 / 512 since 2^16 = 1),
+    against the loop form; the constants exp[loc] then agree bit for bit (exp[65535] = exp[0])."""
+    exp, log, _, _ = o.tables()
+    assert pow(N, -1, 65535) == {64: 1024, 128: 512}[N] and int(exp[65535]) == int(exp[0])
+    L = np.array([int(log[z]) % 65535 if 0 < z < W else 0 for z in range(N)], np.int64)
+    hl = _walsh_mod(L) * pow(N, -1, 65535) % 65535
+    rng = np.random.default_rng(N * 1000 + W)
+    for _ in range(24):
+        ind = np.zeros(N, np.int64)
+        ind[:W] = rng.random(W) < rng.random()
+        got = _walsh_mod(hl * _walsh_mod(ind) % 65535)
+        for x in range(W):
+            want = 0
+            for y in range(W):
+                if ind[y] and y != x:
+                    want = (want + int(log[x ^ y])) % 65535
+            assert got[x] == want, (x, got[x], want)
+            assert int(exp[65535 - got[x]]) == int(exp[(65535 - want) % 65535])
+
+
 # ------------------------------------------------------------------------ layout & rate
 
 def test_shard_layout_roundtrip_and_tail_split():
