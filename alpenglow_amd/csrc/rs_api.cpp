@@ -2171,7 +2171,7 @@ int ag_rs_coder_shred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, const ui
 
 namespace {
 int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
-                       int64_t* plen, size_t m);
+                       int64_t* plen, size_t m, bool no_surplus = false);
 }  // namespace
 
 namespace {
@@ -2187,7 +2187,7 @@ __attribute__((target("avx2"))) uint32_t nonzero_mask32_avx2(const uint8_t* f) {
 // (a macro body, not a template: this part of the file has C linkage)
 #define AG_PACK_PRESENT(MASK32)                                                   \
   const size_t wps = m == kDataShreds ? 1 : 2;                                    \
-  bool surplus = false;                                                           \
+  bool surplus = false, full_data = false;                                        \
   for (size_t b = 0; b < n; ++b) {                                                \
     uint64_t* q = pres + wps * b;                                                 \
     q[0] = uint64_t{MASK32(dpres + b * kDataShreds)} | (uint64_t{MASK32(cpres + b * m)} << 32); \
@@ -2197,20 +2197,27 @@ __attribute__((target("avx2"))) uint32_t nonzero_mask32_avx2(const uint8_t* f) {
       cnt += __builtin_popcountll(q[1]);                                          \
     }                                                                             \
     surplus |= cnt > static_cast<int>(kDataShreds);                               \
+    full_data |= (q[0] & 0xFFFFFFFFull) == 0xFFFFFFFFull;                         \
   }                                                                               \
+  *any_full_data = full_data;                                                     \
   return surplus;
 __attribute__((target("avx2"))) bool pack_present_avx2(const uint8_t* dpres, const uint8_t* cpres, size_t m, size_t n,
-                                                       uint64_t* pres) {
+                                                       uint64_t* pres, bool* any_full_data) {
   AG_PACK_PRESENT(nonzero_mask32_avx2)
 }
 uint32_t nonzero_mask32(const uint8_t* f) { return static_cast<uint32_t>(pack_flags(f, 32)); }
-bool pack_present_scalar(const uint8_t* dpres, const uint8_t* cpres, size_t m, size_t n, uint64_t* pres) {
+bool pack_present_scalar(const uint8_t* dpres, const uint8_t* cpres, size_t m, size_t n, uint64_t* pres,
+                         bool* any_full_data) {
   AG_PACK_PRESENT(nonzero_mask32)
 }
 #undef AG_PACK_PRESENT
-bool pack_present_words(const uint8_t* dpres, const uint8_t* cpres, size_t m, size_t n, uint64_t* pres) {
+// *any_full_data: some slice holds every data shred (its decode is skipped, so its absent
+// coding shreds come from the re-encode)
+bool pack_present_words(const uint8_t* dpres, const uint8_t* cpres, size_t m, size_t n, uint64_t* pres,
+                        bool* any_full_data) {
   static const bool avx2 = __builtin_cpu_supports("avx2");
-  return avx2 ? pack_present_avx2(dpres, cpres, m, n, pres) : pack_present_scalar(dpres, cpres, m, n, pres);
+  return avx2 ? pack_present_avx2(dpres, cpres, m, n, pres, any_full_data)
+              : pack_present_scalar(dpres, cpres, m, n, pres, any_full_data);
 }
 
 // ag_rs_coder_deshred_batch when every slice has the same present shreds (pattern = slice 0's).
@@ -2289,12 +2296,15 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
     // ANY_K always takes the device path; EXACT when no slice keeps more than 32 shreds (both
     // decoders agree then).  (Packing a first ~1/8 range and the rest behind its decode
     // measured even with one whole-batch range, profiles/r05_ab_coder_ranges.jsonl.)
-    const bool surplus = pack_present_words(dpres, cpres, m, n, pres);
+    bool full_data = false;
+    const bool surplus = pack_present_words(dpres, cpres, m, n, pres, &full_data);
     if (mode == AG_RS_DECODE_ANY_K || !surplus) {
       if ((st = c->d_present.ensure(wps * n * 8, c->stream))) return st;
       AG_HIP(hipMemcpyAsync(c->d_present.ptr, pres, wps * n * 8, hipMemcpyHostToDevice, c->stream));
       AG_HIP(hipEventRecord(c->present_ev, c->stream));
-      return pipe_coder_deshred(c, n, S, cw, cw_stride, c->d_present.as<uint64_t>(), out, m);  // synchronous
+      // no surplus and no slice with every data shred: no store mask of the re-encode is set
+      return pipe_coder_deshred(c, n, S, cw, cw_stride, c->d_present.as<uint64_t>(), out, m,
+                                !surplus && !full_data);  // synchronous
     }
   }
   // slices with fewer than 32 shreds: reported, and decoded as "nothing missing" (untouched)
@@ -2762,12 +2772,14 @@ int pipe_coder_reserve(ag_rs_ctx* c, size_t ntot, size_t m) {
 }
 int pipe_coder_finish(ag_rs_ctx* c, size_t n, int64_t* plen);
 int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
-                       const uint64_t* d_present, size_t m);
-// The whole batch in one range (the composed deshred's coder stage).
+                       const uint64_t* d_present, size_t m, bool no_surplus);
+// The whole batch in one range (the composed deshred's coder stage).  no_surplus: the caller
+// knows that no slice keeps more than 32 shreds and none keeps all 32 data shreds.
 int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
-                       int64_t* plen, size_t m) {
+                       int64_t* plen, size_t m, bool no_surplus) {
   int st;
-  if ((st = pipe_coder_reserve(c, n, m)) || (st = pipe_coder_enqueue(c, 0, n, S, cw, cw_stride, d_present, m)))
+  if ((st = pipe_coder_reserve(c, n, m)) ||
+      (st = pipe_coder_enqueue(c, 0, n, S, cw, cw_stride, d_present, m, no_surplus)))
     return st;
   return pipe_coder_finish(c, n, plen);
 }
@@ -2837,7 +2849,7 @@ int pipe_coder_enqueue_lowrate(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint
 }
 
 int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
-                       const uint64_t* d_present, size_t m) {
+                       const uint64_t* d_present, size_t m, bool no_surplus) {
   constexpr size_t k = kDataShreds;
   const size_t cps = S / 64;
   if (n == 0) return AG_RS_OK;
@@ -2894,6 +2906,9 @@ int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw,
   xp.chunks_per_shard = static_cast<uint32_t>(cps);
   xp.total_columns = static_cast<uint64_t>(n) * cps;
   xp.skip_idle = fuse ? 1u : 0u;  // tiles of fused slices only: nothing to re-encode
+  // fused, no slice with surplus shreds and none with every data shred: every store mask is
+  // zero (exactly 32 kept: restored by the decode; fewer, or a failed strip: untouched)
+  if (fuse && no_surplus) return AG_RS_OK;
   if (ag::launch_xform(ag::XformKind::kEncode32, xp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   return AG_RS_OK;
 }

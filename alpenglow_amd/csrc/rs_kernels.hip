@@ -1636,13 +1636,18 @@ __global__ __launch_bounds__(1024) void locator_kernel(const uint8_t* erased, ui
 __global__ __launch_bounds__(256) void coder_pad_kernel(const uint8_t* __restrict__ payload, uint64_t payload_stride,
                                                         const uint32_t* __restrict__ lens, uint8_t* cw,
                                                         uint64_t cw_stride, uint32_t data_bytes, uint64_t nslices) {
-  const uint64_t b = blockIdx.x;
+  // with a payload one workgroup copies one slice; in place (payload null) only the pieces
+  // from byte len on change, so a wave serves one slice and a workgroup four (dispatch-bound
+  // otherwise: 65 536 one-wave workgroups took 25 us for one piece each)
+  const uint64_t b = payload ? blockIdx.x : static_cast<uint64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (b >= nslices) return;
+  const uint32_t tid = payload ? threadIdx.x : (threadIdx.x & 63), nt = payload ? blockDim.x : 64;
   const uint32_t per = data_bytes / 16;
   const uint32_t len = lens[b];
   uint8_t* base = cw + b * cw_stride;
   const uint8_t* src = payload ? payload + b * payload_stride : nullptr;
   const bool a16 = src && (reinterpret_cast<uintptr_t>(src) & 15) == 0;
-  for (uint32_t piece = (src ? 0u : len / 16) + threadIdx.x; piece < per; piece += blockDim.x) {
+  for (uint32_t piece = (src ? 0u : len / 16) + tid; piece < per; piece += nt) {
     const uint32_t j = piece * 16;
     uint8_t* dst = base + j;
     if (j + 16 <= len) {  // whole payload piece (only with a source)
@@ -2256,8 +2261,9 @@ hipError_t launch_coder_pad(const uint8_t* payload, uint64_t payload_stride, con
   if (data_bytes % 16) return hipErrorInvalidValue;
   if (nslices == 0 || data_bytes == 0) return hipSuccess;
   if (nslices > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(coder_pad_kernel, dim3(static_cast<unsigned>(nslices)), dim3(payload ? 256 : 64), 0, stream,
-                     payload, payload_stride, lens, cw, cw_stride, data_bytes, nslices);
+  const uint64_t groups = payload ? nslices : (nslices + 3) / 4;
+  hipLaunchKernelGGL(coder_pad_kernel, dim3(static_cast<unsigned>(groups)), dim3(256), 0, stream, payload,
+                     payload_stride, lens, cw, cw_stride, data_bytes, nslices);
   return hipGetLastError();
 }
 
