@@ -11,7 +11,8 @@
 // Kernels: one wave per packet.  Lane 0 reads the fixed fields and the two lengths (the
 // offsets depend on data_len), the wave then copies the data, signature and proof bytes
 // lane-parallel: deserialize moves the data (at packet offset 37, unaligned) as 16-byte groups
-// of words funnel-shifted with v_alignbyte, the signature and proof bytes singly.  The packet bytes are
+// of words funnel-shifted with v_alignbyte, the signature and proof bytes singly; serialize
+// stores 16 bytes per lane at the rows' unaligned offsets (copy16_any).  The packet bytes are
 // read once and the columns written once: ~1.3 KB per shred each way.
 #include <hip/hip_runtime.h>
 
@@ -68,6 +69,15 @@ __device__ __forceinline__ void copy_to_aligned(uint8_t* __restrict__ dst, const
   const uint32_t nw = len >> 2;
   shift_words(reinterpret_cast<uint32_t*>(dst), reinterpret_cast<const uint32_t*>(src - mis), nw, mis, lane);
   for (uint32_t i = 4 * nw + lane; i < len; i += 64) dst[i] = src[i];
+}
+// dst[0, len) = src[0, len) at any alignment of either: 16-byte lane accesses (gfx950 runs
+// global memory in unaligned mode), the last len % 16 bytes singly.  Lane-parallel.
+__device__ __forceinline__ void copy16_any(uint8_t* __restrict__ dst, const uint8_t* __restrict__ src, uint32_t len,
+                                           int lane) {
+  const uint32_t n16 = len >> 4;
+  for (uint32_t i = lane; i < n16; i += 64)
+    *reinterpret_cast<uint4*>(dst + 16 * i) = *reinterpret_cast<const uint4*>(src + 16 * i);
+  for (uint32_t i = 16 * n16 + lane; i < len; i += 64) dst[i] = src[i];
 }
 // the data rows are 4-byte aligned (every row, so word copies never leave a row)
 __device__ __forceinline__ bool word_rows(const ShredColumns& c) {
@@ -156,12 +166,10 @@ __global__ __launch_bounds__(256) void shred_serialize_kernel(const ShredColumns
     packet_lens[t] = o_sig + 72 + 32 * plen;
   }
   const uint8_t* dd = c.data + t * c.data_stride;
-  // byte stores: the word-wide copy (copy_from_aligned) measured slower here, 4.1 vs 3.2 ms
-  // per 4 M datagrams on 1325-byte rows (profiles/r02_wire_copy_ab.json)
-  for (uint32_t i = lane; i < dlen; i += 64) pk[kShredHeadBytes + i] = dd[i];
-  pk[o_sig + lane] = c.sig[64 * h + lane];
-  const uint8_t* pp = c.proof + t * c.proof_stride;
-  for (uint32_t i = lane; i < 32 * plen; i += 64) pk[o_sig + 72 + i] = pp[i];
+  // unaligned 16-byte stores (the datagram rows sit at any byte offset)
+  copy16_any(pk + kShredHeadBytes, dd, dlen, lane);
+  copy16_any(pk + o_sig, c.sig + 64 * h, 64, lane);
+  copy16_any(pk + o_sig + 72, c.proof + t * c.proof_stride, 32 * plen, lane);
 }
 
 }  // namespace
