@@ -102,11 +102,17 @@ __device__ __forceinline__ void load_digest(const uint8_t* src, uint32_t h[8]) {
 //   level h: thread (slice, j) hashes nodes[off + 2j], nodes[off + 2j + 1] (or EMPTY_ROOTS[h]
 //            past the end) into nodes[off + len + j]; the last level also writes the root
 //   proofs:  thread (slice, leaf) copies its siblings (create_proof)
-template <bool A4>
+// LIST: thread i hashes leaf list[i] for i < list[nslices * n_leaves] (hash_leaf compacted)
+template <bool A4, bool LIST = false>
 __global__ __launch_bounds__(256) void merkle_leaf_kernel(const MerkleBuildParams p, uint8_t* nodes,
                                                           uint64_t nodes_stride) {
-  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (t >= p.nslices * p.n_leaves) return;
+  uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if constexpr (LIST) {
+    if (t >= p.list[p.nslices * p.n_leaves]) return;
+    t = p.list[t];
+  } else {
+    if (t >= p.nslices * p.n_leaves) return;
+  }
   const uint64_t s = t / p.n_leaves, j = t - s * p.n_leaves;
   uint32_t h[8];
   leaf_hash<A4>(p.leaves + s * p.slice_stride + j * p.leaf_stride, p.leaf_bytes, h);
@@ -175,6 +181,8 @@ __global__ __launch_bounds__(256) void merkle_verify_kernel(const MerkleVerifyPa
   }
   uint32_t node[8];
   leaf_hash<A4>(p.leaves + t * p.leaf_stride, p.leaf_bytes, node);
+  if (p.leaf_nodes)
+    store_digest(p.leaf_nodes + (t / p.leaves_per_tree) * p.leaf_nodes_stride + 32 * (t % p.leaves_per_tree), node);
   uint32_t idx = p.index[t];
   const uint8_t* pr = p.proofs + t * p.proofs_stride;
   for (uint32_t h = 0; h < p.height; ++h) {
@@ -234,8 +242,18 @@ hipError_t launch_merkle_build(const MerkleBuildParams& p, uint8_t* nodes, uint6
   if ((p.nslices * p.n_leaves + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const bool a16 = (reinterpret_cast<uintptr_t>(p.leaves) | p.leaf_stride | p.slice_stride) % 16 == 0;
   const dim3 g0 = grid_of(p.nslices * p.n_leaves);
-  if (a16) hipLaunchKernelGGL((merkle_leaf_kernel<true>), g0, dim3(256), 0, stream, p, nodes, nodes_stride);
-  else hipLaunchKernelGGL((merkle_leaf_kernel<false>), g0, dim3(256), 0, stream, p, nodes, nodes_stride);
+  if (p.hash_leaf && p.list) {  // only the flagged leaves: compacted, so no lane idles on a known one
+    const uint64_t nl = p.nslices * p.n_leaves;
+    if (nl >= 0xFFFFFFFFull || hipMemsetAsync(p.list + nl, 0, 4, stream) != hipSuccess) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(compact_active_kernel, dim3(static_cast<unsigned>((nl + 1023) / 1024)), dim3(1024), 0, stream,
+                       p.hash_leaf, nl, p.list + nl, p.list);
+    if (a16) hipLaunchKernelGGL((merkle_leaf_kernel<true, true>), g0, dim3(256), 0, stream, p, nodes, nodes_stride);
+    else hipLaunchKernelGGL((merkle_leaf_kernel<false, true>), g0, dim3(256), 0, stream, p, nodes, nodes_stride);
+  } else if (a16) {
+    hipLaunchKernelGGL((merkle_leaf_kernel<true>), g0, dim3(256), 0, stream, p, nodes, nodes_stride);
+  } else {
+    hipLaunchKernelGGL((merkle_leaf_kernel<false>), g0, dim3(256), 0, stream, p, nodes, nodes_stride);
+  }
   uint32_t off = 0, len = p.n_leaves, height = 0;
   while (len > 1) {
     const uint32_t nlen = (len + 1) / 2;

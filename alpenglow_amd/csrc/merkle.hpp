@@ -26,6 +26,11 @@ struct MerkleBuildParams {
   uint8_t* roots;
   uint8_t* proofs;  // may be null
   uint64_t proofs_stride;
+  // nullable pair: hash only the leaves t (slice-major, t = slice * n_leaves + j) with
+  // hash_leaf[t] != 0, compacted into list (nslices * n_leaves + 1 words of scratch); the other
+  // leaves' digests must already be in nodes (a proof check's leaf_nodes, same bytes)
+  const uint8_t* hash_leaf;
+  uint32_t* list;
 };
 // nodes: the node digests (reference order, nodes_stride per slice; the caller's buffer or
 // scratch) -- the levels are built there.
@@ -50,6 +55,9 @@ struct MerkleVerifyParams {
   const uint8_t* active;  // nullable: leaves with active[t] == 0 are skipped (nothing written)
   uint32_t* list;         // nullable, n + 1 words of device scratch: with `active`, the active
                           // leaves are compacted first so that no lane idles on a skipped one
+  uint8_t* leaf_nodes;    // nullable: leaf t's digest also to leaf_nodes + (t / leaves_per_tree) *
+  uint64_t leaf_nodes_stride;  // leaf_nodes_stride + 32 (t % leaves_per_tree) (a later build's
+  uint32_t leaves_per_tree;    // level 0, launch_merkle_build's nodes layout)
 };
 hipError_t launch_merkle_verify(const MerkleVerifyParams& p, hipStream_t stream);
 

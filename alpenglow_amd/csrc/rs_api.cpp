@@ -179,7 +179,7 @@ struct ag_rs_ctx {
   hipEvent_t lens_ev = nullptr;             // recorded after its upload
   PinBuf h_strip;                           // coder deshred batches: pinned staging of the results
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
-  static constexpr int kPipeBufs = 25;
+  static constexpr int kPipeBufs = 27;
   DevBuf pipe[kPipeBufs];                   // composed shredder scratch (ag_shredder_*_batch)
   DevBuf d_sh_roots, d_sh_commit, d_sh_onvalid, d_sh_list;  // shred validation scratch
   DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
@@ -2376,7 +2376,8 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
                         const uint64_t* slots, const uint64_t* slice_indices, const uint8_t* is_last,
                         const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
                         const uint8_t* has_cached, uint32_t cached_group, const uint8_t* active, uint8_t* status,
-                        uint8_t* roots_out, uint8_t* commitments_out);
+                        uint8_t* roots_out, uint8_t* commitments_out, uint8_t* leaf_nodes = nullptr,
+                        size_t leaf_nodes_stride = 0, uint32_t leaves_per_tree = 0);
 }  // namespace
 
 int ag_ed25519_public_key_batch(ag_rs_ctx* c, size_t n, const uint8_t* seeds, uint8_t* pks) {
@@ -2459,7 +2460,8 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
                         const uint64_t* slots, const uint64_t* slice_indices, const uint8_t* is_last,
                         const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
                         const uint8_t* has_cached, uint32_t cached_group, const uint8_t* active, uint8_t* status,
-                        uint8_t* roots_out, uint8_t* commitments_out) {
+                        uint8_t* roots_out, uint8_t* commitments_out, uint8_t* leaf_nodes, size_t leaf_nodes_stride,
+                        uint32_t leaves_per_tree) {
   if (!c || n >= kMaxSigBatch || data_bytes >= (size_t{1} << 28) ||
       height > static_cast<size_t>(ag::kMerkleMaxHeight) ||
       (n && (!shred_index || !slots || !slice_indices || !is_last || !sigs || !pk || !status ||
@@ -2497,6 +2499,9 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
   mp.roots_out = roots;
   mp.active = active;
   mp.list = list;  // scratch until the signature list below reuses it (stream order)
+  mp.leaf_nodes = leaf_nodes;  // the leaf digests for a later Merkle rebuild over the same rows
+  mp.leaf_nodes_stride = leaf_nodes_stride;
+  mp.leaves_per_tree = leaves_per_tree;
   if (ag::launch_merkle_verify(mp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   // 2. SliceCommitment + cached-commitment rule (validated_shred.rs:57-64)
   AG_HIP(hipMemsetAsync(count, 0, 4, c->stream));
@@ -3105,9 +3110,14 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
     return st;
   if (ag::launch_pipe_cache_flags(pick, pstat, n, hasc, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   // ... then every shred against its slice's commitment (signature only without a cache)
+  // (each checked shred's leaf digest goes to the Merkle rebuild's level 0: step 5 hashes only
+  // the rows the coder restores or may rewrite)
+  const size_t nodes_stride = (32 * ag_merkle_node_count(ag::kPipeShreds) + 255) / 256 * 256;
+  if ((st = c->d_merkle_nodes.ensure(n * nodes_stride, c->stream))) return st;
+  uint8_t* nodes = c->d_merkle_nodes.as<uint8_t>();
   if ((st = shred_validate_impl(c, N, codewords, S, S, cols.shred_index, proof, kPipeProofBytes, ag::kPipeHeight,
                                 cols.slot, cols.slice_index, last, sig, 64, pk, commits, hasc, ag::kPipeShreds, plaus,
-                                vstat, roots, nullptr)))
+                                vstat, roots, nullptr, nodes, nodes_stride, ag::kPipeShreds)))
     return st;
   // 3. per slice: the shreds kept, the root, header and signature
   uint8_t* per_slice;
@@ -3159,10 +3169,31 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
       return st;
   }
   // 5. check_merkle_tree: the rebuilt tree's root must be the signed one; its paths serve
-  //    the reconstructed datagrams
-  if ((st = ag_merkle_build_batch(c, ag::kPipeShreds, S, n, codewords, S, cw_stride, roots2, nullptr, 0, proof,
-                                  ag::kPipeShreds * kPipeProofBytes)))
-    return st;
+  //    the reconstructed datagrams.  Kept shreds the coder left as received reuse the digests
+  //    their proof check computed (same bytes); restored rows, and coding rows the re-encode
+  //    may have rewritten, are hashed again.
+  {
+    uint8_t *lflags, *llist;
+    if ((st = pipe_buf(c, 25, N, &lflags)) || (st = pipe_buf(c, 26, 4 * (N + 1), &llist)) ||
+        (st = ensure_empty_roots(c)))
+      return st;
+    // the host coder path (shreds not whole 64-byte chunks) re-encodes every coding shred
+    if (ag::launch_pipe_leaf_flags(d_present, n, S % 64 != 0, lflags, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    ag::MerkleBuildParams mb{};
+    mb.leaves = codewords;
+    mb.leaf_stride = S;
+    mb.slice_stride = cw_stride;
+    mb.leaf_bytes = static_cast<uint32_t>(S);
+    mb.n_leaves = ag::kPipeShreds;
+    mb.nslices = n;
+    mb.empty_roots = c->d_empty_roots.as<uint32_t>();
+    mb.roots = roots2;
+    mb.proofs = proof;
+    mb.proofs_stride = ag::kPipeShreds * kPipeProofBytes;
+    mb.hash_leaf = lflags;
+    mb.list = reinterpret_cast<uint32_t*>(llist);
+    if (ag::launch_merkle_build(mb, nodes, nodes_stride, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
   uint8_t* same = pstat;  // first validation's statuses are dead
   if (ag::launch_pipe_root_cmp(roots2, sroot, n, same, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   std::vector<uint8_t> h_same(n);

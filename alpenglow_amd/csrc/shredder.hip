@@ -223,6 +223,21 @@ __global__ __launch_bounds__(256) void pipe_store_mask_kernel(const uint8_t* __r
   strip[s] = (few[s] & 1) ? err_few : len < 0 ? err_padding : len;
 }
 
+// Rebuild leaves of the composed deshred's check_merkle_tree: leaf (s, j) is hashed again iff
+// shred j of slice s was not kept (restored by the decode), or it is a coding shred the coder
+// may have rewritten (all: a slice with surplus shreds, or every slice when reencode_all).  The
+// kept rows are the bytes the proof check hashed.
+__global__ __launch_bounds__(256) void pipe_leaf_flags_kernel(const uint64_t* __restrict__ present, uint64_t n,
+                                                              uint32_t reencode_all, uint8_t* __restrict__ flags) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= n * kPipeShreds) return;
+  const uint64_t s = t / kPipeShreds;
+  const uint32_t j = static_cast<uint32_t>(t - s * kPipeShreds);
+  const uint64_t pr = present[s];
+  const bool coding_rewritten = reencode_all || __builtin_popcountll(pr) > static_cast<int>(kPipeData);
+  flags[t] = (!((pr >> j) & 1) || (j >= kPipeData && coding_rewritten)) ? 1 : 0;
+}
+
 }  // namespace
 
 hipError_t launch_pipe_expand(const PipeExpandParams& p, hipStream_t stream) {
@@ -292,6 +307,14 @@ hipError_t launch_pipe_store_masks(const uint8_t* few, int64_t* strip, const uin
   if (nslices == 0) return hipSuccess;
   hipLaunchKernelGGL(pipe_store_mask_kernel, grid256(nslices), dim3(256), 0, stream, few, strip, present, wps, nslices,
                      mask, err_few, err_padding);
+  return hipGetLastError();
+}
+
+hipError_t launch_pipe_leaf_flags(const uint64_t* present, uint64_t nslices, bool reencode_all, uint8_t* flags,
+                                  hipStream_t stream) {
+  if (nslices == 0) return hipSuccess;
+  hipLaunchKernelGGL(pipe_leaf_flags_kernel, grid256(nslices * kPipeShreds), dim3(256), 0, stream, present, nslices,
+                     reencode_all ? 1u : 0u, flags);
   return hipGetLastError();
 }
 

@@ -113,4 +113,10 @@ hipError_t launch_pipe_store_masks(const uint8_t* few, int64_t* strip, const uin
                                    uint64_t nslices, uint64_t* mask, int64_t err_few, int64_t err_padding,
                                    hipStream_t stream);
 
+// flags[64 s + j] = 1: leaf j of slice s is hashed again by the deshred's Merkle rebuild (shred
+// not kept, or a coding shred the coder may have rewritten: surplus slices, or all with
+// reencode_all); 0: its digest from the proof check stands.
+hipError_t launch_pipe_leaf_flags(const uint64_t* present, uint64_t nslices, bool reencode_all, uint8_t* flags,
+                                  hipStream_t stream);
+
 }  // namespace ag
