@@ -162,7 +162,7 @@ struct ag_rs_ctx {
   DevBuf d_x128, d_rows128;                 // W = 128 two-pass decode: masks, constants
   uint64_t last_classes[16] = {};           // patterns per decoder class of the last decode call
   int decode_depth = 0;                     // decode_device nesting (tail restrides decode inside)
-  uint32_t last_encode_kernels = 0;         // EncodeKernelBit of the last ag_rs_encode_batch call
+  uint32_t last_encode_kernels = 0;         // EncodeKernelBit of the last ag_rs_encode_batch / coder deshred batch
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
   DevBuf d_corr, d_corrk, d_corrblocks;     // correction decoder: patterns, K picks, block ids
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
@@ -171,6 +171,7 @@ struct ag_rs_ctx {
   DevBuf d_slice_meta;                           // slice framing / parsing metadata
   DevBuf stage_pad, stage_mask;                  // restrided shards (sizes not whole 64-byte chunks)
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
+  DevBuf d_reenc_mask;                      // uniform coder deshreds: the re-encode's store mask word
   DevBuf d_pipe_few, d_pipe_mask;           // composed deshred: too-few flags, re-encode store masks
   DevBuf d_present;                         // coder batches: per-slice present masks
   PinBuf h_present;                         // their pinned host staging
@@ -301,7 +302,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_x128, &d_rows128, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_x128, &d_rows128, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_reenc_mask, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
                       &one_out, &d_pipe_few, &d_pipe_mask, &d_present})
       b->release();
     for (DevBuf& b : pipe) b.release();
@@ -2242,6 +2243,23 @@ int coder_deshred_uniform(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_t* c
   // re-encode (encode_coding_from_data) the runs of slices that stripped; skipped when the
   // present shreds are exactly the 32 coding shreds (the re-encode reproduces them)
   if (m == kDataShreds && nd == 0 && nc == m) return AG_RS_OK;
+  // LowRate 32:64 (CodingOnly) with exactly 32 kept shreds: the codeword is unique, so the
+  // re-encode reproduces every kept coding shred.  When the absent ones all lie in one 32-shard
+  // recovery chunk (the reference bench's shape: coding 32..63 kept), only that chunk is
+  // encoded -- one 32-point transform under a store mask of its absent shreds instead of the
+  // two-chunk 64-point one
+  int lone = -1;
+  if (m == 2 * kDataShreds && nd + nc == kDataShreds && S % 64 == 0 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
+    const uint64_t absent = ~pack_flags(cpres, m);
+    const uint64_t lo = absent & 0xFFFFFFFFull, hi = absent >> 32;
+    if (lo == 0 || hi == 0) {
+      lone = lo == 0 ? 1 : 0;
+      const uint64_t w = lo == 0 ? hi : lo;
+      if ((st = c->d_reenc_mask.ensure(8, c->stream))) return st;
+      AG_HIP(hipMemsetD32Async(c->d_reenc_mask.ptr, static_cast<int>(static_cast<uint32_t>(w)), 1, c->stream));
+      AG_HIP(hipMemsetD32Async(c->d_reenc_mask.as<uint32_t>() + 1, 0, 1, c->stream));
+    }
+  }
   for (size_t b = 0; b < n;) {
     if (out[b] < 0) {
       ++b;
@@ -2249,9 +2267,25 @@ int coder_deshred_uniform(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_t* c
     }
     size_t e = b;
     while (e < n && out[e] >= 0) ++e;
-    if ((st = encode_device(c, kDataShreds, m, S, e - b, cw + b * cw_stride, cw_stride, rec + b * cw_stride,
-                            cw_stride)))
+    if (lone >= 0) {
+      ag::XformParams p{};
+      p.in = cw + b * cw_stride;
+      p.in_block_stride = cw_stride;
+      p.in_shard_stride = S;
+      p.out = rec + b * cw_stride + static_cast<size_t>(lone) * 32 * S;
+      p.out_block_stride = cw_stride;
+      p.out_shard_stride = S;
+      p.out_mask = c->d_reenc_mask.as<uint64_t>();
+      p.n_in = static_cast<uint32_t>(kDataShreds);
+      p.n_out = 32;
+      p.chunks_per_shard = static_cast<uint32_t>(S / 64);
+      p.total_columns = static_cast<uint64_t>(e - b) * (S / 64);
+      c->last_encode_kernels |= ag::kEkLowRate;
+      if (ag::launch_xform_lowrate(32, static_cast<unsigned>(lone), p, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    } else if ((st = encode_device(c, kDataShreds, m, S, e - b, cw + b * cw_stride, cw_stride, rec + b * cw_stride,
+                                   cw_stride))) {
       return st;
+    }
     b = e;
   }
   AG_HIP(hipStreamSynchronize(c->stream));
@@ -2270,6 +2304,7 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   if (n == 0) return AG_RS_OK;
   int st = c->enter();
   if (st) return st;
+  c->last_encode_kernels = 0;  // the re-encode's kernels (test aid)
   // One pattern for the whole batch (a repair batch; the reference bench's shape): one
   // pattern word on the host, no per-slice bookkeeping past the strip results.
   bool uniform = true;

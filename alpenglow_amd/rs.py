@@ -381,8 +381,8 @@ ENCODE_KERNELS = ("xform4", "xform8", "xform_h8", "encode_mc", "lowrate", "lowra
 
 
 def last_encode_kernels(ctx: Context) -> set:
-    """The encode kernels the last ``encode_batch`` on ``ctx`` launched (test aid; the bits of
-    ``ag::EncodeKernelBit``, rs_launch.hpp)."""
+    """The encode kernels the last ``encode_batch`` or ``coder_deshred_batch`` (its re-encode) on
+    ``ctx`` launched (test aid; the bits of ``ag::EncodeKernelBit``, rs_launch.hpp)."""
     out = ctypes.c_uint32(0)
     _check(load().ag_rs_internal_last_encode_kernels(ctx.handle, ctypes.byref(out)), "last_encode_kernels")
     return {name for i, name in enumerate(ENCODE_KERNELS) if out.value >> i & 1}

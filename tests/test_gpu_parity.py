@@ -777,6 +777,63 @@ def test_coder_deshred_batch(ctx, dev, S, mode, m):
         assert host[b, 32 * S:].tobytes() == b"".join(raw.coding)
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("S", [1024, 128])
+@pytest.mark.parametrize("keep,kernels", [
+    (set(range(64, 96)), {"lowrate"}),                            # coding 32..63 (the reference bench)
+    (set(range(32, 64)), {"lowrate"}),                            # coding 0..31
+    (set(range(16)) | set(range(32, 48)), {"lowrate2"}),          # absent shreds in both chunks
+    (set(range(8)) | set(range(72, 96)), {"lowrate2"}),
+])
+def test_coder_deshred_uniform_lowrate_chunks(ctx, dev, S, keep, kernels):
+    """CodingOnlyShredder's coder (LowRate 32:64) with one pattern for the batch and exactly 32
+    kept shreds: the codeword is unique, so the re-encode only needs the absent coding shreds;
+    when they all lie in one 32-shard recovery chunk that chunk alone is encoded (one 32-point
+    transform, store mask of the absent shreds), else both (the two-chunk kernel).  Against the
+    oracle's ReedSolomonCoder::deshred (reed_solomon.rs:140-208); absent shreds hold garbage,
+    one slice has an invalid padding (its coding shreds stay as received)."""
+    m, n = 64, 6
+    stride = (32 + m) * S
+    rng = random.Random(S + len(keep))
+    lens = _payload_lens(rng, S, n)
+    cw = np.zeros((n, stride), np.uint8)
+    for b in range(n):
+        if b == 3:  # random data without a padding marker
+            data = bytearray(o.splitmix64_bytes(330 + S, 32 * S))
+            data[-1] = 0x11
+            cw[b, :32 * S] = np.frombuffer(bytes(data), np.uint8)
+            cw[b, 32 * S:] = np.frombuffer(b"".join(o.encode([bytes(data[i * S:(i + 1) * S]) for i in range(32)], m)),
+                                           np.uint8)
+            continue
+        raw = o.coder_shred(o.splitmix64_bytes(4400 + b + S, lens[b]), m)
+        cw[b] = np.frombuffer(b"".join(raw.data) + b"".join(raw.coding), np.uint8)
+    damaged = cw.copy()
+    for b in range(n):
+        for i in range(32 + m):
+            if i not in keep:
+                damaged[b, i * S:(i + 1) * S] = (0x3C + i) & 0xFF
+    dp = [1 if i in keep else 0 for _ in range(n) for i in range(32)]
+    cp = [1 if 32 + j in keep else 0 for _ in range(n) for j in range(m)]
+    d_cw = to_dev(damaged, dev)
+    res = rs.coder_deshred_batch(ctx, m, n, S, d_cw, stride, dp, cp, rs.DECODE_ANY_K)
+    assert rs.last_encode_kernels(ctx) == kernels
+    host = d_cw.cpu().numpy()
+    for b in range(n):
+        orig_b = {i: cw[b, i * S:(i + 1) * S].tobytes() for i in range(32) if i in keep}
+        rec_b = {j: cw[b, (32 + j) * S:(33 + j) * S].tobytes() for j in range(m) if 32 + j in keep}
+        try:
+            payload, raw = o.coder_deshred_indexed(orig_b, rec_b, m)
+        except o.RSError as err:
+            assert b == 3 and res[b] == err.kind, (b, res[b], err.kind)
+            for j in range(m):
+                if 32 + j in keep:
+                    assert host[b, (32 + j) * S:(33 + j) * S].tobytes() == damaged[b, (32 + j) * S:(33 + j) * S].tobytes()
+            continue
+        assert res[b] == len(payload), (b, res[b])
+        assert host[b, :32 * S].tobytes() == b"".join(raw.data), b
+        assert host[b, 32 * S:].tobytes() == b"".join(raw.coding), b
+
+
 @pytest.mark.parametrize("mode", [rs.DECODE_ANY_K, rs.DECODE_EXACT])
 def test_coder_deshred_fused_coding_restore(ctx, dev, mode):
     """The follower's deshred at exactly k = 32 kept shreds (slot_block_data.rs:343-355): the
