@@ -78,22 +78,44 @@ __global__ __launch_bounds__(256) void shred_commit_kernel(const ShredCommitPara
     p.status[t] = kShredInvalidSignature;
     return;
   }
-  uint8_t c[kSliceCommitmentLen];
+  static_assert(kSliceCommitmentLen == 49, "slot | slice_index | is_last | root");
+  // the 49 commitment bytes as 12 little-endian words + 1 byte: slot, slice index, then
+  // is_last and the root shifted up one byte (v_alignbyte); rows of 49 bytes take unaligned
+  // 16-byte accesses (byte loops cost ~130 memory instructions per shred)
+  uint32_t w[12];
   const uint64_t slot = p.slots[t], si = p.slice_indices[t];
-  for (int i = 0; i < 8; ++i) {
-    c[i] = static_cast<uint8_t>(slot >> (8 * i));
-    c[8 + i] = static_cast<uint8_t>(si >> (8 * i));
+  w[0] = static_cast<uint32_t>(slot);
+  w[1] = static_cast<uint32_t>(slot >> 32);
+  w[2] = static_cast<uint32_t>(si);
+  w[3] = static_cast<uint32_t>(si >> 32);
+  uint32_t r[8];
+  if ((reinterpret_cast<uintptr_t>(p.roots) & 15) == 0) {
+    const uint4 a = *reinterpret_cast<const uint4*>(p.roots + 32 * t);
+    const uint4 b = *reinterpret_cast<const uint4*>(p.roots + 32 * t + 16);
+    r[0] = a.x; r[1] = a.y; r[2] = a.z; r[3] = a.w;
+    r[4] = b.x; r[5] = b.y; r[6] = b.z; r[7] = b.w;
+  } else {
+    for (int i = 0; i < 8; ++i) {
+      const uint8_t* q = p.roots + 32 * t + 4 * i;
+      r[i] = q[0] | (uint32_t{q[1]} << 8) | (uint32_t{q[2]} << 16) | (uint32_t{q[3]} << 24);
+    }
   }
-  c[16] = p.is_last[t] ? 1 : 0;
-  for (int i = 0; i < 32; ++i) c[17 + i] = p.roots[32 * t + i];
+  w[4] = (p.is_last[t] ? 1u : 0u) | (r[0] << 8);
+  for (int k = 1; k < 8; ++k) w[4 + k] = __builtin_amdgcn_alignbyte(r[k], r[k - 1], 3);
+  const uint8_t last = static_cast<uint8_t>(r[7] >> 24);
   uint8_t* out = p.commitments + kSliceCommitmentLen * t;
-  for (uint32_t i = 0; i < kSliceCommitmentLen; ++i) out[i] = c[i];
+  for (int q = 0; q < 3; ++q)
+    *reinterpret_cast<uint4*>(out + 16 * q) = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+  out[48] = last;
   const uint64_t ci = p.cached_group > 1 ? t / p.cached_group : t;
   const bool cached = p.cached && p.has_cached && p.has_cached[ci];
   if (cached) {
     const uint8_t* cc = p.cached + kSliceCommitmentLen * ci;
-    uint32_t diff = 0;
-    for (uint32_t i = 0; i < kSliceCommitmentLen; ++i) diff |= c[i] ^ cc[i];
+    uint32_t diff = static_cast<uint32_t>(cc[48] ^ last);
+    for (int q = 0; q < 3; ++q) {
+      const uint4 x = *reinterpret_cast<const uint4*>(cc + 16 * q);
+      diff |= (x.x ^ w[4 * q]) | (x.y ^ w[4 * q + 1]) | (x.z ^ w[4 * q + 2]) | (x.w ^ w[4 * q + 3]);
+    }
     if (diff == 0) {  // validated_shred.rs:62-64: same commitment, no signature check
       p.status[t] = kShredOk;
       return;
