@@ -154,15 +154,17 @@ __global__ __launch_bounds__(256) void shred_serialize_kernel(const ShredColumns
   }
   const uint64_t h = c.hdr_group > 1 ? t / c.hdr_group : t;  // header row
   if (lane == 0) {
-    const uint32_t kind = c.kind[t];
-    pk[0] = static_cast<uint8_t>(kind);
-    pk[1] = pk[2] = pk[3] = 0;
-    st_u64(pk + 4, c.slot[h]);
-    st_u64(pk + 12, c.slice_index[h]);
-    pk[20] = c.is_last[h] ? 1 : 0;
-    st_u64(pk + 21, c.shred_index[t]);
-    st_u64(pk + 29, dlen);
-    st_u64(pk + o_sig + 64, plen);
+    // the 37 header bytes as words (unaligned 16-, 4- and 1-byte stores) and the proof length
+    // as 8 bytes: 5 store instructions where byte stores took 45
+    const uint64_t slot = c.slot[h], si = c.slice_index[h];
+    const uint32_t idx = c.shred_index[t], last = c.is_last[h] ? 1u : 0u;
+    *reinterpret_cast<uint4*>(pk) = make_uint4(c.kind[t], static_cast<uint32_t>(slot),
+                                               static_cast<uint32_t>(slot >> 32), static_cast<uint32_t>(si));
+    *reinterpret_cast<uint4*>(pk + 16) = make_uint4(static_cast<uint32_t>(si >> 32), last | (idx << 8), idx >> 24,
+                                                    dlen << 8);  // idx and dlen as u64: high bytes 0
+    *reinterpret_cast<uint32_t*>(pk + 32) = dlen >> 24;
+    pk[36] = 0;
+    *reinterpret_cast<uint2*>(pk + o_sig + 64) = make_uint2(plen, 0);
     packet_lens[t] = o_sig + 72 + 32 * plen;
   }
   const uint8_t* dd = c.data + t * c.data_stride;
