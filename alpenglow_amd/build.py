@@ -29,7 +29,7 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc" if os.path.exists("/opt/ro
 CXX = os.environ.get("CXX_HOST", "g++")
 
 SOURCES = ["rs_kernels.hip", "rs_xform64.hip", "rs_decode_c.hip", "merkle.hip", "cipher.hip", "ed25519.hip", "wire.hip", "slice.hip", "shredder.hip", "rs_api.cpp", "rs_patterns.cpp", "gf16.cpp"]
-HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_xform.hpp", "rs_launch.hpp", "rs_consts.inc", "rs_patterns.hpp", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp", "slice.hpp", "shredder.hpp"]
+HEADERS = ["gf16.hpp", "rs_device.hpp", "rs_xform.hpp", "rs_launch.hpp", "rs_consts.inc", "rs_patterns.hpp", "merkle.hpp", "sha256.hpp", "cipher.hpp", "ed25519.hpp", "ed25519_core.hpp", "wire.hpp", "slice.hpp", "shredder.hpp", "unaligned.hpp"]
 # -fno-slp-vectorize: the SLP vectoriser packs the bitsliced XOR networks into <2 x i32>
 # ops, which lengthens live ranges (measured +40 VGPRs on the transform kernel).
 # -amdgpu-promote-alloca-to-vector-limit: keeps the four-Russians tables of decode_x and

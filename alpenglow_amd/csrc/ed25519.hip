@@ -23,6 +23,7 @@
 #include <cstdlib>
 
 #include "ed25519.hpp"
+#include "unaligned.hpp"
 #include "ed25519_core.hpp"
 
 namespace ag {
@@ -105,7 +106,7 @@ __global__ __launch_bounds__(256) void shred_commit_kernel(const ShredCommitPara
   const uint8_t last = static_cast<uint8_t>(r[7] >> 24);
   uint8_t* out = p.commitments + kSliceCommitmentLen * t;
   for (int q = 0; q < 3; ++q)
-    *reinterpret_cast<uint4*>(out + 16 * q) = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+    st16u(out + 16 * q, make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]));
   out[48] = last;
   const uint64_t ci = p.cached_group > 1 ? t / p.cached_group : t;
   const bool cached = p.cached && p.has_cached && p.has_cached[ci];
@@ -113,7 +114,7 @@ __global__ __launch_bounds__(256) void shred_commit_kernel(const ShredCommitPara
     const uint8_t* cc = p.cached + kSliceCommitmentLen * ci;
     uint32_t diff = static_cast<uint32_t>(cc[48] ^ last);
     for (int q = 0; q < 3; ++q) {
-      const uint4 x = *reinterpret_cast<const uint4*>(cc + 16 * q);
+      const uint4 x = ld16u(cc + 16 * q);
       diff |= (x.x ^ w[4 * q]) | (x.y ^ w[4 * q + 1]) | (x.z ^ w[4 * q + 2]) | (x.w ^ w[4 * q + 3]);
     }
     if (diff == 0) {  // validated_shred.rs:62-64: same commitment, no signature check

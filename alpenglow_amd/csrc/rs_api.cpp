@@ -197,6 +197,7 @@ struct ag_rs_ctx {
   hipStream_t server_stream = nullptr;
   uint32_t server_seq = 0;
   bool server_broken = false;  // a job timed out: the server path is off for this context
+  bool fail_next_server_job = false;  // test aid: the next server job takes the timeout path
   std::vector<PinBuf> abandoned_pins;  // staging a timed-out job named (freed once the server is gone)
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
   std::vector<uint64_t> stage_mask_host;  // last restride masks uploaded to stage_mask
@@ -1276,6 +1277,14 @@ int ag_rs_internal_last_decode_classes(ag_rs_ctx* c, uint64_t* out16) {
 
 // Test aid (not in the header): the encode kernels (ag::EncodeKernelBit) the last
 // ag_rs_encode_batch call on this context launched.
+// Test aid (not in the header): the context's next per-call server job takes the timeout path
+// (retired, staging abandoned, server path off) without waiting 5 s.
+int ag_rs_internal_fail_next_server_job(ag_rs_ctx* c) {
+  if (!c) return AG_RS_ERR_INVALID_ARGUMENT;
+  c->fail_next_server_job = true;
+  return AG_RS_OK;
+}
+
 int ag_rs_internal_last_encode_kernels(ag_rs_ctx* c, uint32_t* out) {
   if (!c || !out) return AG_RS_ERR_INVALID_ARGUMENT;
   *out = c->last_encode_kernels;
@@ -1709,6 +1718,22 @@ int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t m
     c->mb_dev = static_cast<ag::LatencyMailbox*>(d);
   }
   ag::LatencyMailbox* mb = c->mb;
+  // Retire a job that did not complete: a queued or slow server that wakes later finds a quit
+  // job instead.  It may already be inside the job, so the staging buffer the job names is
+  // abandoned (kept allocated, never reused: `stage` is left empty, and the encoder / decoder
+  // that owned it drops its received shards, see pin_lost) and later calls take the launch path.
+  auto retire = [&]() {
+    c->server_broken = true;
+    mb->kind = ag::kJobQuit;
+    __atomic_store_n(&mb->doorbell, ++c->server_seq, __ATOMIC_RELEASE);
+    c->abandoned_pins.push_back(stage);
+    stage = PinBuf{};
+    return AG_RS_ERR_DEVICE;
+  };
+  if (c->fail_next_server_job) {
+    c->fail_next_server_job = false;
+    return retire();
+  }
   mb->kind = kind;
   mb->mask = mask;
   std::memcpy(static_cast<void*>(&mb->p), &p, sizeof p);
@@ -1726,17 +1751,8 @@ int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t m
         return AG_RS_ERR_DEVICE;
       }
     }
-    if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-      // Retire the job: a queued or slow server that wakes later finds a quit job instead.
-      // It may already be inside the job, so the staging buffer the job names is abandoned
-      // (kept allocated, never reused) and later calls take the launch path.
-      c->server_broken = true;
-      mb->kind = ag::kJobQuit;
-      __atomic_store_n(&mb->doorbell, ++c->server_seq, __ATOMIC_RELEASE);
-      c->abandoned_pins.push_back(stage);
-      stage = PinBuf{};
-      return AG_RS_ERR_DEVICE;
-    }
+    if ((spins & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5))
+      return retire();
     __builtin_ia32_pause();
   }
 }
@@ -1845,8 +1861,21 @@ int ag_rs_encoder_new_on_device(int device, size_t k, size_t m, size_t S, ag_rs_
   return AG_RS_OK;
 }
 
+// A server job that timed out abandoned the object's staging (server_job: `stage` left
+// empty): the shards it held are gone, so the object starts a new round in a fresh buffer.
+static int encoder_pin_lost(ag_rs_encoder* e) {
+  e->received = 0;
+  e->encoded = false;
+  int st = e->ctx->enter();
+  return st ? st : e->pin.ensure((e->k + e->m) * e->S);
+}
+
 int ag_rs_encoder_add_original_shard(ag_rs_encoder* e, const uint8_t* shard, size_t len) {
   if (!e || (!shard && len)) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (!e->pin.ptr) {
+    const int st = encoder_pin_lost(e);
+    if (st) return st;
+  }
   if (e->encoded) {  // the crate resets the received set once a result is dropped
     e->received = 0;
     e->encoded = false;
@@ -1860,9 +1889,14 @@ int ag_rs_encoder_add_original_shard(ag_rs_encoder* e, const uint8_t* shard, siz
 
 int ag_rs_encoder_encode(ag_rs_encoder* e) {
   if (!e) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (!e->pin.ptr) e->received = 0;  // staging abandoned by a timed-out job: nothing received
   if (e->received != e->k) return AG_RS_ERR_TOO_FEW_ORIGINAL_SHARDS;
   const int st = run_one_encode(e->ctx, e->k, e->m, e->S, e->pin);
-  if (st) return st;
+  if (st) {
+    if (!e->pin.ptr) e->received = 0;
+    e->encoded = false;
+    return st;
+  }
   e->encoded = true;
   return AG_RS_OK;
 }
@@ -1923,6 +1957,17 @@ int ag_rs_decoder_new_on_device(int device, size_t k, size_t m, size_t S, ag_rs_
   return AG_RS_OK;
 }
 
+// The decoder's counterpart of encoder_pin_lost: every received shard is dropped.
+static int decoder_pin_lost(ag_rs_decoder* d) {
+  std::fill(d->opres.begin(), d->opres.end(), 0);
+  std::fill(d->rpres.begin(), d->rpres.end(), 0);
+  std::fill(d->restored.begin(), d->restored.end(), 0);
+  d->no = d->nr = 0;
+  d->decoded = false;
+  int st = d->ctx->enter();
+  return st ? st : d->pin.ensure((d->k + 2 * d->m) * d->S);
+}
+
 static void decoder_begin_round(ag_rs_decoder* d) {
   if (!d->decoded) return;
   std::fill(d->opres.begin(), d->opres.end(), 0);
@@ -1934,6 +1979,10 @@ static void decoder_begin_round(ag_rs_decoder* d) {
 
 int ag_rs_decoder_add_original_shard(ag_rs_decoder* d, size_t index, const uint8_t* shard, size_t len) {
   if (!d || (!shard && len)) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (!d->pin.ptr) {
+    const int st = decoder_pin_lost(d);
+    if (st) return st;
+  }
   decoder_begin_round(d);
   if (index >= d->k) return AG_RS_ERR_INVALID_ORIGINAL_SHARD_INDEX;
   if (d->opres[index]) return AG_RS_ERR_DUPLICATE_ORIGINAL_SHARD_INDEX;
@@ -1946,6 +1995,10 @@ int ag_rs_decoder_add_original_shard(ag_rs_decoder* d, size_t index, const uint8
 
 int ag_rs_decoder_add_recovery_shard(ag_rs_decoder* d, size_t index, const uint8_t* shard, size_t len) {
   if (!d || (!shard && len)) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (!d->pin.ptr) {
+    const int st = decoder_pin_lost(d);
+    if (st) return st;
+  }
   decoder_begin_round(d);
   if (index >= d->m) return AG_RS_ERR_INVALID_RECOVERY_SHARD_INDEX;
   if (d->rpres[index]) return AG_RS_ERR_DUPLICATE_RECOVERY_SHARD_INDEX;
@@ -1958,13 +2011,20 @@ int ag_rs_decoder_add_recovery_shard(ag_rs_decoder* d, size_t index, const uint8
 
 int ag_rs_decoder_decode(ag_rs_decoder* d) {
   if (!d) return AG_RS_ERR_INVALID_ARGUMENT;
+  if (!d->pin.ptr) {  // staging abandoned by a timed-out job: nothing received
+    const int st = decoder_pin_lost(d);
+    if (st) return st;
+  }
   if (d->no + d->nr < d->k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
   std::fill(d->restored.begin(), d->restored.end(), 0);
   if (d->no < d->k) {
     // exact crate semantics: decode from every present shard
     const int st = run_one_decode(d->ctx, d->k, d->m, d->S, d->pin, d->opres.data(), d->rpres.data(),
                                   AG_RS_DECODE_EXACT, false, nullptr);
-    if (st) return st;
+    if (st) {
+      if (!d->pin.ptr) (void)decoder_pin_lost(d);
+      return st;
+    }
     for (size_t i = 0; i < d->k; ++i) d->restored[i] = d->opres[i] ? 0 : 1;
   }
   d->decoded = true;
@@ -3207,6 +3267,15 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   //    the reconstructed datagrams.  Kept shreds the coder left as received reuse the digests
   //    their proof check computed (same bytes); restored rows, and coding rows the re-encode
   //    may have rewritten, are hashed again.
+  //    Invariant the reuse depends on: present ⊆ active ∧ proof-ok.  Every kept
+  //    shred (a bit of d_present, set by pipe_check only for shreds that were active in the
+  //    step-3 verify and whose derived root matched) had its leaf digest written to
+  //    d_merkle_nodes at (slice, index) by that verify; nothing between step 3 and here writes
+  //    those rows of the codeword or those nodes (the coder stage touches only absent rows
+  //    and, per the store masks, coding rows the leaf flags mark for re-hashing).  The verify
+  //    also stores digests of rows it then rejects: those rows are not in d_present, so the
+  //    flags below re-hash or ignore them.  A new step in between that writes kept rows or
+  //    d_merkle_nodes must clear the matching present bits or re-hash.
   {
     uint8_t *lflags, *llist;
     if ((st = pipe_buf(c, 25, N, &lflags)) || (st = pipe_buf(c, 26, 4 * (N + 1), &llist)) ||

@@ -1997,6 +1997,9 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
   if (W == 64 && pass == 0) {
     if (p.rows_w != 64) return hipErrorInvalidValue;
     const bool packed = pl && p.any_k && p.chunks_per_shard == 16 && (p.low_rate || p.chunk == 32);
+    // fused coding restore: the caller's patterns restore absent coding positions too and skip
+    // those slices in the re-encode, which only decode_pk<-1> honours
+    if (p.fuse && (!packed || p.low_rate)) return hipErrorInvalidValue;
     if (packed) {
       if (p.low_rate) hipLaunchKernelGGL((decode_pk_kernel<0>), g32, dim3(512), 0, stream, p);
       else if (p.fuse) hipLaunchKernelGGL((decode_pk_kernel<-1>), g32, dim3(512), 0, stream, p);

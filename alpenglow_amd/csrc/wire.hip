@@ -18,6 +18,7 @@
 
 #include <cstdint>
 
+#include "unaligned.hpp"
 #include "wire.hpp"
 
 namespace ag {
@@ -45,7 +46,7 @@ __device__ __forceinline__ void shift_words(uint32_t* __restrict__ dw, const uin
                                             uint32_t sh, int lane) {
   for (uint32_t w = 4 * lane; w < nw; w += 256) {
     if (w + 4 <= nw) {
-      const uint4 x = *reinterpret_cast<const uint4*>(sw + w);
+      const uint4 x = ld16u(sw + w);
       uint4 o = x;
       if (sh) {
         const uint32_t e = sw[w + 4];
@@ -54,7 +55,7 @@ __device__ __forceinline__ void shift_words(uint32_t* __restrict__ dw, const uin
         o.z = __builtin_amdgcn_alignbyte(x.w, x.z, sh);
         o.w = __builtin_amdgcn_alignbyte(e, x.w, sh);
       }
-      *reinterpret_cast<uint4*>(dw + w) = o;
+      st16u(dw + w, o);
     } else {
       for (uint32_t v = w; v < nw; ++v) dw[v] = sh ? __builtin_amdgcn_alignbyte(sw[v + 1], sw[v], sh) : sw[v];
     }
@@ -76,7 +77,7 @@ __device__ __forceinline__ void copy16_any(uint8_t* __restrict__ dst, const uint
                                            int lane) {
   const uint32_t n16 = len >> 4;
   for (uint32_t i = lane; i < n16; i += 64)
-    *reinterpret_cast<uint4*>(dst + 16 * i) = *reinterpret_cast<const uint4*>(src + 16 * i);
+    st16u(dst + 16 * i, ld16u(src + 16 * i));
   for (uint32_t i = 16 * n16 + lane; i < len; i += 64) dst[i] = src[i];
 }
 // the data rows are 4-byte aligned (every row, so word copies never leave a row)
@@ -158,13 +159,13 @@ __global__ __launch_bounds__(256) void shred_serialize_kernel(const ShredColumns
     // as 8 bytes: 5 store instructions where byte stores took 45
     const uint64_t slot = c.slot[h], si = c.slice_index[h];
     const uint32_t idx = c.shred_index[t], last = c.is_last[h] ? 1u : 0u;
-    *reinterpret_cast<uint4*>(pk) = make_uint4(c.kind[t], static_cast<uint32_t>(slot),
-                                               static_cast<uint32_t>(slot >> 32), static_cast<uint32_t>(si));
-    *reinterpret_cast<uint4*>(pk + 16) = make_uint4(static_cast<uint32_t>(si >> 32), last | (idx << 8), idx >> 24,
-                                                    dlen << 8);  // idx and dlen as u64: high bytes 0
-    *reinterpret_cast<uint32_t*>(pk + 32) = dlen >> 24;
+    st16u(pk, make_uint4(c.kind[t], static_cast<uint32_t>(slot), static_cast<uint32_t>(slot >> 32),
+                         static_cast<uint32_t>(si)));
+    st16u(pk + 16, make_uint4(static_cast<uint32_t>(si >> 32), last | (idx << 8), idx >> 24,
+                              dlen << 8));  // idx and dlen as u64: high bytes 0
+    st4u(pk + 32, dlen >> 24);
     pk[36] = 0;
-    *reinterpret_cast<uint2*>(pk + o_sig + 64) = make_uint2(plen, 0);
+    st8u(pk + o_sig + 64, make_uint2(plen, 0));
     packet_lens[t] = o_sig + 72 + 32 * plen;
   }
   const uint8_t* dd = c.data + t * c.data_stride;

@@ -170,6 +170,7 @@ def load():
     }
     sigs["ag_rs_internal_last_decode_classes"] = ([p, p], i)  # test aid, not in the header
     sigs["ag_rs_internal_last_encode_kernels"] = ([p, p], i)  # test aid, not in the header
+    sigs["ag_rs_internal_fail_next_server_job"] = ([p], i)  # test aid, not in the header
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
             continue              # check the shipped library exports everything
@@ -386,6 +387,12 @@ def last_encode_kernels(ctx: Context) -> set:
     out = ctypes.c_uint32(0)
     _check(load().ag_rs_internal_last_encode_kernels(ctx.handle, ctypes.byref(out)), "last_encode_kernels")
     return {name for i, name in enumerate(ENCODE_KERNELS) if out.value >> i & 1}
+
+
+def fail_next_server_job(ctx: Context):
+    """Test aid: the next per-call server job on ``ctx`` takes the timeout path (the job is
+    retired, its staging abandoned and the server path turned off for the context)."""
+    _check(load().ag_rs_internal_fail_next_server_job(ctx.handle), "fail_next_server_job")
 
 
 def fill_splitmix(ctx: Context, device_dst, nblocks: int, block_bytes: int, dst_block_stride: int,

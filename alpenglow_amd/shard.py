@@ -103,3 +103,108 @@ def erasure_patterns(plan: RankPlan, k: int, m: int, erased: int, lost_coding: i
         opres += [0 if i in lost else 1 for i in range(k)]
         rpres += [0 if j in lost_r else 1 for j in range(m)]
     return opres, rpres
+
+
+def gather_objects(obj, dist=None) -> list:
+    """``obj`` (any picklable value) of every rank, in rank order (per-rank sub-lines)."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+# ---- NUMA placement of a rank's host staging (SURVEY.md §8e: blocks arrive from the
+# disseminator in host memory, disseminator/rotor.rs:108-112, network/udp.rs:9-12) ----------
+
+def _sysfs_root() -> str:
+    import os
+
+    return os.environ.get("AG_SYSFS_ROOT", "/sys")
+
+
+def parse_cpulist(text: str) -> set:
+    """The kernel's cpulist format ("0-3,8,10-11") as a set of CPU ids."""
+    cpus = set()
+    for part in text.strip().split(","):
+        if not part:
+            continue
+        a, _, b = part.partition("-")
+        cpus.update(range(int(a), int(b or a) + 1))
+    return cpus
+
+
+def gpu_bdf(device_index: int):
+    """PCI address (domain:bus:device.function) of torch device ``device_index``, or None."""
+    try:
+        import torch
+
+        p = torch.cuda.get_device_properties(device_index)
+        return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}.0"
+    except Exception:
+        return None
+
+
+def pci_numa_node(bdf, sysfs=None) -> int:
+    """NUMA node of PCI device ``bdf`` from /sys/bus/pci/devices/<bdf>/numa_node (-1: unknown
+    or a single-node host)."""
+    import os
+
+    if not bdf:
+        return -1
+    try:
+        return int(open(os.path.join(sysfs or _sysfs_root(), "bus/pci/devices", bdf, "numa_node")).read())
+    except (OSError, ValueError):
+        return -1
+
+
+def node_cpus(node: int, sysfs=None) -> set:
+    import os
+
+    if node < 0:
+        return set()
+    try:
+        return parse_cpulist(open(os.path.join(sysfs or _sysfs_root(), f"devices/system/node/node{node}/cpulist")).read())
+    except OSError:
+        return set()
+
+
+def bind_to_gpu_node(bdf, sysfs=None) -> dict:
+    """Bind this rank's host threads to the CPUs of its GPU's NUMA node (intersected with the
+    CPUs the process may use), so that host staging it allocates and touches afterwards is
+    placed on that node (first-touch, the default local policy) and its copies do not cross
+    the socket link.  Returns what was chosen (reported per rank in the bench line)."""
+    import os
+
+    node = pci_numa_node(bdf, sysfs)
+    allowed = os.sched_getaffinity(0)
+    cpus = node_cpus(node, sysfs) & allowed
+    bound = bool(cpus) and cpus != allowed
+    if bound:
+        os.sched_setaffinity(0, cpus)
+    return {"bdf": bdf, "numa_node": node, "cpus": len(cpus) if cpus else len(allowed), "bound": bound}
+
+
+def pages_numa_node(ptr: int, nbytes: int, samples: int = 16) -> int:
+    """NUMA node holding the pages of host range [ptr, ptr + nbytes) (the node of most sampled
+    pages, via move_pages(2) with no target nodes: a query), or -1 when it cannot be told."""
+    import collections
+    import ctypes
+    import os
+    import platform
+
+    if nbytes <= 0 or platform.machine() != "x86_64":
+        return -1
+    page = os.sysconf("SC_PAGE_SIZE")
+    first = ptr // page * page
+    npages = (ptr + nbytes - first + page - 1) // page
+    k = max(1, min(samples, npages))
+    addrs = (ctypes.c_void_p * k)(*[first + (i * npages // k) * page for i in range(k)])
+    status = (ctypes.c_int * k)()
+    libc = ctypes.CDLL(None, use_errno=True)
+    libc.syscall.restype = ctypes.c_long
+    SYS_move_pages = 279  # x86_64
+    if libc.syscall(SYS_move_pages, 0, ctypes.c_ulong(k), addrs, None, status, 0) != 0:
+        return -1
+    nodes = [s for s in status if s >= 0]
+    return collections.Counter(nodes).most_common(1)[0][0] if nodes else -1

@@ -52,7 +52,8 @@ def parse():
     ap.add_argument("--strong-stream", type=int, default=-1,
                     help="after the main measurement, also time one stream of this many blocks split "
                          "contiguously over the ranks and report it as `strong_stream` (BASELINE "
-                         "configs[4]); default: 65536 when --gpus > 1 without --stream-blocks, else off")
+                         "configs[4]); default: 65536 for the headline shape (32:32, 4096 x 1 MiB per "
+                         "GPU, 16 data shreds erased) without --stream-blocks, else off")
     ap.add_argument("--block-bytes", type=int, default=1 << 20)
     ap.add_argument("--k", type=int, default=32)
     ap.add_argument("--m", type=int, default=32)
@@ -67,7 +68,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = every CPU this process may use")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--pcie", action="store_true", help="also time host-buffer calls")
+    ap.add_argument("--pcie", action="store_true",
+                    help="also time host-buffer calls, on every rank, with each rank's host staging "
+                         "on its GPU's NUMA node")
     ap.add_argument("--pcie-blocks", type=int, default=4096, help="blocks in the host-buffer run")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-settle", action="store_true",
@@ -78,10 +81,19 @@ def parse():
     ap.add_argument("--dry-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--dry-verify-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     ap.add_argument("--dry-stream-verify-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
+    ap.add_argument("--dry-bdfs", default="", help=argparse.SUPPRESS)  # per-rank PCI addresses (--dry-device)
     args = ap.parse_args()
+    args.strong_stream_default = args.strong_stream < 0
     if args.strong_stream < 0:
-        args.strong_stream = STREAM_BLOCKS if args.gpus > 1 and not args.stream_blocks else 0
+        args.strong_stream = STREAM_BLOCKS if _headline_shape(args) and not args.stream_blocks else 0
     return args
+
+
+def _headline_shape(args) -> bool:
+    """The driver's workload (BASELINE configs[1] + [2]): the shape configs[4]'s stream uses."""
+    return (args.k == 32 and args.m == 32 and args.block_bytes == 1 << 20 and args.erase in (-1, 16)
+            and not args.lose_coding and not args.random_patterns and args.only == "both"
+            and args.nblocks == 4096)
 
 
 STREAM_BLOCKS = 65536  # BASELINE configs[4]: a 64k-block stream batch-sharded one range per GPU
@@ -194,6 +206,19 @@ def _dry_main(args, world: int, rank: int, local: int) -> int:
     firsts = gather_over_ranks(plan.first, d)
     # a rank's "verification" here is only the flag the test asks for (--dry-verify-fail-rank)
     ok = None if args.no_verify else rank != args.dry_verify_fail_rank
+    pcie = None
+    if args.pcie:
+        # the NUMA placement only (no device, no transfer): bind to the GPU's node, allocate and
+        # touch the staging there, report the node its pages landed on
+        import numpy as np
+
+        from alpenglow_amd.shard import bind_to_gpu_node, gather_objects, pages_numa_node
+
+        bdfs = [b for b in args.dry_bdfs.split(",") if b]
+        numa = bind_to_gpu_node(bdfs[rank] if rank < len(bdfs) else None)
+        stage = np.ones(1 << 22, np.uint8)
+        numa["staging_node"] = pages_numa_node(stage.ctypes.data, stage.nbytes)
+        pcie = gather_objects(dict(rank=rank, numa=numa, blocks=0, matches_device_result=None), d)
     sub = None
     if args.strong_stream:
         splan = RankPlan(rank, world, 0, args.strong_stream)
@@ -219,6 +244,8 @@ def _dry_main(args, world: int, rank: int, local: int) -> int:
         }
         if sub is not None:
             line["strong_stream"] = sub
+        if pcie is not None:
+            line["pcie_inclusive"] = _pcie_line(pcie)
     status = _finish(args, d, None, rank, line, ok)
     if d:
         d.destroy_process_group()
@@ -439,16 +466,32 @@ def main():
             ok = ok is not False and line["cpu_baseline"]["gpu_parity_matches_cpu"]
         else:
             line["cpu_baseline"] = None
-        if args.pcie and world == 1:
-            line["pcie_inclusive"] = _pcie(args, ctx, cw, k, m, S, e, torch, dev)
-            ok = ok is not False and line["pcie_inclusive"]["matches_device_result"]
+    if args.pcie:
+        # every rank moves its own blocks through its own host staging, concurrently
+        from alpenglow_amd.shard import bind_to_gpu_node, gather_objects, gpu_bdf
+
+        numa = bind_to_gpu_node(gpu_bdf(local))
+        pc = _pcie(args, ctx, cw, k, m, S, e, torch, dev, barrier, numa)
+        pc["rank"] = rank
+        ok = _and_ok(ok, pc["matches_device_result"])
+        per = gather_objects(pc, dist)
+        if rank == 0:
+            line["pcie_inclusive"] = _pcie_line(per)
     if args.strong_stream:
         # BASELINE configs[4]: the weak workload's buffers go first (the stream's codewords
         # are strong_stream / world x (k + m) x S bytes per rank: 128 GiB at N = 1)
         del cw, view
         torch.cuda.synchronize()
         torch.cuda.empty_cache()
-        sub, sok = _strong_stream(args, ctx, dist, dev, torch, stream, rank, world, k, m, S, e, lc)
+        try:
+            sub, sok = _strong_stream(args, ctx, dist, dev, torch, stream, rank, world, k, m, S, e, lc)
+        except torch.cuda.OutOfMemoryError:
+            # the default 128 GiB stream on one GPU whose HBM another tenant holds part of: the
+            # main measurement stands; an explicitly requested stream (or any N > 1) fails loudly
+            if world > 1 or not args.strong_stream_default:
+                raise
+            torch.cuda.empty_cache()
+            sub, sok = {"skipped": "out of device memory", "stream_blocks": args.strong_stream}, None
         ok = _and_ok(ok, sok)
         if rank == 0:
             line["strong_stream"] = sub
@@ -680,11 +723,31 @@ def _cpu_model():
     return None
 
 
-def _pcie(args, ctx, cw, k, m, S, e, torch, dev):
+def _pcie_line(per: list) -> dict:
+    """The `pcie_inclusive` sub-line: one rank's dict at N = 1; at N > 1 every rank's dict
+    (`per_rank`, with the NUMA node each chose) and the job's aggregate rates (bytes of all
+    ranks over the slowest rank's time; the ranks ran concurrently between barriers)."""
+    if len(per) == 1:
+        return per[0]
+    out = {"per_rank": per, "n_ranks": len(per)}
+    if all(p.get("bytes") for p in per):
+        tot = sum(p["bytes"] for p in per)
+        out["encode_GiBps"] = tot / max(p["encode_s"] for p in per) / GIB
+        out["reconstruct_GiBps"] = tot / max(p["reconstruct_s"] for p in per) / GIB
+        out["encode_plus_reconstruct_GiBps"] = tot / max(p["encode_s"] + p["reconstruct_s"] for p in per) / GIB
+    out["matches_device_result"] = all(p.get("matches_device_result") for p in per)
+    return out
+
+
+def _pcie(args, ctx, cw, k, m, S, e, torch, dev, barrier, numa):
     """Host-buffer (PCIe-inclusive) rate: blocks start and end in pinned host memory; the
     library pipelines H2D / kernels / D2H over two staging slots.  Also reports the raw
-    pinned-copy rates of the same bytes for context."""
+    pinned-copy rates of the same bytes for context.  The caller bound this rank to its GPU's
+    NUMA node first (`numa`), so the pinned buffers allocated and touched here sit on that
+    node (reported as `numa.staging_node`); the timed runs start after a barrier, so at N > 1
+    the ranks' transfers overlap as they would in service."""
     from alpenglow_amd import rs
+    from alpenglow_amd.shard import pages_numa_node
 
     nb = min(cw.shape[0], args.pcie_blocks)
     stride = (k + m) * S
@@ -707,14 +770,17 @@ def _pcie(args, ctx, cw, k, m, S, e, torch, dev):
         td = time.perf_counter() - t
         return te, td
 
+    numa = dict(numa, staging_node=pages_numa_node(host.data_ptr(), host.numel()))
     run()  # warm-up: staging buffers, streams
+    barrier()
     te, td = run()
+    barrier()
     ok = bool(torch.equal(host, ref))
     # raw pinned copies of one batch's data bytes (contiguous), each direction alone
     dbuf = torch.empty((nb, k * S), dtype=torch.uint8, device=dev)
     src = torch.empty((nb, k * S), dtype=torch.uint8, pin_memory=True)
     dbuf.copy_(src, non_blocking=True)  # warm
-    torch.cuda.synchronize()
+    barrier()
     t = time.perf_counter()
     dbuf.copy_(src, non_blocking=True)
     torch.cuda.synchronize()
@@ -724,7 +790,8 @@ def _pcie(args, ctx, cw, k, m, S, e, torch, dev):
     torch.cuda.synchronize()
     tdn = time.perf_counter() - t
     B = k * S
-    return {"blocks": nb, "encode_GiBps": nb * B / te / GIB, "reconstruct_GiBps": nb * B / td / GIB,
+    return {"blocks": nb, "bytes": nb * B, "encode_s": te, "reconstruct_s": td, "numa": numa,
+            "encode_GiBps": nb * B / te / GIB, "reconstruct_GiBps": nb * B / td / GIB,
             "encode_plus_reconstruct_GiBps": nb * B / (te + td) / GIB, "matches_device_result": ok,
             "pinned_h2d_GBps": nb * B / th / 1e9, "pinned_d2h_GBps": nb * B / tdn / 1e9,
             "note": "host buffers pinned; encode moves k*S up and m*S down per block, reconstruct "

@@ -186,12 +186,17 @@ def test_bench_strong_stream_verify_fails_job(bad):
 
 
 def test_bench_strong_stream_flags():
-    """--strong-stream 0 turns the sub-line off; at one rank it is off by default and on
-    when asked (the driver's N = 1 line stays configs[1] + configs[2])."""
+    """--strong-stream 0 turns the sub-line off; the headline shape has it on by default at
+    every N, including the driver's N = 1 line (whose `value` stays configs[1] + configs[2]);
+    other shapes (sweep points) have it off unless asked."""
     r = _bench("--gpus", "2", "--dry-device", "--steps", "1", "--strong-stream", "0")
     assert r.returncode == 0, r.stderr
     assert "strong_stream" not in json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     r = _bench("--gpus", "1", "--dry-device", "--steps", "1")
+    assert r.returncode == 0, r.stderr
+    sub = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])["strong_stream"]
+    assert sub["stream_blocks"] == 65536 and sub["first_block"] == [0] and sub["blocks_per_rank"] == [65536]
+    r = _bench("--gpus", "1", "--dry-device", "--steps", "1", "--k", "16", "--m", "4")
     assert r.returncode == 0, r.stderr
     assert "strong_stream" not in json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
     r = _bench("--gpus", "1", "--dry-device", "--steps", "1", "--strong-stream", "1000")
@@ -237,3 +242,54 @@ def test_bench_launcher_fails_loudly():
     assert r.returncode != 0
     r = _bench("--gpus", "2", "--dry-device", "--steps", "1", env_extra={"WORLD_SIZE": "1", "RANK": "0"})
     assert r.returncode != 0 and "launcher started 1 rank" in r.stderr
+
+
+def _fake_sysfs(tmp_path, nodes):
+    """A sysfs tree with one GPU per entry of ``nodes`` (bdf -> NUMA node) and node cpulists
+    that split this process's CPUs in two."""
+    cpus = sorted(os.sched_getaffinity(0))
+    half = max(1, len(cpus) // 2)
+    groups = {0: cpus[:half], 1: cpus[half:] or cpus[:half]}
+    for node, cs in groups.items():
+        d = tmp_path / "devices" / "system" / "node" / f"node{node}"
+        d.mkdir(parents=True)
+        (d / "cpulist").write_text(",".join(str(c) for c in cs) + "\n")
+    for bdf, node in nodes.items():
+        d = tmp_path / "bus" / "pci" / "devices" / bdf
+        d.mkdir(parents=True)
+        (d / "numa_node").write_text(f"{node}\n")
+    return groups
+
+
+def test_numa_helpers(tmp_path):
+    from alpenglow_amd import shard
+
+    groups = _fake_sysfs(tmp_path, {"0000:11:00.0": 1, "0000:21:00.0": -1})
+    assert shard.parse_cpulist("0-3,8,10-11") == {0, 1, 2, 3, 8, 10, 11}
+    assert shard.pci_numa_node("0000:11:00.0", str(tmp_path)) == 1
+    assert shard.pci_numa_node("0000:21:00.0", str(tmp_path)) == -1  # single-node host
+    assert shard.pci_numa_node("0000:99:00.0", str(tmp_path)) == -1  # no such device
+    assert shard.node_cpus(1, str(tmp_path)) == set(groups[1])
+    import numpy as np
+
+    a = np.ones(1 << 22, np.uint8)
+    assert shard.pages_numa_node(a.ctypes.data, a.nbytes) >= 0  # this host's node of the pages
+
+
+def test_bench_pcie_numa_per_rank(tmp_path):
+    """SURVEY §8e / VERDICT r5: with --pcie every rank binds to its GPU's NUMA node before it
+    allocates its host staging, and rank 0's line carries one `pcie_inclusive` entry per rank
+    with the node chosen, the CPUs bound and the node the staging pages landed on."""
+    groups = _fake_sysfs(tmp_path, {"0000:11:00.0": 0, "0000:21:00.0": 1})
+    r = _bench("--gpus", "2", "--dry-device", "--steps", "1", "--pcie", "--strong-stream", "0",
+               "--dry-bdfs", "0000:11:00.0,0000:21:00.0", env_extra={"AG_SYSFS_ROOT": str(tmp_path)})
+    assert r.returncode == 0, r.stderr
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][0])
+    pc = line["pcie_inclusive"]
+    assert pc["n_ranks"] == 2 and [p["rank"] for p in pc["per_rank"]] == [0, 1]
+    for rank, p in enumerate(pc["per_rank"]):
+        numa = p["numa"]
+        assert numa["bdf"] == ["0000:11:00.0", "0000:21:00.0"][rank]
+        assert numa["numa_node"] == rank
+        assert numa["cpus"] == len(groups[rank])
+        assert isinstance(numa["staging_node"], int)

@@ -1434,3 +1434,62 @@ def test_per_call_server_jobs_and_restart(ctx):
         assert got == payload, (i, keep)
         if i % 15 == 14:
             time.sleep(0.06)  # the server idles out; the next call relaunches it
+
+
+def test_server_timeout_abandons_staging_safely(ctx):  # ctx: torch initialises the device first
+    """a per-call server job that times out abandons the pinned staging it named.
+    The encoder / decoder that owned it must then drop its received shards and take a fresh
+    buffer -- a retry without reset returns an error instead of handing null staging to the
+    device, later adds land in the new buffer, and the context falls back to the launch path
+    (results against the oracle).  The timeout is injected (ag_rs_internal_fail_next_server_job)."""
+    k = m = 32
+    S = 1024
+    orig = _shards(777, k, S)
+    rec = o.encode(orig, m)
+
+    ectx = rs.Context(0)
+    enc = rs.ReedSolomonEncoder(ectx, k, m, S)
+    for s in orig:
+        enc.add_original_shard(s)
+    rs.fail_next_server_job(ectx)
+    with pytest.raises(rs.RSError) as e:
+        enc.encode()
+    assert e.value.status == 102  # AG_RS_ERR_DEVICE
+    with pytest.raises(rs.RSError) as e:  # retry without reset: the shards were dropped
+        enc.encode()
+    assert e.value.kind == "TooFewOriginalShards"
+    for it in range(2):
+        for s in orig:
+            enc.add_original_shard(s)
+        assert enc.encode() == rec, it  # launch path from now on
+
+    dctx = rs.Context(0)
+    dec = rs.ReedSolomonDecoder(dctx, k, m, S)
+    for j in range(m):
+        dec.add_recovery_shard(j, rec[j])
+    rs.fail_next_server_job(dctx)
+    with pytest.raises(rs.RSError) as e:
+        dec.decode()
+    assert e.value.status == 102
+    with pytest.raises(rs.RSError) as e:
+        dec.decode()
+    assert e.value.kind == "NotEnoughShards"
+    for j in range(m):
+        dec.add_recovery_shard(j, rec[j])
+    res = dec.decode()
+    assert sorted(res) == list(range(k)) and all(res[i] == orig[i] for i in res)
+
+    cctx = rs.Context(0)
+    coder = rs.ReedSolomonCoder(cctx, 32)
+    payload = o.splitmix64_bytes(99, 32767)  # S = 1024: a server job
+    rs.fail_next_server_job(cctx)
+    with pytest.raises(rs.RSError):
+        coder.shred(payload)
+    raw = coder.shred(payload)
+    exp = o.coder_shred(payload, 32)
+    assert raw.data == exp.data and raw.coding == exp.coding
+    got, _ = coder.deshred([None] * 32 + [(False, c) for c in raw.coding])
+    assert got == payload
+    del enc, dec, coder
+    for c in (ectx, dctx, cctx):
+        c.close()

@@ -215,17 +215,23 @@ def test_deshred_batch_matches_oracle(ctx, dev):
     _check_against_oracle(res, out, cw, want)
 
 
-def test_deshred_batch_adversarial_random(ctx, dev):
+# S = 1024: the fused window decode with the coding restore (decode_pk<-1>); S = 512 / 64:
+# whole-chunk shreds on the other window decoders, whose exactly-32 slices re-encode only the
+# absent coding shreds (store mask ~present) and whose Merkle rebuild reuses the proof check's
+# leaf digests for kept rows; S = 2: a tail-only shred (S % 64 != 0: every coding shred
+# re-encoded, the LIST leaf kernel) -- ADVICE r5.
+@pytest.mark.parametrize("S", [1024, 512, 64, 2])
+def test_deshred_batch_adversarial_random(ctx, dev, S):
     """24 slices, about half of them from a leader that altered one random shred after
-    encoding, each received as a random 32..64 of its datagrams: verdicts, filled datagrams
-    and raw shreds equal the oracle's (every kept shred through the crate's decoder)."""
-    S = 1024
-    rng = random.Random(2024)
+    encoding, each received as a random 32..64 of its datagrams (every fourth slice exactly
+    32): verdicts, filled datagrams and raw shreds equal the oracle's (every kept shred through
+    the crate's decoder)."""
+    rng = random.Random(2024 + S)
     slices = _slices(rng, 24, S)
     inp = []
     for b, sl_ in enumerate(slices):
         rows = _non_codeword(sl_, rng.randrange(64)) if b % 2 else so.shred(*sl_[:5], SEED)[0]
-        keep = set(rng.sample(range(64), rng.randrange(32, 65)))
+        keep = set(rng.sample(range(64), 32 if b % 4 < 2 else rng.randrange(32, 65)))
         inp.append([rows[j] if j in keep else None for j in range(64)])
     pk_bytes = ed.secret_to_public(SEED)
     want = _expect(inp, pk_bytes, S)
@@ -234,17 +240,18 @@ def test_deshred_batch_adversarial_random(ctx, dev):
     _check_against_oracle(res, out, cw, want)
 
 
-def test_pipeline_roundtrip_random_arrival(ctx, dev):
-    """shred_batch -> a random 32..64 of each slice's datagrams -> deshred_batch restores
-    every payload and every datagram (256 maximum slices)."""
-    S, n = 1024, 256
-    rng = random.Random(5)
+@pytest.mark.parametrize("S", [1024, 512, 64, 2])
+def test_pipeline_roundtrip_random_arrival(ctx, dev, S):
+    """shred_batch -> a random 32..64 of each slice's datagrams (every other slice exactly 32)
+    -> deshred_batch restores every payload and every datagram (256 slices of shred size S)."""
+    n = 256
+    rng = random.Random(5 + S)
     slices = _slices(rng, n, S)
     cw, pk_buf, lens, _, _, pk = _gpu_shred(ctx, dev, slices, S)
     full = _packets(pk_buf, lens, n)
     inp = []
     for b in range(n):
-        keep = set(rng.sample(range(64), rng.randrange(32, 65)))
+        keep = set(rng.sample(range(64), 32 if b % 2 else rng.randrange(32, 65)))
         inp.append([full[b][j] if j in keep else None for j in range(64)])
     res, out, cw2 = _deshred(ctx, dev, inp, pk, S)
     assert (res.status == 0).all()
