@@ -14,15 +14,16 @@ launcher that starts N fresh rank processes before any GPU call and exits non-ze
 rank fails.  Each rank shards its own independent blocks (weak scaling, or --stream-blocks
 for BASELINE configs[4]'s one stream split over the GPUs); there is no data-path collective,
 the only collectives are the timing barrier, the max-over-ranks reduction and the gather of
-per-rank wall times reported in the line.  With --gpus N > 1 (and no --stream-blocks) the
-same run then also times configs[4]'s 65 536 x 1 MiB stream split contiguously over the
-ranks and reports it as the `strong_stream` sub-line (value, per-rank walls and verdicts);
-`value` stays the weak-scaling figure, so the N = 1 line equals configs[1] + configs[2].
+per-rank wall times reported in the line.  For the headline shape (and no --stream-blocks)
+the same run then also times configs[4]'s 65 536 x 1 MiB stream split contiguously over the
+ranks -- at every N, N = 1 included (128 GiB of codewords in one GPU's HBM) -- and reports
+it as the `strong_stream` sub-line (value, per-rank walls and verdicts); `value` stays the
+weak-scaling figure, so the N = 1 line equals configs[1] + configs[2].
 
 Also printed in the JSON line: per-kernel HIP-event timings on the launch stream with the
 HBM roofline, a CPU baseline (the C oracle, a restatement of the reference algorithm, on a
 bounded sample of the same blocks, rank 0 at N=1) and, with --pcie, the host-buffer
-(PCIe-inclusive) rate.
+(PCIe-inclusive) rate of every rank, each rank's pinned staging on its GPU's NUMA node.
 """
 
 from __future__ import annotations
