@@ -75,13 +75,18 @@ def gen_consts() -> str:
     srcs = [os.path.join(CSRC, "gen_consts.cpp"), os.path.join(CSRC, "gf16.cpp")]
     if _mtime(gen) < max(_mtime(s) for s in srcs + [os.path.join(CSRC, "gf16.hpp")]):
         _run([CXX, "-O2", "-std=c++17", f"-I{CSRC}", *srcs, "-o", gen])
-    out = os.path.join(OBJDIR, "rs_consts.inc")
+    # per-process output and an atomic replace: concurrent builds (parallel test workers) must
+    # never read or install a half-written table
+    out = os.path.join(OBJDIR, f"rs_consts.{os.getpid()}.inc")
     _run([gen, out])
     dst = os.path.join(CSRC, "rs_consts.inc")
     new = open(out).read()
     if not os.path.exists(dst) or open(dst).read() != new:
-        with open(dst, "w") as f:
+        tmp = f"{dst}.{os.getpid()}.tmp"
+        with open(tmp, "w") as f:
             f.write(new)
+        os.replace(tmp, dst)
+    os.remove(out)
     return dst
 
 

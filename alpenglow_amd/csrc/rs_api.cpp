@@ -198,6 +198,7 @@ struct ag_rs_ctx {
   uint32_t server_seq = 0;
   bool server_broken = false;  // a job timed out: the server path is off for this context
   bool fail_next_server_job = false;  // test aid: the next server job takes the timeout path
+  uint64_t server_jobs[4] = {};        // jobs posted per LatencyJob kind (test aid)
   std::vector<PinBuf> abandoned_pins;  // staging a timed-out job named (freed once the server is gone)
   std::vector<uint64_t> mask_host;        // last store-mask words uploaded to d_mask
   std::vector<uint64_t> stage_mask_host;  // last restride masks uploaded to stage_mask
@@ -1277,6 +1278,14 @@ int ag_rs_internal_last_decode_classes(ag_rs_ctx* c, uint64_t* out16) {
 
 // Test aid (not in the header): the encode kernels (ag::EncodeKernelBit) the last
 // ag_rs_encode_batch call on this context launched.
+// Test aid (not in the header): per-call server jobs posted on the context, per LatencyJob kind
+// (encode, decode, decode half, decode_pk).
+int ag_rs_internal_server_jobs(ag_rs_ctx* c, uint64_t* out4) {
+  if (!c || !out4) return AG_RS_ERR_INVALID_ARGUMENT;
+  std::copy(std::begin(c->server_jobs), std::end(c->server_jobs), out4);
+  return AG_RS_OK;
+}
+
 // Test aid (not in the header): the context's next per-call server job takes the timeout path
 // (retired, staging abandoned, server path off) without waiting 5 s.
 int ag_rs_internal_fail_next_server_job(ag_rs_ctx* c) {
@@ -1701,8 +1710,10 @@ ag::XformParams one_tile(const uint8_t* in, size_t in_stride, uint8_t* out, size
   p.total_columns = S / 64;
   return p;
 }
-// `stage`: the pinned buffer the job reads and writes (abandoned on a timeout).
-int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t mask, PinBuf& stage) {
+// `stage`: the pinned buffer the job reads and writes (abandoned on a timeout).  `dp`: the
+// kJobDecodePk parameters (then `p` is unused).
+int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t mask, PinBuf& stage,
+               const ag::DecodeXParams* dp = nullptr) {
   if (!c->mb) {
     void* h = nullptr;
     AG_HIP(hipHostMalloc(&h, sizeof(ag::LatencyMailbox), hipHostMallocMapped | hipHostMallocCoherent));
@@ -1736,7 +1747,13 @@ int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t m
   }
   mb->kind = kind;
   mb->mask = mask;
-  std::memcpy(static_cast<void*>(&mb->p), &p, sizeof p);
+  if (dp) {
+    std::memcpy(static_cast<void*>(&mb->dp), dp, sizeof *dp);
+    mb->tables = c->dtables();
+  } else {
+    std::memcpy(static_cast<void*>(&mb->p), &p, sizeof p);
+  }
+  if (kind < 4) ++c->server_jobs[kind];
   const uint32_t seq = ++c->server_seq;
   __atomic_store_n(&mb->doorbell, seq, __ATOMIC_RELEASE);  // x86: the job's fields are visible first
   const auto t0 = std::chrono::steady_clock::now();
@@ -1808,6 +1825,39 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, PinBuf& pin, cons
     if (coding && !reuse &&
         (st = server_job(c, ag::kJobEncode32, one_tile(pd, ob, pd + ob + rb, rb, S), 0, pin)))
       return st;
+    return AG_RS_OK;
+  }
+  if (present == k && S == 1024 && server_fits(c, k, m, S)) {
+    // exactly k = 32 of the 64 shreds of a 32:32 slice of 1 KiB shreds (the follower's deshred
+    // at its 32nd arriving shred): decode_pk<-1>'s one-slice window decode on the server
+    // restores every absent data and coding shred in place -- the codeword through the 32
+    // survivors is unique, so the restored coding shreds are the re-encode, bit for bit
+    uint64_t pres = 0;
+    for (size_t j = 0; j < m; ++j)
+      if (rpres[j]) pres |= uint64_t{1} << j;
+    for (size_t i = 0; i < k; ++i)
+      if (opres[i]) pres |= uint64_t{1} << (32 + i);
+    ag::DecodeXParams dp{};
+    dp.rec = pd + ob;
+    dp.rec_block_stride = (k + m) * S;
+    dp.rec_shard_stride = S;
+    dp.orig = pd;
+    dp.orig_block_stride = (k + m) * S;
+    dp.orig_shard_stride = S;
+    dp.k = 32;
+    dp.m = 32;
+    dp.chunk = 32;
+    dp.low_rate = 0;
+    dp.chunks_per_shard = 16;
+    dp.total_columns = 16;
+    dp.per_lane = 1;
+    dp.rows_w = 64;
+    dp.any_k = 1;
+    dp.fuse = 1;
+    std::fill(std::begin(c->last_classes), std::end(c->last_classes), uint64_t{0});
+    ++c->last_classes[9];  // "server_window64"
+    if ((st = server_job(c, ag::kJobDecodePk, ag::XformParams{}, pres, pin, &dp))) return st;
+    if (coding_src) *coding_src = pin.as<uint8_t>() + ob;  // the whole coding set, in place
     return AG_RS_OK;
   }
   if ((st = decode_device(c, k, m, S, 1, pd, ob, pd + ob, rb, opres, rpres, 1, mode))) return st;

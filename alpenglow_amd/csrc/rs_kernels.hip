@@ -861,8 +861,17 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
 // =====================================================================================
 // The transform's multiplies use the subset-greedy programs (TAB 1, rs_device.hpp mul_acc): with
 // the cancellation programs this kernel's allocation spills (14 VGPRs).
+// The tile body (decode_pk_kernel, and the per-call server's random-arrival job with one slice):
+// `lds` is the 64 KiB exchange buffer (packed items [item][q][16 lanes] or swap regions), `sh`
+// the tile's lists.  p.pmask / p.rows may address LDS (the server stages them there).
+struct PkShared {
+  uint32_t lcoef[2 * 64];         // the two slices' locator constants (polynomial basis)
+  uint64_t smask[2][2];           // per slice: positions present (loaded), restored
+  uint8_t ilist[2][64], olist[2][64];  // per slice: survivor / restored positions by rank
+};
 template <int OUTH>
-__global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p) {
+__device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t tile, uint4* lds, X8Flags* fl,
+                                               PkShared& sh) {
   static_assert(OUTH >= -1 && OUTH <= 1, "OUTH: the restored positions' window half, -1 both");
   using LB = X8Lay<2, 1, 3, 4, 5>;
   using LC = X8Lay<2, 3, 1, 4, 5>;
@@ -870,15 +879,14 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
   using LE = X8Lay<4, 5, 1, 2, 3>;
   constexpr int W = 64, kSl = 16;           // positions, columns per slice
   constexpr int D = 2;                      // derivative epochs 4, 5; FFT swaps 4 + D ..
-  __shared__ uint4 lds[16 * 4 * kXfLanes];  // 64 KiB: packed items ([item][q][16 lanes]) or swap regions
-  __shared__ X8Flags flags;
-  __shared__ uint32_t lcoef[2 * W];         // the two slices' locator constants (polynomial basis)
-  __shared__ uint64_t smask[2][2];          // per slice: positions present (loaded), restored
-  __shared__ uint8_t ilist[2][W], olist[2][W];  // per slice: survivor / restored positions by rank
+  X8Flags& flags = *fl;
+  uint32_t* lcoef = sh.lcoef;
+  auto& smask = sh.smask;
+  auto& ilist = sh.ilist;
+  auto& olist = sh.olist;
   const int lane = threadIdx.x & 63;
   const int h = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t tile = dev::xcd_tile(blockIdx.x, gridDim.x);
   const uint64_t sb0 = static_cast<uint64_t>(tile) * 2;  // the tile's first slice (block)
   const uint64_t nblk = p.total_columns / kSl;
   const uint32_t opos = p.low_rate ? 0 : p.chunk, rpos = p.low_rate ? p.chunk : 0;
@@ -1114,6 +1122,14 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
       }
     }
   });
+}
+
+template <int OUTH>
+__global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p) {
+  __shared__ uint4 lds[16 * 4 * kXfLanes];
+  __shared__ X8Flags flags;
+  __shared__ PkShared sh;
+  decode_pk_tile<OUTH>(p, dev::xcd_tile(blockIdx.x, gridDim.x), lds, &flags, sh);
 }
 
 // Per pattern and window position x: the decoder's locator constant as a bitsliced
@@ -2123,10 +2139,17 @@ __device__ __forceinline__ uint32_t sys_load(const uint32_t* a) {
 __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* mb, uint64_t idle_ticks) {
   __shared__ uint4 lds[16 * 4 * kXfLanes];
   __shared__ X8Flags flags;
-  __shared__ uint32_t job[sizeof(XformParams) / 4];
+  constexpr unsigned kXw = sizeof(XformParams) / 4, kDw = sizeof(DecodeXParams) / 4,
+                     kTw = sizeof(GfDeviceTables) / 4;
+  __shared__ __attribute__((aligned(16))) uint32_t job[kXw > kDw + kTw ? kXw : kDw + kTw];
   __shared__ uint64_t mask;
   __shared__ uint32_t cmd;
-  static_assert(sizeof(XformParams) % 4 == 0 && sizeof(XformParams) / 4 <= 512, "params copy");
+  __shared__ PkShared pk;                 // kJobDecodePk: the tile's lists
+  __shared__ uint64_t pk_mask[4];         // slice 0: present, restored; slice 1: none
+  __shared__ uint32_t pk_rows[64];        // slice 0's locator constants (polynomial basis)
+  static_assert(sizeof(XformParams) % 4 == 0 && kXw <= 512, "params copy");
+  static_assert(sizeof(DecodeXParams) % 4 == 0 && sizeof(GfDeviceTables) % 4 == 0 && kDw + kTw <= 512,
+                "decode params copy");
   uint32_t last = 0;
   if (threadIdx.x == 0) {
     last = sys_load(&mb->done);
@@ -2151,8 +2174,14 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
     __syncthreads();
     const uint32_t kind = __builtin_amdgcn_readfirstlane(cmd);
     if (kind >= kJobQuit) break;
-    if (threadIdx.x < sizeof(XformParams) / 4)
+    if (kind == kJobDecodePk) {
+      if (threadIdx.x < kDw)
+        job[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->dp) + threadIdx.x);
+      else if (threadIdx.x >= 256 && threadIdx.x < 256 + kTw)
+        job[kDw + threadIdx.x - 256] = sys_load(reinterpret_cast<const uint32_t*>(&mb->tables) + threadIdx.x - 256);
+    } else if (threadIdx.x < kXw) {
       job[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->p) + threadIdx.x);
+    }
     if (threadIdx.x == 64) {
       const uint32_t* m = reinterpret_cast<const uint32_t*>(&mb->mask);
       mask = static_cast<uint64_t>(sys_load(m)) | static_cast<uint64_t>(sys_load(m + 1)) << 32;
@@ -2160,6 +2189,39 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
     if (threadIdx.x >= 128 && threadIdx.x < 144) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x - 128] = 0;
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale input bytes in this CU's caches
+    if (kind == kJobDecodePk) {
+      // the tile reads its parameters from the LDS copy: a private copy would be indexed by the
+      // rec / orig selects and land in scratch
+      DecodeXParams& dp = *reinterpret_cast<DecodeXParams*>(job);
+      GfDeviceTables t;
+      uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
+#pragma unroll
+      for (unsigned i = 0; i < kTw; ++i) tw[i] = __builtin_amdgcn_readfirstlane(job[kDw + i]);
+      const uint64_t present = mask;
+      if (threadIdx.x < 64) {
+        // decode_rows_kernel's Walsh route for the one pattern: erased = restored = ~present
+        const int lane = threadIdx.x;
+        const uint32_t x = static_cast<uint32_t>(lane);
+        const uint64_t e = ~present;
+        const uint32_t hl = m65535_mul(walsh64(x ? t.log[x] : 0u, lane), 1024u);
+        const uint32_t hi = walsh64(static_cast<uint32_t>((e >> x) & 1), lane);
+        const uint32_t acc = walsh64(m65535_mul(hl, hi), lane);
+        pk_rows[x] = dev::to_poly(t.exp[locator_log(acc, (present >> x) & 1)]);
+        if (lane == 0) {
+          pk_mask[0] = present;
+          pk_mask[1] = e;
+          pk_mask[2] = pk_mask[3] = 0;
+          dp.pmask = pk_mask;
+          dp.rows = pk_rows;
+        }
+      }
+      __syncthreads();
+      decode_pk_tile<-1>(dp, 0, lds, &flags, pk);
+      __threadfence_system();
+      __syncthreads();
+      if (threadIdx.x == 0) __hip_atomic_store(&mb->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      continue;
+    }
     XformParams p;
     uint32_t* pw = reinterpret_cast<uint32_t*>(&p);
     for (unsigned i = 0; i < sizeof(XformParams) / 4; ++i) pw[i] = __builtin_amdgcn_readfirstlane(job[i]);

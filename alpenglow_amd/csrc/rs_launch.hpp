@@ -52,24 +52,6 @@ inline EncodeKernelBit encode32_kernel(const XformParams& p) {
   return groups < 256 || p.chunks_per_shard == 128 || p.chunks_per_shard == 256 ? kEkXform8 : kEkXform4;
 }
 
-// The per-call server (latency_server_kernel): one resident workgroup per context serves
-// single-tile 32-point transforms posted through a mailbox in mapped, fine-grained host
-// memory, so a per-slice call costs no kernel dispatch and no completion signal.
-//   host:   writes kind / mask / p, then doorbell = seq; spins until done == seq
-//   server: polls doorbell, runs the job, releases its stores, writes done = seq; exits
-//           (alive = 0) on kJobQuit or after idle_ticks of the 100 MHz wall clock with no job
-enum LatencyJob : uint32_t { kJobEncode32 = 0, kJobDecode32 = 1, kJobDecode32Half = 2, kJobQuit = 3 };
-struct LatencyMailbox {
-  uint32_t doorbell;  // host: sequence number of the posted job
-  uint32_t done;      // server: sequence number of the last finished job
-  uint32_t alive;     // 0 no server, 1 server running, 2 launch requested (host)
-  uint32_t kind;      // LatencyJob
-  uint64_t mask;      // decode: store mask (bit s: shard s restored); the server copies it to LDS
-  XformParams p;      // in / out: device addresses of mapped host memory; p.out_mask ignored
-};
-hipError_t launch_latency_server(LatencyMailbox* mb_dev, uint64_t idle_ticks, hipStream_t stream);
-
-
 hipError_t launch_xform(XformKind kind, const XformParams& p, hipStream_t stream);
 // True when the bitsliced transform exists for this transform size.
 bool xform_supported(unsigned n);
@@ -208,6 +190,36 @@ hipError_t launch_decode_rows128(const uint64_t* m6, uint32_t npat, const GfDevi
 // rows for npat patterns: emask[p] = erased positions (locator), pmask as above.
 hipError_t launch_decode_rows(const uint64_t* emask, const uint64_t* pmask, uint32_t npat, uint32_t W,
                               const GfDeviceTables& t, uint32_t* rows, bool poly, hipStream_t stream);
+
+// The per-call server (latency_server_kernel): one resident workgroup per context serves
+// single-tile 32-point transforms posted through a mailbox in mapped, fine-grained host
+// memory, so a per-slice call costs no kernel dispatch and no completion signal.
+//   host:   writes kind / mask / p, then doorbell = seq; spins until done == seq
+//   server: polls doorbell, runs the job, releases its stores, writes done = seq; exits
+//           (alive = 0) on kJobQuit or after idle_ticks of the 100 MHz wall clock with no job
+// kJobDecodePk: one 32:32 slice of 1 KiB shreds with exactly 32 shreds present (the follower's
+// deshred at its 32nd arriving shred, slot_block_data.rs:353): decode_pk<-1>'s window decode on
+// a one-slice tile, restoring every absent data and coding shred in place; `mask` = the present
+// window positions (bit j < 32: coding shred j, bit 32 + i: data shred i), the locator
+// constants are computed by the server (decode_rows' Walsh route) from `tables`.
+enum LatencyJob : uint32_t {
+  kJobEncode32 = 0,
+  kJobDecode32 = 1,
+  kJobDecode32Half = 2,
+  kJobDecodePk = 3,
+  kJobQuit = 4
+};
+struct LatencyMailbox {
+  uint32_t doorbell;  // host: sequence number of the posted job
+  uint32_t done;      // server: sequence number of the last finished job
+  uint32_t alive;     // 0 no server, 1 server running, 2 launch requested (host)
+  uint32_t kind;      // LatencyJob
+  uint64_t mask;      // decode: store mask (bit s: shard s restored); pk: present positions
+  XformParams p;      // in / out: device addresses of mapped host memory; p.out_mask ignored
+  DecodeXParams dp;   // kJobDecodePk: rec / orig / strides (pmask, rows set by the server)
+  GfDeviceTables tables;  // kJobDecodePk: the device log / exp tables
+};
+hipError_t launch_latency_server(LatencyMailbox* mb_dev, uint64_t idle_ticks, hipStream_t stream);
 
 // Generic (any geometry) table-driven kernels.  One thread per (block, symbol).
 

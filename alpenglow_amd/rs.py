@@ -171,6 +171,7 @@ def load():
     sigs["ag_rs_internal_last_decode_classes"] = ([p, p], i)  # test aid, not in the header
     sigs["ag_rs_internal_last_encode_kernels"] = ([p, p], i)  # test aid, not in the header
     sigs["ag_rs_internal_fail_next_server_job"] = ([p], i)  # test aid, not in the header
+    sigs["ag_rs_internal_server_jobs"] = ([p, p], i)  # test aid, not in the header
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
             continue              # check the shipped library exports everything
@@ -366,7 +367,7 @@ def coder_deshred_batch(ctx: Context, num_coding: int, nslices: int, shred_bytes
 
 
 DECODE_CLASSES = {0: "none", 1: "transform", 2: "generic", 3: "window64", 4: "syndrome", 5: "lowrate_chunk",
-                  6: "correction", 8: "window128"}
+                  6: "correction", 8: "window128", 9: "server_window64"}
 
 
 def last_decode_classes(ctx: Context) -> dict:
@@ -387,6 +388,18 @@ def last_encode_kernels(ctx: Context) -> set:
     out = ctypes.c_uint32(0)
     _check(load().ag_rs_internal_last_encode_kernels(ctx.handle, ctypes.byref(out)), "last_encode_kernels")
     return {name for i, name in enumerate(ENCODE_KERNELS) if out.value >> i & 1}
+
+
+SERVER_JOBS = ("encode32", "decode32", "decode32_half", "decode_pk")
+
+
+def server_jobs(ctx: Context) -> dict:
+    """Per-call server jobs posted on ``ctx`` so far, per kind (test aid)."""
+    import numpy as np
+
+    out = np.zeros(4, np.uint64)
+    _check(load().ag_rs_internal_server_jobs(ctx.handle, out.ctypes.data), "server_jobs")
+    return dict(zip(SERVER_JOBS, (int(v) for v in out)))
 
 
 def fail_next_server_job(ctx: Context):

@@ -1421,6 +1421,8 @@ def test_per_call_server_jobs_and_restart(ctx):
     coder = rs.ReedSolomonCoder(ctx, 32)
     rng = random.Random(4242)
     sizes = [32767, 32704, 2047, 4095, 1000, 16383, 63, 0, 20000]
+    jobs0 = rs.server_jobs(ctx)
+    pk_calls = 0
     for i in range(45):
         payload = o.splitmix64_bytes(5000 + i, sizes[i % len(sizes)])
         raw = coder.shred(payload)
@@ -1428,12 +1430,43 @@ def test_per_call_server_jobs_and_restart(ctx):
         assert raw.data == exp.data and raw.coding == exp.coding, (i, len(payload))
         got, raw2 = coder.deshred([None] * 32 + [(False, c) for c in raw.coding])
         assert got == payload and raw2.coding == exp.coding, (i, len(payload))
-        keep = sorted(rng.sample(range(64), 32))
-        shreds = [((j < 32), (raw.data + raw.coding)[j]) if j in keep else None for j in range(64)]
-        got, _ = coder.deshred(shreds)
-        assert got == payload, (i, keep)
+        # random arrival: exactly 32 of 64 (S = 1 KiB: the server's decode_pk job, data and
+        # coding restored in one job), and a surplus set (launch path)
+        for cnt in (32, 40):
+            keep = sorted(rng.sample(range(64), cnt))
+            shreds = [((j < 32), (raw.data + raw.coding)[j]) if j in keep else None for j in range(64)]
+            before = rs.server_jobs(ctx)["decode_pk"]
+            got, raw3 = coder.deshred(shreds)
+            assert got == payload and raw3.data == exp.data and raw3.coding == exp.coding, (i, keep)
+            served = rs.server_jobs(ctx)["decode_pk"] - before
+            lost = set(range(64)) - set(keep)
+            fits = (cnt == 32 and len(raw.data[0]) == 1024 and any(j < 32 for j in lost)
+                    and any(j >= 32 for j in lost))  # else: no decode, or the coding-only transform
+            assert served == (1 if fits else 0), (i, cnt, len(raw.data[0]))
+            pk_calls += served
         if i % 15 == 14:
             time.sleep(0.06)  # the server idles out; the next call relaunches it
+    assert pk_calls >= 8
+    # the crate-API decoder (INTEGRATION.md Route A) from a random 32 of 64: the same job
+    dec = rs.ReedSolomonDecoder(ctx, 32, 32, 1024)
+    for it in range(6):
+        orig = _shards(900 + it, 32, 1024)
+        rec = o.encode(orig, 32)
+        dec.reset(32, 32, 1024)
+        keep = set(rng.sample(range(64), 32))
+        for j in sorted(keep):
+            if j < 32:
+                dec.add_original_shard(j, orig[j])
+            else:
+                dec.add_recovery_shard(j - 32, rec[j - 32])
+        before = rs.server_jobs(ctx)["decode_pk"]
+        res = dec.decode()
+        assert sorted(res) == [i for i in range(32) if i not in keep]
+        assert all(res[i] == orig[i] for i in res), it
+        pk = 0 < len(res) < 32 or (len(res) == 32 and keep != set(range(32, 64)))
+        assert rs.server_jobs(ctx)["decode_pk"] - before == (1 if pk else 0)
+        if pk:
+            assert rs.last_decode_classes(ctx) == {"server_window64": 1}
 
 
 def test_server_timeout_abandons_staging_safely(ctx):  # ctx: torch initialises the device first

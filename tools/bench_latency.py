@@ -8,6 +8,7 @@ interpreter overhead per ctypes call are included and reported separately as the
 a no-op ABI call).  Prints one JSON line with median / p90 microseconds per call:
   shred    ReedSolomonCoder::shred(max payload)          -> 32 + 32 shreds of 1 KiB
   deshred  ReedSolomonCoder::deshred(first 32 lost)      -> payload + re-encoded coding
+  deshred_random_32_of_64  the same from a random 32 of the 64 shreds (the follower's arrival)
   encoder  ReedSolomonEncoder: 32 x add_original_shard + encode + 32 recovery reads
 """
 import json
@@ -27,6 +28,10 @@ def main():
     payload = os.urandom(rs.MAX_DATA_PER_SLICE)
     raw = coder.shred(payload)
     shreds = [None] * 32 + [(False, c) for c in raw.coding]
+    import random
+
+    keep = set(random.Random(7).sample(range(64), 32))  # the follower's random 32 of 64
+    shreds_r = [((j < 32), (raw.data + raw.coding)[j]) if j in keep else None for j in range(64)]
     enc = rs.ReedSolomonEncoder(ctx, 32, 32, 1024)
 
     def t_shred():
@@ -34,6 +39,10 @@ def main():
 
     def t_deshred():
         got, _ = coder.deshred(shreds)
+        assert got == payload
+
+    def t_deshred_random():
+        got, _ = coder.deshred(shreds_r)
         assert got == payload
 
     def t_encoder():
@@ -47,7 +56,7 @@ def main():
 
     out = {"unit": "us per call", "slice": "32767-byte payload, 32:32 shreds of 1 KiB"}
     for name, f, reps in (("noop_abi_call", t_noop, 2000), ("shred", t_shred, 300), ("deshred", t_deshred, 300),
-                          ("encoder", t_encoder, 300)):
+                          ("deshred_random_32_of_64", t_deshred_random, 300), ("encoder", t_encoder, 300)):
         for _ in range(20):
             f()
         ts = []
