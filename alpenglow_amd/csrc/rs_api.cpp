@@ -1854,6 +1854,9 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, PinBuf& pin, cons
     dp.rows_w = 64;
     dp.any_k = 1;
     dp.fuse = 1;
+    // the server computes the locator constants from the device log / exp tables: they must
+    // exist before the first job (a context whose earlier calls all ran on the server has none)
+    if ((st = c->ensure_tables())) return st;
     std::fill(std::begin(c->last_classes), std::end(c->last_classes), uint64_t{0});
     ++c->last_classes[9];  // "server_window64"
     if ((st = server_job(c, ag::kJobDecodePk, ag::XformParams{}, pres, pin, &dp))) return st;

@@ -1447,8 +1447,10 @@ def test_per_call_server_jobs_and_restart(ctx):
         if i % 15 == 14:
             time.sleep(0.06)  # the server idles out; the next call relaunches it
     assert pk_calls >= 8
-    # the crate-API decoder (INTEGRATION.md Route A) from a random 32 of 64: the same job
-    dec = rs.ReedSolomonDecoder(ctx, 32, 32, 1024)
+    # the crate-API decoder (INTEGRATION.md Route A) from a random 32 of 64: the same job, on a
+    # fresh context whose first call is that job (the server needs the device tables)
+    fctx = rs.Context(0)
+    dec = rs.ReedSolomonDecoder(fctx, 32, 32, 1024)
     for it in range(6):
         orig = _shards(900 + it, 32, 1024)
         rec = o.encode(orig, 32)
@@ -1459,14 +1461,16 @@ def test_per_call_server_jobs_and_restart(ctx):
                 dec.add_original_shard(j, orig[j])
             else:
                 dec.add_recovery_shard(j - 32, rec[j - 32])
-        before = rs.server_jobs(ctx)["decode_pk"]
+        before = rs.server_jobs(fctx)["decode_pk"]
         res = dec.decode()
         assert sorted(res) == [i for i in range(32) if i not in keep]
         assert all(res[i] == orig[i] for i in res), it
         pk = 0 < len(res) < 32 or (len(res) == 32 and keep != set(range(32, 64)))
-        assert rs.server_jobs(ctx)["decode_pk"] - before == (1 if pk else 0)
+        assert rs.server_jobs(fctx)["decode_pk"] - before == (1 if pk else 0)
         if pk:
-            assert rs.last_decode_classes(ctx) == {"server_window64": 1}
+            assert rs.last_decode_classes(fctx) == {"server_window64": 1}
+    del dec
+    fctx.close()
 
 
 def test_server_timeout_abandons_staging_safely(ctx):  # ctx: torch initialises the device first
