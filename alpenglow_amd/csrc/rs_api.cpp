@@ -1728,6 +1728,9 @@ int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t m
     c->mb = static_cast<ag::LatencyMailbox*>(h);
     c->mb_dev = static_cast<ag::LatencyMailbox*>(d);
   }
+  // the server caches part of the log table at launch (kJobDecodePk's locator)
+  int st = c->ensure_tables();
+  if (st) return st;
   ag::LatencyMailbox* mb = c->mb;
   // Retire a job that did not complete: a queued or slow server that wakes later finds a quit
   // job instead.  It may already be inside the job, so the staging buffer the job names is
@@ -1749,7 +1752,6 @@ int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t m
   mb->mask = mask;
   if (dp) {
     std::memcpy(static_cast<void*>(&mb->dp), dp, sizeof *dp);
-    mb->tables = c->dtables();
   } else {
     std::memcpy(static_cast<void*>(&mb->p), &p, sizeof p);
   }
@@ -1763,7 +1765,7 @@ int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t m
       // no server (first call, or it idled out -- possibly just after this doorbell)
       if (__atomic_load_n(&mb->done, __ATOMIC_ACQUIRE) == seq) return AG_RS_OK;
       __atomic_store_n(&mb->alive, 2u, __ATOMIC_RELEASE);
-      if (ag::launch_latency_server(c->mb_dev, kServerIdleTicks, c->server_stream) != hipSuccess) {
+      if (ag::launch_latency_server(c->mb_dev, kServerIdleTicks, c->dtables().log, c->server_stream) != hipSuccess) {
         __atomic_store_n(&mb->alive, 0u, __ATOMIC_RELEASE);
         return AG_RS_ERR_DEVICE;
       }
@@ -1854,9 +1856,6 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, PinBuf& pin, cons
     dp.rows_w = 64;
     dp.any_k = 1;
     dp.fuse = 1;
-    // the server computes the locator constants from the device log / exp tables: they must
-    // exist before the first job (a context whose earlier calls all ran on the server has none)
-    if ((st = c->ensure_tables())) return st;
     std::fill(std::begin(c->last_classes), std::end(c->last_classes), uint64_t{0});
     ++c->last_classes[9];  // "server_window64"
     if ((st = server_job(c, ag::kJobDecodePk, ag::XformParams{}, pres, pin, &dp))) return st;

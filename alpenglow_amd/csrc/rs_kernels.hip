@@ -837,6 +837,38 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   });
 }
 
+__device__ __forceinline__ uint32_t m65535_add(uint32_t a, uint32_t b) {
+  const uint32_t s = a + b;
+  return s >= 65535u ? s - 65535u : s;
+}
+__device__ __forceinline__ uint32_t m65535_sub(uint32_t a, uint32_t b) { return a >= b ? a - b : a + 65535u - b; }
+__device__ __forceinline__ uint32_t m65535_mul(uint32_t a, uint32_t b) {  // canonical a, b < 65535
+  const uint32_t p = a * b;
+  uint32_t s = (p & 0xFFFFu) + (p >> 16);  // 2^16 = 1 (mod 65535)
+  s = (s & 0xFFFFu) + (s >> 16);
+  return s >= 65535u ? s - 65535u : s;
+}
+// the unnormalised Walsh transform over the 64 lanes (one residue per lane)
+__device__ __forceinline__ uint32_t walsh64(uint32_t v, int lane) {
+  static_for<6>([&](auto B) {
+    constexpr int d = 1 << decltype(B)::value;
+    const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
+    v = (lane & d) ? m65535_sub(o, v) : m65535_add(v, o);
+  });
+  return v;
+}
+// 128 points: position lane in v0, lane + 64 in v1
+__device__ __forceinline__ void walsh128(uint32_t& v0, uint32_t& v1, int lane) {
+  v0 = walsh64(v0, lane);
+  v1 = walsh64(v1, lane);
+  const uint32_t a = v0;
+  v0 = m65535_add(a, v1);
+  v1 = m65535_sub(a, v1);
+}
+__device__ __forceinline__ uint16_t locator_log(uint32_t loc, bool in) {  // exp of +loc (present), -loc (restored)
+  return static_cast<uint16_t>(in ? loc : 65535u - loc);
+}
+
 // =====================================================================================
 // decode_pk<OUTH>: decode_h8's W = 64 window for per-slice patterns on 1 KiB shreds (16 chunks
 // per shard: a 32-column tile is two slices) with the locator products packed.  In decode_h8 a
@@ -869,9 +901,30 @@ struct PkShared {
   uint64_t smask[2][2];           // per slice: positions present (loaded), restored
   uint8_t ilist[2][64], olist[2][64];  // per slice: survivor / restored positions by rank
 };
-template <int OUTH>
+// The per-call server's locator tables (built once per server launch): log x for the window's
+// 64 positions, and a^i, a^(256 i) (i < 256) in the polynomial basis, where a constant of the
+// decoder is to_poly(exp[l]) = a^l (the basis map sends exp[l] to the l-th power of the
+// polynomial generator, a^16 = a^5 + a^3 + a^2 + 1; checked for every l by
+// tests/test_oracle.py::test_poly_basis_powers) -- so the server needs no table lookups in HBM.
+struct PkLocTables {
+  uint16_t log64[64];
+  uint16_t apow_lo[256], apow_hi[256];
+};
+__device__ __forceinline__ uint32_t poly_mul(uint32_t a, uint32_t b) {  // GF(2)[a] / (a^16 + a^5 + a^3 + a^2 + 1)
+  uint32_t r = 0;
+  for (int i = 0; i < 16; ++i) r ^= ((b >> i) & 1) ? a << i : 0u;
+  for (int i = 30; i >= 16; --i) r ^= ((r >> i) & 1) ? (1u << i) ^ (0x2Du << (i - 16)) : 0u;
+  return r;
+}
+__device__ __forceinline__ uint32_t poly_pow_a(const PkLocTables& t, uint32_t l) {  // a^l, l <= 65535
+  return poly_mul(t.apow_hi[l >> 8], t.apow_lo[l & 255]);
+}
+
+// SRV: the per-call server's one-slice job; the locator constants of slice 0 are computed in
+// the list phase by wave 0 (decode_rows' Walsh route over `loc`) instead of read from p.rows.
+template <int OUTH, bool SRV = false>
 __device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t tile, uint4* lds, X8Flags* fl,
-                                               PkShared& sh) {
+                                               PkShared& sh, const PkLocTables* loc = nullptr) {
   static_assert(OUTH >= -1 && OUTH <= 1, "OUTH: the restored positions' window half, -1 both");
   using LB = X8Lay<2, 1, 3, 4, 5>;
   using LC = X8Lay<2, 3, 1, 4, 5>;
@@ -896,7 +949,16 @@ __device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t 
     if (sb0 + sl < nblk) {
       im = p.pmask[2 * (sb0 + sl)];
       om = p.pmask[2 * (sb0 + sl) + 1];
-      if (((im | om) >> j) & 1) lcoef[threadIdx.x] = p.rows[(sb0 + sl) * p.rows_w + j];
+      if constexpr (SRV) {
+        // wave 0 (slice 0): loc(x) = sum over erased e != x of log(x ^ e), as H(H(L) H(I)) / 64
+        const uint64_t e = ~im;
+        const uint32_t hl = m65535_mul(walsh64(j ? loc->log64[j] : 0u, static_cast<int>(j)), 1024u);
+        const uint32_t hi = walsh64(static_cast<uint32_t>((e >> j) & 1), static_cast<int>(j));
+        const uint32_t acc = walsh64(m65535_mul(hl, hi), static_cast<int>(j));
+        lcoef[threadIdx.x] = poly_pow_a(*loc, locator_log(acc, (im >> j) & 1));
+      } else if (((im | om) >> j) & 1) {
+        lcoef[threadIdx.x] = p.rows[(sb0 + sl) * p.rows_w + j];
+      }
     }
     const uint64_t below = (uint64_t{1} << j) - 1;
     if ((im >> j) & 1) ilist[sl][__builtin_popcountll(im & below)] = static_cast<uint8_t>(j);
@@ -923,12 +985,13 @@ __device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t 
     return is_rec ? p.rec + (g - rpos) * p.rec_shard_stride + blk * p.rec_block_stride + col * 64
                   : p.orig + (g - opos) * p.orig_shard_stride + blk * p.orig_block_stride + col * 64;
   };
-  // 2. packed input products: item i on row group i & 3 of slot (i >> 2) & 1 of wave i >> 3.
-  // Both items' loads are issued before either product (one HBM round trip per wave, not two)
+  // 2. packed input products: item i on row group i & 3 of wave (i >> 2) & 7, slot i >> 5 (a
+  // one-slice tile's 32 items fill all eight waves' first slot).  Both items' loads are issued
+  // before either product (one HBM round trip per wave, not two)
   uint32_t v[2][16];
   static_for<2>([&](auto U) {
     constexpr int u = decltype(U)::value;
-    const uint32_t i = wave * 8 + u * 4 + row;
+    const uint32_t i = u * 32 + wave * 4 + row;
     if (i < nin) {
       const uint32_t sl = i < nA ? 0u : 1u;
       const uint8_t* src = src_of(sl, ilist[sl][i - (sl ? nA : 0u)]);
@@ -946,8 +1009,8 @@ __device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t 
   });
   static_for<2>([&](auto U) {
     constexpr int u = decltype(U)::value;
-    if (static_cast<uint32_t>(wave * 8 + u * 4) < nin) {  // wave-uniform
-      const uint32_t i = wave * 8 + u * 4 + row;
+    if (static_cast<uint32_t>(u * 32 + wave * 4) < nin) {  // wave-uniform
+      const uint32_t i = u * 32 + wave * 4 + row;
       const bool ok = i < nin;
       const uint32_t sl = i < nA ? 0u : 1u;
       const uint32_t j = ok ? ilist[sl][i - (sl ? nA : 0u)] : 0u;
@@ -1099,12 +1162,13 @@ __device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t 
     constexpr int w2 = decltype(Wv)::value;
     x8_wait_ge(&flags.ready[w2 | kHi], 7 + D);
   });
-  // item o on row group o & 3 of slot (o >> 2) & (kPer / 4 - 1) of live wave o / kPer
+  // item o on row group o & 3 of live wave (o >> 2) % kLive, slot o / (4 kLive) (the first
+  // 4 kLive items spread over every live wave)
   constexpr int kPer = 64 / kLive;  // items per live wave
   static_for<kPer / 4>([&](auto U) {
     constexpr int u = decltype(U)::value;
-    if (static_cast<uint32_t>(lw * kPer + u * 4) < nout) {  // wave-uniform
-      const uint32_t o = lw * kPer + u * 4 + row;
+    if (static_cast<uint32_t>(u * 4 * kLive + lw * 4) < nout) {  // wave-uniform
+      const uint32_t o = u * 4 * kLive + lw * 4 + row;
       if (o < nout) {
         const uint32_t sl = o < noA ? 0u : 1u;
         const uint32_t j = olist[sl][o - (sl ? noA : 0u)];
@@ -1145,39 +1209,6 @@ __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p
 // (N = 64, or 128 with two positions per lane) serves every W <= N.  One wave per pattern,
 // lane-shuffle stages, no loop over the erased positions; exp depends only on the residue
 // (exp[65535] = exp[0]), so the constants are the loop form's bit for bit.
-namespace {
-__device__ __forceinline__ uint32_t m65535_add(uint32_t a, uint32_t b) {
-  const uint32_t s = a + b;
-  return s >= 65535u ? s - 65535u : s;
-}
-__device__ __forceinline__ uint32_t m65535_sub(uint32_t a, uint32_t b) { return a >= b ? a - b : a + 65535u - b; }
-__device__ __forceinline__ uint32_t m65535_mul(uint32_t a, uint32_t b) {  // canonical a, b < 65535
-  const uint32_t p = a * b;
-  uint32_t s = (p & 0xFFFFu) + (p >> 16);  // 2^16 = 1 (mod 65535)
-  s = (s & 0xFFFFu) + (s >> 16);
-  return s >= 65535u ? s - 65535u : s;
-}
-// the unnormalised Walsh transform over the 64 lanes (one residue per lane)
-__device__ __forceinline__ uint32_t walsh64(uint32_t v, int lane) {
-  static_for<6>([&](auto B) {
-    constexpr int d = 1 << decltype(B)::value;
-    const uint32_t o = static_cast<uint32_t>(__shfl_xor(static_cast<int>(v), d));
-    v = (lane & d) ? m65535_sub(o, v) : m65535_add(v, o);
-  });
-  return v;
-}
-// 128 points: position lane in v0, lane + 64 in v1
-__device__ __forceinline__ void walsh128(uint32_t& v0, uint32_t& v1, int lane) {
-  v0 = walsh64(v0, lane);
-  v1 = walsh64(v1, lane);
-  const uint32_t a = v0;
-  v0 = m65535_add(a, v1);
-  v1 = m65535_sub(a, v1);
-}
-__device__ __forceinline__ uint16_t locator_log(uint32_t loc, bool in) {  // exp of +loc (present), -loc (restored)
-  return static_cast<uint16_t>(in ? loc : 65535u - loc);
-}
-}  // namespace
 
 __global__ __launch_bounds__(256) void decode_rows_kernel(const uint64_t* __restrict__ emask,
                                                           const uint64_t* __restrict__ pmask, uint32_t npat,
@@ -2136,20 +2167,37 @@ hipError_t launch_decode_syn(unsigned chunk, const DecodeSynParams& p, hipStream
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* a) {
   return __hip_atomic_load(a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* mb, uint64_t idle_ticks) {
+__global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* mb, uint64_t idle_ticks,
+                                                                const uint16_t* log_t) {
   __shared__ uint4 lds[16 * 4 * kXfLanes];
   __shared__ X8Flags flags;
-  constexpr unsigned kXw = sizeof(XformParams) / 4, kDw = sizeof(DecodeXParams) / 4,
-                     kTw = sizeof(GfDeviceTables) / 4;
-  __shared__ __attribute__((aligned(16))) uint32_t job[kXw > kDw + kTw ? kXw : kDw + kTw];
+  constexpr unsigned kXw = sizeof(XformParams) / 4, kDw = sizeof(DecodeXParams) / 4;
+  __shared__ __attribute__((aligned(16))) uint32_t job[kXw > kDw ? kXw : kDw];
   __shared__ uint64_t mask;
   __shared__ uint32_t cmd;
   __shared__ PkShared pk;                 // kJobDecodePk: the tile's lists
   __shared__ uint64_t pk_mask[4];         // slice 0: present, restored; slice 1: none
-  __shared__ uint32_t pk_rows[64];        // slice 0's locator constants (polynomial basis)
+  __shared__ PkLocTables loc;             // kJobDecodePk: the locator's tables
   static_assert(sizeof(XformParams) % 4 == 0 && kXw <= 512, "params copy");
-  static_assert(sizeof(DecodeXParams) % 4 == 0 && sizeof(GfDeviceTables) % 4 == 0 && kDw + kTw <= 512,
-                "decode params copy");
+  static_assert(sizeof(DecodeXParams) % 4 == 0 && kDw <= 512, "decode params copy");
+  // the locator tables, once per launch: log x (x < 64) from the device table, a^i and a^(256 i)
+  // by square-and-multiply
+  if (threadIdx.x < 64) loc.log64[threadIdx.x] = log_t[threadIdx.x];
+  if (threadIdx.x < 256) {
+    uint32_t b = 2, bh = 2;  // a^(2^i) and a^(256 * 2^i) at step i
+    for (int q = 0; q < 8; ++q) bh = poly_mul(bh, bh);
+    uint32_t lo = 1, hi = 1;
+    for (int i = 0; i < 8; ++i) {
+      if ((threadIdx.x >> i) & 1) {
+        lo = poly_mul(lo, b);
+        hi = poly_mul(hi, bh);
+      }
+      b = poly_mul(b, b);
+      bh = poly_mul(bh, bh);
+    }
+    loc.apow_lo[threadIdx.x] = static_cast<uint16_t>(lo);
+    loc.apow_hi[threadIdx.x] = static_cast<uint16_t>(hi);
+  }
   uint32_t last = 0;
   if (threadIdx.x == 0) {
     last = sys_load(&mb->done);
@@ -2175,10 +2223,7 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
     const uint32_t kind = __builtin_amdgcn_readfirstlane(cmd);
     if (kind >= kJobQuit) break;
     if (kind == kJobDecodePk) {
-      if (threadIdx.x < kDw)
-        job[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->dp) + threadIdx.x);
-      else if (threadIdx.x >= 256 && threadIdx.x < 256 + kTw)
-        job[kDw + threadIdx.x - 256] = sys_load(reinterpret_cast<const uint32_t*>(&mb->tables) + threadIdx.x - 256);
+      if (threadIdx.x < kDw) job[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->dp) + threadIdx.x);
     } else if (threadIdx.x < kXw) {
       job[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->p) + threadIdx.x);
     }
@@ -2193,30 +2238,14 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
       // the tile reads its parameters from the LDS copy: a private copy would be indexed by the
       // rec / orig selects and land in scratch
       DecodeXParams& dp = *reinterpret_cast<DecodeXParams*>(job);
-      GfDeviceTables t;
-      uint32_t* tw = reinterpret_cast<uint32_t*>(&t);
-#pragma unroll
-      for (unsigned i = 0; i < kTw; ++i) tw[i] = __builtin_amdgcn_readfirstlane(job[kDw + i]);
-      const uint64_t present = mask;
-      if (threadIdx.x < 64) {
-        // decode_rows_kernel's Walsh route for the one pattern: erased = restored = ~present
-        const int lane = threadIdx.x;
-        const uint32_t x = static_cast<uint32_t>(lane);
-        const uint64_t e = ~present;
-        const uint32_t hl = m65535_mul(walsh64(x ? t.log[x] : 0u, lane), 1024u);
-        const uint32_t hi = walsh64(static_cast<uint32_t>((e >> x) & 1), lane);
-        const uint32_t acc = walsh64(m65535_mul(hl, hi), lane);
-        pk_rows[x] = dev::to_poly(t.exp[locator_log(acc, (present >> x) & 1)]);
-        if (lane == 0) {
-          pk_mask[0] = present;
-          pk_mask[1] = e;
-          pk_mask[2] = pk_mask[3] = 0;
-          dp.pmask = pk_mask;
-          dp.rows = pk_rows;
-        }
+      if (threadIdx.x == 0) {
+        pk_mask[0] = mask;   // present positions
+        pk_mask[1] = ~mask;  // restored: every absent data and coding position
+        pk_mask[2] = pk_mask[3] = 0;
+        dp.pmask = pk_mask;
       }
       __syncthreads();
-      decode_pk_tile<-1>(dp, 0, lds, &flags, pk);
+      decode_pk_tile<-1, true>(dp, 0, lds, &flags, pk, &loc);
       __threadfence_system();
       __syncthreads();
       if (threadIdx.x == 0) __hip_atomic_store(&mb->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2240,8 +2269,10 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
   if (threadIdx.x == 0) __hip_atomic_store(&mb->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-hipError_t launch_latency_server(LatencyMailbox* mb_dev, uint64_t idle_ticks, hipStream_t stream) {
-  hipLaunchKernelGGL(latency_server_kernel, dim3(1), dim3(512), 0, stream, mb_dev, idle_ticks);
+hipError_t launch_latency_server(LatencyMailbox* mb_dev, uint64_t idle_ticks, const uint16_t* log_t,
+                                 hipStream_t stream) {
+  if (!log_t) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(latency_server_kernel, dim3(1), dim3(512), 0, stream, mb_dev, idle_ticks, log_t);
   return hipGetLastError();
 }
 

@@ -200,8 +200,8 @@ hipError_t launch_decode_rows(const uint64_t* emask, const uint64_t* pmask, uint
 // kJobDecodePk: one 32:32 slice of 1 KiB shreds with exactly 32 shreds present (the follower's
 // deshred at its 32nd arriving shred, slot_block_data.rs:353): decode_pk<-1>'s window decode on
 // a one-slice tile, restoring every absent data and coding shred in place; `mask` = the present
-// window positions (bit j < 32: coding shred j, bit 32 + i: data shred i), the locator
-// constants are computed by the server (decode_rows' Walsh route) from `tables`.
+// window positions (bit j < 32: coding shred j, bit 32 + i: data shred i); the server computes
+// the locator constants itself (decode_rows' Walsh route, PkLocTables).
 enum LatencyJob : uint32_t {
   kJobEncode32 = 0,
   kJobDecode32 = 1,
@@ -216,10 +216,11 @@ struct LatencyMailbox {
   uint32_t kind;      // LatencyJob
   uint64_t mask;      // decode: store mask (bit s: shard s restored); pk: present positions
   XformParams p;      // in / out: device addresses of mapped host memory; p.out_mask ignored
-  DecodeXParams dp;   // kJobDecodePk: rec / orig / strides (pmask, rows set by the server)
-  GfDeviceTables tables;  // kJobDecodePk: the device log / exp tables
+  DecodeXParams dp;   // kJobDecodePk: rec / orig / strides (pmask set by the server; rows unused)
 };
-hipError_t launch_latency_server(LatencyMailbox* mb_dev, uint64_t idle_ticks, hipStream_t stream);
+// log_t: the device log table (the server caches log x for x < 64 at start)
+hipError_t launch_latency_server(LatencyMailbox* mb_dev, uint64_t idle_ticks, const uint16_t* log_t,
+                                 hipStream_t stream);
 
 // Generic (any geometry) table-driven kernels.  One thread per (block, symbol).
 

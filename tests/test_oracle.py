@@ -6,6 +6,7 @@ The oracle restates reed-solomon-simd 3.1.0; parity against the crate itself is 
 """
 
 import hashlib
+import os
 import random
 
 import numpy as np
@@ -13,6 +14,8 @@ import pytest
 
 import ro_c
 import rs_oracle as o
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def sha(b):
@@ -184,6 +187,44 @@ def test_window_locator_walsh_route(N, W):
                     want = (want + int(log[x ^ y])) % 65535
             assert got[x] == want, (x, got[x], want)
             assert int(exp[65535 - got[x]]) == int(exp[(65535 - want) % 65535])
+
+
+def test_poly_basis_powers():
+    """The per-call server's locator (rs_kernels.hip PkLocTables, poly_pow_a) computes a
+    decoder constant to_poly(exp[l]) as a^l in GF(2)[a] / (a^16 + a^5 + a^3 + a^2 + 1), from
+    the tables a^i and a^(256 i): to_poly (the basis map of rs_device.hpp, kBasisMat[0] of the
+    generated rs_consts.inc) sends exp[l] to the l-th power of the polynomial generator for
+    every l, exp[65535] included."""
+    import re
+
+    exp, _, _, _ = o.tables()
+    inc = open(os.path.join(ROOT, "alpenglow_amd", "csrc", "rs_consts.inc")).read()
+    body = re.search(r"kBasisMat\[2\]\[16\] = \{(.*?)\};", inc, re.S).group(1)
+    rows = [int(x, 0) for x in re.findall(r"0x[0-9A-Fa-f]+|\d+", body)][:16]
+
+    def to_poly(c):
+        return sum(((bin(rows[o_] & c).count("1") & 1) << o_) for o_ in range(16))
+
+    def pmul(a, b):
+        r = 0
+        for i in range(16):
+            if b >> i & 1:
+                r ^= a << i
+        for i in range(30, 15, -1):
+            if r >> i & 1:
+                r ^= (1 << i) ^ (0x2D << (i - 16))
+        return r
+
+    lo = [1]
+    for _ in range(255):
+        lo.append(pmul(lo[-1], 2))
+    a256 = pmul(lo[255], 2)
+    hi = [1]
+    for _ in range(255):
+        hi.append(pmul(hi[-1], a256))
+    tp = np.array([to_poly(int(x)) for x in exp[:65536]], np.int64)
+    got = np.array([pmul(hi[l_ >> 8], lo[l_ & 255]) for l_ in range(65536)], np.int64)
+    assert np.array_equal(tp, got)
 
 
 # ------------------------------------------------------------------------ layout & rate
