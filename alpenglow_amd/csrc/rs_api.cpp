@@ -163,6 +163,7 @@ struct ag_rs_ctx {
   uint64_t last_classes[16] = {};           // patterns per decoder class of the last decode call
   int decode_depth = 0;                     // decode_device nesting (tail restrides decode inside)
   uint32_t last_encode_kernels = 0;         // EncodeKernelBit of the last ag_rs_encode_batch / coder deshred batch
+  uint32_t last_window_kernels = 0;         // DecodeXKernelBit of the last coder deshred batch's window decode
   DevBuf d_syn, d_synblocks;                // syndrome decoder: patterns, block ids
   DevBuf d_corr, d_corrk, d_corrblocks;     // correction decoder: patterns, K picks, block ids
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
@@ -1278,6 +1279,14 @@ int ag_rs_internal_last_decode_classes(ag_rs_ctx* c, uint64_t* out16) {
 
 // Test aid (not in the header): the encode kernels (ag::EncodeKernelBit) the last
 // ag_rs_encode_batch call on this context launched.
+// Test aid (not in the header): the W = 64 window kernels (DecodeXKernelBit) the last coder
+// deshred batch on the context launched.
+int ag_rs_internal_last_window_kernels(ag_rs_ctx* c, uint32_t* out) {
+  if (!c || !out) return AG_RS_ERR_INVALID_ARGUMENT;
+  *out = c->last_window_kernels;
+  return AG_RS_OK;
+}
+
 // Test aid (not in the header): per-call server jobs posted on the context, per LatencyJob kind
 // (encode, decode, decode half, decode_pk).
 int ag_rs_internal_server_jobs(ag_rs_ctx* c, uint64_t* out4) {
@@ -2417,6 +2426,7 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   int st = c->enter();
   if (st) return st;
   c->last_encode_kernels = 0;  // the re-encode's kernels (test aid)
+  c->last_window_kernels = 0;  // the window decode's kernels (test aid)
   // One pattern for the whole batch (a repair batch; the reference bench's shape): one
   // pattern word on the host, no per-slice bookkeeping past the strip results.
   bool uniform = true;
@@ -3012,9 +3022,10 @@ int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw,
   uint8_t* few = c->d_pipe_few.as<uint8_t>() + s0;
   uint64_t* mask = c->d_pipe_mask.as<uint64_t>() + s0;
   int64_t* strip = c->d_strip.as<int64_t>() + s0;
-  // 1 KiB shreds (every maximum slice) decode on the packed window decoder, which also restores
-  // the absent coding shreds of exactly-k slices (few 2): the re-encode below skips those
-  const bool fuse = cps == 16;
+  // The window decode also restores the absent coding shreds of exactly-k slices (few 2): the
+  // re-encode below skips those.  1 KiB shreds (every maximum slice) run the packed decoder
+  // (decode_pk<-1>), the other whole-chunk sizes decode_h8<-1> (the full 64-point FFT).
+  const bool fuse = true;
   if (ag::launch_pipe_patterns(d_present, n, xm, few, fuse, c->stream) != hipSuccess ||
       ag::launch_decode_rows(xm, xm + n, static_cast<uint32_t>(n), static_cast<uint32_t>(W), c->dtables(), rows, true,
                              c->stream) != hipSuccess)
@@ -3038,7 +3049,8 @@ int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw,
   p.rows_w = static_cast<uint32_t>(W);
   p.any_k = 1;  // launch_pipe_patterns keeps exactly k survivors
   p.fuse = fuse ? 1u : 0u;
-  if (ag::launch_decode_x(static_cast<unsigned>(W), 0, p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
+  if (ag::launch_decode_x(static_cast<unsigned>(W), 0, p, (p.total_columns + 63) / 64, c->stream,
+                          &c->last_window_kernels) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   if (ag::launch_coder_strip(cw, cw_stride, static_cast<uint32_t>(k * S), n, strip, c->stream) != hipSuccess ||
       ag::launch_pipe_store_masks(few, strip, d_present, 1, n, mask, -AG_RS_ERR_NOT_ENOUGH_SHARDS,

@@ -815,6 +815,12 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
     const uint32_t j = posA(t);
     if ((qall >> t) & 1) {
       uint8_t* dst = p.orig + (DOUT + j - opos) * p.orig_shard_stride + off_o;
+      if constexpr (PASS == 0 && OUTH < 0) {
+        // fused coding restore (p.fuse, HighRate): an absent recovery position's value is the
+        // re-encoded coding shard; it goes back to its own slot (the ANY_K patterns of other
+        // callers never restore recovery positions)
+        if (DOUT + j < p.chunk) dst = const_cast<uint8_t*>(p.rec) + (DOUT + j) * p.rec_shard_stride + off_r;
+      }
       if constexpr (PASS == 2) {
         // + pass 1's partial, in planes.  The load is the youngest memory operation when it is
         // waited on (vmcnt(0)): the earlier slots' stores may alias it, so it is not hoisted
@@ -2022,8 +2028,12 @@ hipError_t launch_xform_lowrate_decode(unsigned j, const XformParams& p, hipStre
   return hipGetLastError();
 }
 
-hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream) {
+hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream,
+                           uint32_t* which) {
   if (ntiles == 0) return hipSuccess;
+  auto rec = [&](uint32_t bit) {
+    if (which) *which |= bit;
+  };
   if (ntiles > 0x7FFFFFFFull) return hipErrorInvalidValue;
   if (p.k + p.chunk > W || p.m > p.chunk || (p.low_rate && (p.k > p.chunk || p.m + p.chunk > W)))
     return hipErrorInvalidValue;
@@ -2045,16 +2055,27 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
     if (p.rows_w != 64) return hipErrorInvalidValue;
     const bool packed = pl && p.any_k && p.chunks_per_shard == 16 && (p.low_rate || p.chunk == 32);
     // fused coding restore: the caller's patterns restore absent coding positions too and skip
-    // those slices in the re-encode, which only decode_pk<-1> honours
-    if (p.fuse && (!packed || p.low_rate)) return hipErrorInvalidValue;
+    // those slices in the re-encode, which decode_pk<-1> and the full-FFT decode_h8<-1> honour
+    // (per-lane HighRate chunk 32 only)
+    if (p.fuse && (p.low_rate || !pl || p.chunk != 32)) return hipErrorInvalidValue;
     if (packed) {
       if (p.low_rate) hipLaunchKernelGGL((decode_pk_kernel<0>), g32, dim3(512), 0, stream, p);
       else if (p.fuse) hipLaunchKernelGGL((decode_pk_kernel<-1>), g32, dim3(512), 0, stream, p);
       else hipLaunchKernelGGL((decode_pk_kernel<1>), g32, dim3(512), 0, stream, p);
-    } else if (!pl) AG_X16(0, 0, 0);
-    else if (p.low_rate) AG_H8(0, 0, 0, 0);
-    else if (p.chunk == 32) AG_H8(1, 0, 0, 0);
-    else AG_H8(-1, 0, 0, 0);
+      rec(p.fuse ? kDxPkFused : kDxPk);
+    } else if (!pl) {
+      AG_X16(0, 0, 0);
+      rec(kDxX16);
+    } else if (p.low_rate) {
+      AG_H8(0, 0, 0, 0);
+      rec(kDxH8);
+    } else if (p.chunk == 32 && !p.fuse) {
+      AG_H8(1, 0, 0, 0);
+      rec(kDxH8);
+    } else {
+      AG_H8(-1, 0, 0, 0);  // (fused: restored positions in both window halves)
+      rec(p.fuse ? kDxH8Fused : kDxH8);
+    }
   } else if (W == 128 && (pass == 1 || pass == 2)) {
     // the originals must lie in one window half: LowRate k <= 64 (half 0); HighRate chunk 64
     // (half 1).  Both passes of a decode come from the same kernel family.

@@ -184,7 +184,10 @@ struct DecodeXParams {
 };
 // W = 32 / 64: pass 0.  W = 128: pass 1 (the other half's inputs, raw partial outputs), then
 // pass 2 (the output half's inputs, the partial added, output multiply); masks per pass.
-hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream);
+// which (optional): ORed with the DecodeXKernelBit of the W = 64 kernel launched (test aid)
+enum DecodeXKernelBit : uint32_t { kDxPkFused = 1, kDxPk = 2, kDxH8Fused = 4, kDxH8 = 8, kDxX16 = 16 };
+hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_t ntiles, hipStream_t stream,
+                           uint32_t* which = nullptr);
 hipError_t launch_decode_rows128(const uint64_t* m6, uint32_t npat, const GfDeviceTables& t, uint32_t* rows,
                                  hipStream_t stream);
 // rows for npat patterns: emask[p] = erased positions (locator), pmask as above.

@@ -172,6 +172,7 @@ def load():
     sigs["ag_rs_internal_last_encode_kernels"] = ([p, p], i)  # test aid, not in the header
     sigs["ag_rs_internal_fail_next_server_job"] = ([p], i)  # test aid, not in the header
     sigs["ag_rs_internal_server_jobs"] = ([p, p], i)  # test aid, not in the header
+    sigs["ag_rs_internal_last_window_kernels"] = ([p, p], i)  # test aid, not in the header
     for name, (args, res) in sigs.items():
         if not hasattr(L, name):  # older build (A/B timing of a previous commit); tests
             continue              # check the shipped library exports everything
@@ -388,6 +389,17 @@ def last_encode_kernels(ctx: Context) -> set:
     out = ctypes.c_uint32(0)
     _check(load().ag_rs_internal_last_encode_kernels(ctx.handle, ctypes.byref(out)), "last_encode_kernels")
     return {name for i, name in enumerate(ENCODE_KERNELS) if out.value >> i & 1}
+
+
+WINDOW_KERNELS = ("decode_pk_fused", "decode_pk", "decode_h8_fused", "decode_h8", "decode_x16")
+
+
+def last_window_kernels(ctx: Context) -> set:
+    """The W = 64 window kernels the last ``coder_deshred_batch`` on ``ctx`` launched (test aid;
+    the bits of ``ag::DecodeXKernelBit``, rs_launch.hpp)."""
+    out = ctypes.c_uint32(0)
+    _check(load().ag_rs_internal_last_window_kernels(ctx.handle, ctypes.byref(out)), "last_window_kernels")
+    return {name for i, name in enumerate(WINDOW_KERNELS) if out.value >> i & 1}
 
 
 SERVER_JOBS = ("encode32", "decode32", "decode32_half", "decode_pk")

@@ -37,6 +37,9 @@ def main():
                     help="the follower's real deshred: per slice, the first 32 of its 64 shreds to arrive "
                          "in a seeded random order (slot_block_data.rs:331-370 deshreds at the 32nd), so data "
                          "and coding shreds are lost in arbitrary per-slice patterns")
+    ap.add_argument("--payload-len", type=int, default=32767,
+                    help="payload bytes per slice (default MAX_DATA_PER_SLICE = 32767: 1 KiB shreds); the "
+                         "shred size is the padded length / 32 (reed_solomon.rs:94-95), e.g. 16383 -> 512 B")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
     import numpy as np
@@ -49,8 +52,10 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    n, S, m = args.slices, 1024, (64 if args.coding_only else 32)
-    L = 32 * S - 1  # MAX_DATA_PER_SLICE payload: pads to S = 1024 (reed_solomon.rs:94-95)
+    L = args.payload_len  # MAX_DATA_PER_SLICE by default: pads to S = 1024 (reed_solomon.rs:94-95)
+    if not 0 <= L <= 32767:
+        raise SystemExit("--payload-len must be in [0, 32767]")
+    n, S, m = args.slices, (L + 64 - L % 64) // 32, (64 if args.coding_only else 32)
     stride = (32 + m) * S
     cw = torch.empty((n, stride), dtype=torch.uint8, device=dev)
     rs.fill_splitmix(ctx, cw, n, 32 * S, stride, 0xC0DE0000)  # payload bytes in the data regions
@@ -113,10 +118,11 @@ def main():
         raw = o.coder_shred(host[i, :L].tobytes(), m)
         spot &= host[i, :32 * S].tobytes() == b"".join(raw.data)
         spot &= host[i, 32 * S:].tobytes() == b"".join(raw.coding)
+    size = "max slices" if L == 32767 else f"{L}-byte slices"
     line = {
-        "metric": ("slices/s ReedSolomonCoder shred + deshred (random 32 of 64 output shreds per slice), max slices"
+        "metric": (f"slices/s ReedSolomonCoder shred + deshred (random 32 of 64 output shreds per slice), {size}"
                    if args.random_patterns else
-                   "slices/s ReedSolomonCoder shred + deshred (first 32 output shreds lost), max slices"),
+                   f"slices/s ReedSolomonCoder shred + deshred (first 32 output shreds lost), {size}"),
         "value": n * args.steps / wall,
         "unit": "slices/s",
         "n_gpus": 1,

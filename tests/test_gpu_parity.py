@@ -834,16 +834,18 @@ def test_coder_deshred_uniform_lowrate_chunks(ctx, dev, S, keep, kernels):
         assert host[b, 32 * S:].tobytes() == b"".join(raw.coding), b
 
 
+@pytest.mark.parametrize("S", [1024, 512, 64])
 @pytest.mark.parametrize("mode", [rs.DECODE_ANY_K, rs.DECODE_EXACT])
-def test_coder_deshred_fused_coding_restore(ctx, dev, mode):
+def test_coder_deshred_fused_coding_restore(ctx, dev, mode, S):
     """The follower's deshred at exactly k = 32 kept shreds (slot_block_data.rs:343-355): the
-    packed window decoder restores the absent coding shreds in the same transform as the data
-    shreds (decode_pk<-1>, no re-encode pass), bit-exact against the oracle's re-encode
-    (o.encode of the restored data, reed_solomon.rs:206), mixed with slices that keep the
-    separate re-encode (surplus shreds; every data shred present), NotEnoughShreds and
-    InvalidPadding slices.  Every absent shred is overwritten with garbage first."""
-    rng = random.Random(0xF05E + mode)
-    n, S, m = 64, 1024, 32
+    window decoder restores the absent coding shreds in the same transform as the data shreds
+    (1 KiB shreds: decode_pk<-1>; other whole-chunk sizes: decode_h8<-1>; no re-encode pass),
+    bit-exact against the oracle's re-encode (o.encode of the restored data,
+    reed_solomon.rs:206), mixed with slices that keep the separate re-encode (surplus shreds;
+    every data shred present), NotEnoughShreds and InvalidPadding slices.  Every absent shred is
+    overwritten with garbage first.  The kernel record names the fused window kernel."""
+    rng = random.Random(0xF05E + mode + S)
+    n, m = 64, 32
     stride = (32 + m) * S
     lens = _payload_lens(rng, S, n)
     cw = np.zeros((n, stride), np.uint8)
@@ -896,6 +898,42 @@ def test_coder_deshred_fused_coding_restore(ctx, dev, mode):
         assert host[b, :32 * S].tobytes() == b"".join(raw.data), b
         assert host[b, 32 * S:].tobytes() == b"".join(raw.coding), b
     assert ok >= n - 4
+    assert rs.last_window_kernels(ctx) == {"decode_pk_fused" if S == 1024 else "decode_h8_fused"}
+
+
+@pytest.mark.parametrize("S", [1024, 256])
+def test_coder_deshred_fused_at_scale(ctx, dev, S):
+    """The fused route at production scale: 4096 slices, each received as a random 32 of its 64
+    shreds (absent shreds overwritten with garbage).  Every slice must come back as its
+    original codeword (data and coding shreds); the kernel record shows the fused window
+    decoder ran and no re-encode kernel was launched (no slice has surplus or every data
+    shred).  A sample of slices is also checked against the oracle's coder."""
+    rng = np.random.default_rng(0xFA57 + S)
+    n, m = 4096, 32
+    L = 32 * S - 1
+    stride = 64 * S
+    d_cw = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    rs.fill_splitmix(ctx, d_cw, n, 32 * S, stride, 0xF0F0)
+    rs.coder_shred_batch(ctx, m, n, S, None, 0, np.full(n, L, np.uint32), d_cw, stride)
+    want = d_cw.clone()
+    arrived = np.argsort(rng.random((n, 64)), axis=1)[:, :32]
+    present = np.zeros((n, 64), np.uint8)
+    np.put_along_axis(present, arrived, 1, axis=1)
+    pres = torch.from_numpy(present).to(dev)
+    view = d_cw.view(n, 64, S)
+    garbage = torch.full_like(view, 0xA5)
+    view.copy_(torch.where(pres.bool().unsqueeze(-1), view, garbage))
+    dp = np.ascontiguousarray(present[:, :32]).reshape(-1)
+    cp = np.ascontiguousarray(present[:, 32:]).reshape(-1)
+    res = rs.coder_deshred_batch(ctx, m, n, S, d_cw, stride, dp, cp, rs.DECODE_ANY_K, as_array=True)
+    assert (res == L).all()
+    assert torch.equal(d_cw, want)
+    assert rs.last_window_kernels(ctx) == {"decode_pk_fused" if S == 1024 else "decode_h8_fused"}
+    assert rs.last_encode_kernels(ctx) == set()  # the re-encode was skipped
+    host = want[:4].cpu().numpy()
+    for b in range(4):
+        raw = o.coder_shred(host[b, :L].tobytes(), m)
+        assert host[b].tobytes() == b"".join(raw.data) + b"".join(raw.coding), b
 
 
 # --------------------------------------------------------- host-memory (PCIe) pipeline

@@ -11,6 +11,7 @@
 #   point LABEL [ARGS]       one bench.py line (10 timed steps, no CPU baseline) -> points.jsonl
 #   points PRESET            a preset list of points: tail | lost | w128 | random | c4 | c4x64
 #   coder [ARGS]             bench_coder.py over its four arrival shapes -> coder.jsonl
+#   coder_short [ARGS]       bench_coder.py --random-patterns at four non-maximal payload lengths
 #   shredder                 bench_shredder.py -> shredder.json
 #   latency                  tools/bench_latency.py -> latency.json
 #   kt NAME [CMD...]         rocprofv3 --kernel-trace --stats of CMD (default: the headline
@@ -108,6 +109,13 @@ step() {
         timeout -k 10 300 $PY bench_coder.py $a --steps 5 --warmup 2 --no-cpu-baseline "$@" > $OUT/c.json 2> $OUT/c.err
         local rc=$?; [ $rc = 0 ] || { tail -5 $OUT/c.err; fail "coder '$a'" $rc; }
         jsonl_last $OUT/c.json "coder${a// /_}" $OUT/coder.jsonl
+      done ;;
+    coder_short)  # the follower's batches of non-maximal slices (whole-chunk and tail shred sizes)
+      for L in 16383 4095 2047 31999; do
+        timeout -k 10 300 $PY bench_coder.py --random-patterns --payload-len $L --steps 5 --warmup 2 --no-cpu-baseline "$@" \
+          > $OUT/c.json 2> $OUT/c.err
+        local rc=$?; [ $rc = 0 ] || { tail -5 $OUT/c.err; fail "coder_short $L" $rc; }
+        jsonl_last $OUT/c.json "coder_random_L$L" $OUT/coder.jsonl
       done ;;
     shredder)
       timeout -k 10 400 $PY bench_shredder.py "$@" > $OUT/shredder.json 2> $OUT/shredder.err
