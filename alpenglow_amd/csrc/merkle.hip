@@ -32,7 +32,11 @@ namespace {
 
 using sha::hash_pair;
 
-// SHA-256(LEAF_LABEL || data[0..len)).  A4: data is 4-byte aligned (word loads).
+// SHA-256(LEAF_LABEL || data[0..len)).  A4: data is 16-byte aligned (vector loads).
+// The blocks made only of data bytes (b = 1 .. T/64 - 1, T = 32 + len) are software-pipelined:
+// block b + 1's four 16-byte loads are issued before block b's compression, so each lane's
+// HBM latency (its leaf is 1 KiB away from its neighbours', one cache line per lane and
+// instruction) hides under ~1.2k VALU of rounds instead of stalling every block.
 template <bool A4>
 __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ data, uint32_t len, uint32_t out[8]) {
   uint32_t st[8];
@@ -48,29 +52,47 @@ __device__ __forceinline__ void leaf_hash(const uint8_t* __restrict__ data, uint
     }
   };
   auto byte = [&](uint32_t i) -> uint32_t { return data[i]; };
-  for (uint32_t b = 0; b < nblk; ++b) {
+  auto generic = [&](uint32_t b) __attribute__((always_inline)) {
     uint32_t w[16];
-    const uint32_t o0 = 64 * b;
-    if (b > 0 && o0 + 64 <= T) {  // a block of data only: words j0 .. j0 + 15
-      const uint32_t j0 = (o0 - 32) >> 2;
-      if constexpr (A4) {
 #pragma unroll
-        for (int i = 0; i < 16; i += 4) {
-          const uint4 x = *reinterpret_cast<const uint4*>(data + 4 * (j0 + i));  // 16-B aligned when A4 & 16|stride
-          w[i] = sha::bswap(x.x);
-          w[i + 1] = sha::bswap(x.y);
-          w[i + 2] = sha::bswap(x.z);
-          w[i + 3] = sha::bswap(x.w);
-        }
-      } else {
+    for (int i = 0; i < 16; ++i) w[i] = sha::leaf_msg_word(16 * b + i, len, nblk, word, byte);
+    sha::compress(st, w);
+  };
+  if constexpr (A4) {
+    const uint32_t nd = T / 64;  // blocks 1 .. nd - 1 are data only (words 16 b - 8 ..)
+    uint4 nx[4];
+    auto fetch = [&](uint32_t b) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) nx[q] = *reinterpret_cast<const uint4*>(data + 64 * b - 32 + 16 * q);
+    };
+    if (nd > 1) fetch(1);
+    generic(0);
+    for (uint32_t b = 1; b < nd; ++b) {
+      uint32_t w[16];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        w[4 * q] = sha::bswap(nx[q].x);
+        w[4 * q + 1] = sha::bswap(nx[q].y);
+        w[4 * q + 2] = sha::bswap(nx[q].z);
+        w[4 * q + 3] = sha::bswap(nx[q].w);
+      }
+      if (b + 1 < nd) fetch(b + 1);
+      sha::compress(st, w);
+    }
+    for (uint32_t b = nd > 1 ? nd : 1; b < nblk; ++b) generic(b);
+  } else {
+    for (uint32_t b = 0; b < nblk; ++b) {
+      uint32_t w[16];
+      const uint32_t o0 = 64 * b;
+      if (b > 0 && o0 + 64 <= T) {  // a block of data only: words j0 .. j0 + 15
+        const uint32_t j0 = (o0 - 32) >> 2;
 #pragma unroll
         for (int i = 0; i < 16; ++i) w[i] = sha::bswap(word(j0 + i));
+        sha::compress(st, w);
+      } else {
+        generic(b);
       }
-    } else {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) w[i] = sha::leaf_msg_word(16 * b + i, len, nblk, word, byte);
     }
-    sha::compress(st, w);
   }
 #pragma unroll
   for (int i = 0; i < 8; ++i) out[i] = st[i];
