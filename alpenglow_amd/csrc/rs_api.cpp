@@ -507,6 +507,10 @@ int decode_device(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, ui
                   const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
                   int mode);
 
+// ag_rs_coder_deshred_batch's flag packer (below): word b = data flags | coding 0..31 << 32
+bool pack_present_words(const uint8_t* dpres, const uint8_t* cpres, size_t m, size_t n, uint64_t* pres,
+                        bool* any_full_data);
+
 // The decode counterpart of encode_restrided: originals and recovery shards of a group of
 // blocks go to one padded buffer, the bitsliced decoders run there, and only the restored
 // originals are restrided back (a store mask per pattern).
@@ -514,17 +518,29 @@ int decode_restrided(ag_rs_ctx* c, size_t k, size_t m, size_t Sv, size_t sstride
                      uint8_t* orig, size_t ostride, const uint8_t* rec, size_t rstride, const uint8_t* opres,
                      const uint8_t* rpres, size_t npat, int mode) {
   const size_t Sp = padded_shard(Sv), per_block = (k + m) * Sp;
-  for (size_t p = 0; p < npat; ++p)  // NotEnoughShards before anything is launched
-    if (count_flags(opres + p * k, k) + count_flags(rpres + p * m, m) < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
   // store masks: the absent originals of each pattern (k <= 64 on every bitsliced path)
   // and the pack masks: only present shards are packed (decoders never read absent ones)
   std::vector<uint64_t> mask(3 * npat);
   const uint64_t kmask = k >= 64 ? ~uint64_t{0} : (uint64_t{1} << k) - 1;
   const bool rmask = m <= 64;
-  for (size_t p = 0; p < npat; ++p) {
-    mask[p] = ~pack_flags(opres + p * k, k) & kmask;
-    mask[npat + p] = pack_flags(opres + p * k, k);
-    mask[2 * npat + p] = rmask ? pack_flags(rpres + p * m, m) : 0;
+  if (k == 32 && m == 32) {  // the flags packed 32 at a time (AVX2 where the host has it)
+    std::vector<uint64_t> w(npat);
+    bool full_data = false;
+    (void)pack_present_words(opres, rpres, m, npat, w.data(), &full_data);
+    for (size_t p = 0; p < npat; ++p) {
+      if (__builtin_popcountll(w[p]) < 32) return AG_RS_ERR_NOT_ENOUGH_SHARDS;  // nothing launched yet
+      mask[p] = ~w[p] & kmask;
+      mask[npat + p] = w[p] & kmask;
+      mask[2 * npat + p] = w[p] >> 32;
+    }
+  } else {
+    for (size_t p = 0; p < npat; ++p)  // NotEnoughShards before anything is launched
+      if (count_flags(opres + p * k, k) + count_flags(rpres + p * m, m) < k) return AG_RS_ERR_NOT_ENOUGH_SHARDS;
+    for (size_t p = 0; p < npat; ++p) {
+      mask[p] = ~pack_flags(opres + p * k, k) & kmask;
+      mask[npat + p] = pack_flags(opres + p * k, k);
+      mask[2 * npat + p] = rmask ? pack_flags(rpres + p * m, m) : 0;
+    }
   }
   // upload only when the masks changed (steady-state batches reuse them, no sync)
   int st;
@@ -657,6 +673,78 @@ int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblock
   return decode_cols(c, k, m, S, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
 }
 
+constexpr int kNotApplicable = -1;
+
+// Per-block patterns of the 32:32 code on tiles that straddle blocks (chunks per shard not a
+// multiple of 64: the follower's slices, tail shreds' whole chunks and their restrided tails),
+// ANY_K, where some recovery shards are lost: the per-lane window decode with its masks built
+// on the device (launch_pipe_patterns, the coder batches' kernel), so the host only packs the
+// presence flags (AVX2) -- the per-pattern classification, window masks and mask compares cost
+// ~25 ns per pattern and call on the host, 3-7 ms per 131 072-block call
+// (profiles/r06_kt_tail_lose4_kernel_stats.csv against the call's wall time).  kNotApplicable
+// when some pattern has its full recovery set and lost data (the transform decodes those) --
+// the host route below takes the call then.
+int decode_cols_device_patterns(ag_rs_ctx* c, size_t S, size_t sstride, size_t nblocks, uint8_t* orig,
+                                size_t ostride, const uint8_t* rec, size_t rstride, const uint8_t* opres,
+                                const uint8_t* rpres) {
+  constexpr size_t k = 32, m = 32, W = 64;
+  const size_t n = nblocks, cps = S / 64;
+  int st;
+  if (c->present_ev) AG_HIP(hipEventSynchronize(c->present_ev));  // the previous upload has read h_present
+  else AG_HIP(hipEventCreateWithFlags(&c->present_ev, hipEventDisableTiming));
+  if ((st = c->h_present.ensure(n * 8))) return st;
+  uint64_t* pres = c->h_present.as<uint64_t>();
+  bool full_data = false;
+  (void)pack_present_words(opres, rpres, m, n, pres, &full_data);
+  size_t restore = 0;
+  for (size_t b = 0; b < n; ++b) {
+    const uint64_t w = pres[b];
+    if (__builtin_popcountll(w) < static_cast<int>(k)) return AG_RS_ERR_NOT_ENOUGH_SHARDS;  // nothing launched
+    const bool data_full = (w & 0xFFFFFFFFull) == 0xFFFFFFFFull;
+    if (!data_full && (w >> 32) == 0xFFFFFFFFull) return kNotApplicable;
+    restore += data_full ? 0 : 1;
+  }
+  c->last_classes[0] += n - restore;
+  c->last_classes[3] += restore;
+  if (!restore) return AG_RS_OK;
+  if ((st = c->ensure_tables()) || (st = c->d_present.ensure(n * 8, c->stream)) ||
+      (st = c->d_pipe_few.ensure(n, c->stream)) || (st = c->d_xmask.ensure(3 * n * 8, c->stream)) ||
+      (st = c->d_rows.ensure(n * W * 4, c->stream)))
+    return st;
+  c->xmask_host.clear();  // d_xmask / d_rows no longer hold the host route's cached patterns
+  c->xmask_w = 0;
+  AG_HIP(hipMemcpyAsync(c->d_present.ptr, pres, n * 8, hipMemcpyHostToDevice, c->stream));
+  AG_HIP(hipEventRecord(c->present_ev, c->stream));
+  uint64_t* xm = c->d_xmask.as<uint64_t>();
+  uint32_t* rows = c->d_rows.as<uint32_t>();
+  if (ag::launch_pipe_patterns(c->d_present.as<uint64_t>(), n, xm, c->d_pipe_few.as<uint8_t>(), false, c->stream) !=
+          hipSuccess ||
+      ag::launch_decode_rows(xm, xm + n, static_cast<uint32_t>(n), static_cast<uint32_t>(W), c->dtables(), rows, true,
+                             c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  ag::DecodeXParams p{};
+  p.rec = rec;
+  p.rec_block_stride = rstride;
+  p.rec_shard_stride = sstride;
+  p.orig = orig;
+  p.orig_block_stride = ostride;
+  p.orig_shard_stride = sstride;
+  p.pmask = xm + n;
+  p.rows = rows;
+  p.k = static_cast<uint32_t>(k);
+  p.m = static_cast<uint32_t>(m);
+  p.chunk = 32;
+  p.low_rate = 0;
+  p.chunks_per_shard = static_cast<uint32_t>(cps);
+  p.total_columns = static_cast<uint64_t>(n) * cps;
+  p.per_lane = 1;
+  p.rows_w = static_cast<uint32_t>(W);
+  p.any_k = 1;  // launch_pipe_patterns keeps exactly k survivors
+  if (ag::launch_decode_x(static_cast<unsigned>(W), 0, p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  return AG_RS_OK;
+}
+
 int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size_t nblocks, uint8_t* orig,
                 size_t ostride, const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres,
                 size_t npat, int mode) {
@@ -688,6 +776,11 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
   const size_t xw = hr == 1 ? next_pow2(xchunk + k) : x_lr ? 64 : 0;
   const size_t xm_rec = hr == 1 ? m : std::min<size_t>(m, 32);  // recovery shards inside the window
   const size_t cps = S / 64;
+  if (npat > 1 && npat == nblocks && hr == 1 && k == 32 && m == 32 && mode == AG_RS_DECODE_ANY_K && S % 64 == 0 &&
+      cps % 64 != 0 && aligned) {
+    const int st = decode_cols_device_patterns(c, S, sstride, nblocks, orig, ostride, rec, rstride, opres, rpres);
+    if (st != kNotApplicable) return st;
+  }
   // decode_x: one pattern per tile (single pattern, or tiles that never straddle blocks),
   // else per-lane patterns (each lane one chunk of one block: the follower's per-slice
   // patterns on 1 KiB shreds)

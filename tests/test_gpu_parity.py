@@ -1071,6 +1071,36 @@ def test_decode_per_slice_random_patterns(ctx, dev, S, n, mode):
     assert np.array_equal(got, blocks)
 
 
+@pytest.mark.parametrize("S,n", [(1024, 300), (960, 257), (1000, 300), (192, 131), (64, 600), (2000, 90)])
+def test_decode_device_patterns_lost_coding(ctx, dev, S, n):
+    """Per-block patterns of the 32:32 code with lost coding shreds on tiles that straddle blocks
+    (S < 4 KiB, and the whole chunks plus restrided tail of S = 1000 / 2000): the window decode
+    with its masks built on the device from the packed presence words (decode_cols_device_
+    patterns).  Random 8-20 data shards erased and 1-12 coding shards lost per block, a few
+    blocks with every data shard present; absent shards overwritten with garbage; ANY_K.
+    Compared with the original data, and the class record counts every block's pattern."""
+    rng = random.Random(S * 13 + n)
+    k = m = 32
+    blocks = _blocks(4400 + S, n, k, S)
+    rec = ro_c.encode_blocks(blocks, m, threads=8)
+    d_o, d_r, op, rp = blocks.copy(), rec.copy(), [], []
+    restore = 0
+    for b in range(n):
+        lost_c = set(rng.sample(range(m), rng.randint(1, 12)))
+        erased = set() if b % 11 == 3 else set(rng.sample(range(k), rng.randint(8, min(20, m - len(lost_c)))))
+        restore += 1 if erased else 0
+        op += [0 if i in erased else 1 for i in range(k)]
+        rp += [0 if j in lost_c else 1 for j in range(m)]
+        for i in erased:
+            d_o[b, i] = 0x77
+        for j in lost_c:
+            d_r[b, j] = 0x99
+    got = gpu_decode(ctx, dev, d_o, d_r, op, rp, rs.DECODE_ANY_K)
+    assert np.array_equal(got, blocks)
+    parts = 1 if S % 64 == 0 else 2  # whole chunks, then the restrided tail: both add patterns
+    assert rs.last_decode_classes(ctx) == {"window64": parts * restore, "none": parts * (n - restore)}
+
+
 @pytest.mark.parametrize("k,m,n", [(32, 32, 25), (32, 32, 64), (32, 64, 11), (20, 40, 9)])
 def test_packed_window64_follower(ctx, dev, k, m, n):
     """decode_pk (the W = 64 window with packed locator products) on 1 KiB shreds, ANY_K: the
