@@ -15,7 +15,8 @@
 #   shredder                 bench_shredder.py -> shredder.json
 #   latency                  tools/bench_latency.py -> latency.json
 #   kt NAME [CMD...]         rocprofv3 --kernel-trace --stats of CMD (default: the headline
-#                            bench) into gpurun_out/kt_NAME
+#                            bench without the configs[4] stream, so every launch has the
+#                            4096-block shape) into gpurun_out/kt_NAME
 #   pmc NAME PASSES [CMD...] rocprofv3 --pmc, one run per ';'-separated counter pass, into
 #                            gpurun_out/pmc_NAME/p<i>; then tools/pmc_summary.py
 #   stress                   tools/stress_xform64.py (repeated per-block-mask reconstructs)
@@ -125,7 +126,7 @@ step() {
       local rc=$?; echo "latency exit $rc"; cat $OUT/latency.json; [ $rc = 0 ] || fail latency $rc ;;
     kt)
       local tag=$1; shift
-      [ $# -gt 0 ] || set -- $PY bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-verify
+      [ $# -gt 0 ] || set -- $PY bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-verify --strong-stream 0
       rm -rf $OUT/kt_$tag
       timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/kt_$tag -o kt --output-format csv -- "$@" \
         > $OUT/kt_$tag.log 2>&1
@@ -133,7 +134,7 @@ step() {
       find $OUT/kt_$tag -name "*kernel_stats.csv" -exec head -8 {} \; | cut -c1-200 ;;
     pmc)
       local tag=$1 passes=$2; shift 2
-      [ $# -gt 0 ] || set -- $PY bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify
+      [ $# -gt 0 ] || set -- $PY bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify --strong-stream 0
       rm -rf $OUT/pmc_$tag
       local i=0 p
       IFS=';' read -ra PS <<< "$passes"
