@@ -181,7 +181,7 @@ struct ag_rs_ctx {
   hipEvent_t lens_ev = nullptr;             // recorded after its upload
   PinBuf h_strip;                           // coder deshred batches: pinned staging of the results
   DevBuf d_ed_base;                         // Ed25519 fixed-base table (ed25519.hpp)
-  static constexpr int kPipeBufs = 27;
+  static constexpr int kPipeBufs = 28;
   DevBuf pipe[kPipeBufs];                   // composed shredder scratch (ag_shredder_*_batch)
   DevBuf d_sh_roots, d_sh_commit, d_sh_onvalid, d_sh_list;  // shred validation scratch
   DevBuf stage_in, stage_out;             // host-memory calls (unused; see slots)
@@ -3268,6 +3268,7 @@ int ag_shredder_shred_batch(ag_rs_ctx* c, size_t nslices, size_t S, const uint8_
   ag::PipeExpandParams ep{};
   ep.nslices = n;
   ep.shred_bytes = static_cast<uint32_t>(S);
+  ep.num_data = ag::kPipeData;
   ep.kind = kind;
   ep.shred_index = reinterpret_cast<uint32_t*>(sidx);
   ep.data_len = reinterpret_cast<uint32_t*>(dlen);
@@ -3342,6 +3343,7 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   ag::PipePickParams pp{};
   pp.nslices = n;
   pp.shred_bytes = static_cast<uint32_t>(S);
+  pp.num_data = ag::kPipeData;
   pp.wire_status = wire;
   pp.cols = cols;
   pp.pick = pick;
@@ -3386,6 +3388,7 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   ag::PipeCheckParams kp{};
   kp.nslices = n;
   kp.shred_bytes = static_cast<uint32_t>(S);
+  kp.num_data = ag::kPipeData;
   kp.wire_status = wire;
   kp.val_status = vstat;
   kp.roots = roots;
@@ -3507,6 +3510,7 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   ag::PipeExpandParams ep{};
   ep.nslices = n;
   ep.shred_bytes = static_cast<uint32_t>(S);
+  ep.num_data = ag::kPipeData;
   ep.skip = d_present;
   ep.slice_ok = d_ok;
   ep.kind = kind;
@@ -3526,6 +3530,350 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
           hipSuccess)
     return AG_RS_ERR_DEVICE;
   AG_HIP(hipStreamSynchronize(c->stream));  // host vectors read by async copies
+  return AG_RS_OK;
+}
+
+
+// ---- the other three shredders of shredder.rs composed (CodingOnly, PETS, AONT) -------------
+// (outside extern "C": helpers)
+}  // extern "C"
+
+namespace {
+// Output shred j of a slice <-> codeword row (data rows 0..31, coding rows 32..32+m-1):
+// Regular / AONT: j; CodingOnly: 32 + j (the 64 coding shreds, no data shreds: shredder.rs:
+// 367-376); PETS: j for j < 31, 32 + (j - 31) after (the data shred holding the key dropped,
+// :414-422).  A run [out0, out0 + count) of output rows is codeword rows [row0, row0 + count).
+struct OutRun {
+  uint32_t out0, row0, count;
+};
+struct ShredderKind {
+  uint32_t m;         // coding shreds of the coder (ReedSolomonCoder::new(CODING_OUTPUT_SHREDS))
+  uint32_t num_data;  // DATA_OUTPUT_SHREDS
+  int aon;            // AG_AON_* or -1
+  OutRun runs[2];
+  int nruns;
+};
+bool shredder_kind(int kind, ShredderKind* k) {
+  switch (kind) {
+    case AG_SHREDDER_CODING_ONLY: *k = {64, 0, -1, {{0, 32, 64}, {0, 0, 0}}, 1}; return true;
+    case AG_SHREDDER_PETS: *k = {33, 31, AG_AON_PETS, {{0, 0, 31}, {31, 32, 33}}, 2}; return true;
+    case AG_SHREDDER_AONT: *k = {32, 32, AG_AON_AONT, {{0, 0, 64}, {0, 0, 0}}, 1}; return true;
+    default: return false;
+  }
+}
+// rows (64 * S per slice) <-> codewords (cw_stride per slice), every run of the map
+int copy_runs(ag_rs_ctx* c, const ShredderKind& k, size_t n, size_t S, uint8_t* rows, uint8_t* cw, size_t cw_stride,
+              bool to_rows) {
+  for (int i = 0; i < k.nruns; ++i) {
+    const OutRun& r = k.runs[i];
+    uint8_t* a = rows + r.out0 * S;
+    uint8_t* b = cw + r.row0 * S;
+    const hipError_t e = to_rows ? hipMemcpy2DAsync(a, ag::kPipeShreds * S, b, cw_stride, r.count * S, n,
+                                                    hipMemcpyDeviceToDevice, c->stream)
+                                 : hipMemcpy2DAsync(b, cw_stride, a, ag::kPipeShreds * S, r.count * S, n,
+                                                    hipMemcpyDeviceToDevice, c->stream);
+    if (e != hipSuccess) return AG_RS_ERR_DEVICE;
+  }
+  return AG_RS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ag_shredder_shred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_t S, const uint8_t* parent_flags,
+                                 const uint8_t* parent_ids, const uint8_t* data, size_t data_stride,
+                                 const uint32_t* data_lens, const uint64_t* slots, const uint64_t* slice_indices,
+                                 const uint8_t* is_last, const uint8_t* seed, const uint8_t* pk, const uint8_t* keys,
+                                 uint8_t* codewords, size_t cw_stride, uint8_t* roots_out, uint8_t* sigs_out,
+                                 uint8_t* packets, size_t packet_stride, uint32_t* packet_lens) {
+  if (kind == AG_SHREDDER_REGULAR) {
+    if (cw_stride != ag::kPipeShreds * S) return AG_RS_ERR_INVALID_ARGUMENT;
+    return ag_shredder_shred_batch(c, nslices, S, parent_flags, parent_ids, data, data_stride, data_lens, slots,
+                                   slice_indices, is_last, seed, pk, codewords, roots_out, sigs_out, packets,
+                                   packet_stride, packet_lens);
+  }
+  ShredderKind k;
+  if (!c || !shredder_kind(kind, &k) || !pipe_args_ok(nslices, S, codewords, packets, packet_lens) ||
+      cw_stride < (kDataShreds + k.m) * S || cw_stride % 4 ||
+      (nslices && (!parent_flags || !parent_ids || !data_lens || !slots || !slice_indices || !is_last || !seed ||
+                   !pk || (k.aon >= 0 && !keys))))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (nslices == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  const size_t n = nslices, N = n * ag::kPipeShreds;
+  // MAX_DATA_SIZE: the key tail of PETS / AONT must fit the slice as well (shredder.rs:409, 457)
+  const size_t extra = k.aon >= 0 ? ag::kCipherKeyBytes : 0;
+  for (size_t b = 0; b < n; ++b) {
+    const size_t framed = 1 + (parent_flags[b] ? AG_SLICE_BLOCK_ID_BYTES : 0) + 8 + size_t{data_lens[b]};
+    if (framed + extra > kMaxPayload) return AG_RS_ERR_TOO_MUCH_DATA;
+  }
+  // 1. Slice::payload_bytes into the data regions; 2. PETS / AONT: encrypt_with_random_key with
+  //    the caller's key + the key tail; 3. ReedSolomonCoder::shred in place
+  std::vector<uint32_t> lens(n);
+  int st = ag_slice_frame_batch(c, n, S, parent_flags, parent_ids, data, data_stride, data_lens, codewords, cw_stride,
+                                lens.data());
+  if (st) return st;
+  if (k.aon >= 0) {
+    if ((st = ag_aon_encrypt_batch(c, k.aon, n, keys, codewords, cw_stride, lens.data()))) return st;
+    for (uint32_t& l : lens) l += static_cast<uint32_t>(ag::kCipherKeyBytes);
+  }
+  if ((st = ag_rs_coder_shred_batch(c, k.m, n, S, nullptr, 0, lens.data(), codewords, cw_stride))) return st;
+  // 4. the 64 output shreds (data first) as rows; Merkle tree, signature, datagrams over them
+  uint8_t *rows, *roots = roots_out, *sigs = sigs_out, *proofs, *kcol, *sidx, *dlen, *height;
+  if ((st = pipe_buf(c, 27, N * S, &rows))) return st;
+  if ((st = copy_runs(c, k, n, S, rows, codewords, cw_stride, true))) return st;
+  if (!roots && (st = pipe_buf(c, 0, 32 * n, &roots))) return st;
+  if (!sigs && (st = pipe_buf(c, 1, 64 * n, &sigs))) return st;
+  if ((st = pipe_buf(c, 2, kPipeProofBytes * N, &proofs)) || (st = pipe_buf(c, 3, N, &kcol)) ||
+      (st = pipe_buf(c, 4, 4 * N, &sidx)) || (st = pipe_buf(c, 5, 4 * N, &dlen)) ||
+      (st = pipe_buf(c, 6, 4 * N, &height)))
+    return st;
+  if ((st = ag_merkle_build_batch(c, ag::kPipeShreds, S, n, rows, S, ag::kPipeShreds * S, roots, nullptr, 0, proofs,
+                                  ag::kPipeShreds * kPipeProofBytes)))
+    return st;
+  if ((st = ag_slice_sign_batch(c, n, seed, pk, slots, slice_indices, is_last, roots, sigs, nullptr))) return st;
+  ag::PipeExpandParams ep{};
+  ep.nslices = n;
+  ep.shred_bytes = static_cast<uint32_t>(S);
+  ep.num_data = k.num_data;
+  ep.kind = kcol;
+  ep.shred_index = reinterpret_cast<uint32_t*>(sidx);
+  ep.data_len = reinterpret_cast<uint32_t*>(dlen);
+  ep.height = reinterpret_cast<uint32_t*>(height);
+  if (ag::launch_pipe_expand(ep, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  ag::ShredColumns cols{};
+  cols.kind = kcol;
+  cols.slot = const_cast<uint64_t*>(slots);
+  cols.slice_index = const_cast<uint64_t*>(slice_indices);
+  cols.is_last = const_cast<uint8_t*>(is_last);
+  cols.shred_index = ep.shred_index;
+  cols.data = rows;
+  cols.data_stride = S;
+  cols.data_len = ep.data_len;
+  cols.sig = sigs;
+  cols.proof = proofs;
+  cols.proof_stride = kPipeProofBytes;
+  cols.height = ep.height;
+  cols.hdr_group = ag::kPipeShreds;
+  if (ag::launch_shred_serialize(cols, N, packets, packet_stride, packet_lens, c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  return AG_RS_OK;
+}
+
+int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_t S, uint8_t* packets,
+                                   size_t packet_stride, uint32_t* packet_lens, const uint8_t* pk, uint8_t* codewords,
+                                   size_t cw_stride, int32_t* status, uint64_t* slots_out, uint64_t* slice_indices_out,
+                                   uint8_t* is_last_out, uint8_t* parent_flags_out, uint8_t* parent_ids_out,
+                                   uint32_t* data_offsets_out, uint32_t* data_lens_out) {
+  if (kind == AG_SHREDDER_REGULAR) {
+    if (cw_stride != ag::kPipeShreds * S) return AG_RS_ERR_INVALID_ARGUMENT;
+    return ag_shredder_deshred_batch(c, nslices, S, packets, packet_stride, packet_lens, pk, codewords, status,
+                                     slots_out, slice_indices_out, is_last_out, parent_flags_out, parent_ids_out,
+                                     data_offsets_out, data_lens_out);
+  }
+  ShredderKind k;
+  if (!c || !shredder_kind(kind, &k) || !pipe_args_ok(nslices, S, codewords, packets, packet_lens) ||
+      cw_stride < (kDataShreds + k.m) * S || cw_stride % 4 ||
+      (nslices && (!pk || !status || !slots_out || !slice_indices_out || !is_last_out || !parent_flags_out ||
+                   !parent_ids_out || !data_offsets_out || !data_lens_out)))
+    return AG_RS_ERR_INVALID_ARGUMENT;
+  if (nslices == 0) return AG_RS_OK;
+  if (c->enter()) return AG_RS_ERR_DEVICE;
+  const size_t n = nslices, N = n * ag::kPipeShreds;
+  int st;
+  // per-shred columns; payload rows into `rows` (row 64 s + j = output shred j of slice s)
+  uint8_t *rows, *kcol, *slot, *sidx, *last, *shidx, *dlen, *sig, *proof, *height, *wire, *vstat, *roots;
+  if ((st = pipe_buf(c, 27, N * S, &rows)) || (st = pipe_buf(c, 0, N, &kcol)) || (st = pipe_buf(c, 1, 8 * N, &slot)) ||
+      (st = pipe_buf(c, 2, 8 * N, &sidx)) || (st = pipe_buf(c, 3, N, &last)) || (st = pipe_buf(c, 4, 4 * N, &shidx)) ||
+      (st = pipe_buf(c, 5, 4 * N, &dlen)) || (st = pipe_buf(c, 6, 64 * N, &sig)) ||
+      (st = pipe_buf(c, 7, kPipeProofBytes * N, &proof)) || (st = pipe_buf(c, 8, 4 * N, &height)) ||
+      (st = pipe_buf(c, 9, N, &wire)) || (st = pipe_buf(c, 10, N, &vstat)) || (st = pipe_buf(c, 11, 32 * N, &roots)))
+    return st;
+  ag::ShredColumns cols{};
+  cols.kind = kcol;
+  cols.slot = reinterpret_cast<uint64_t*>(slot);
+  cols.slice_index = reinterpret_cast<uint64_t*>(sidx);
+  cols.is_last = last;
+  cols.shred_index = reinterpret_cast<uint32_t*>(shidx);
+  cols.data = rows;
+  cols.data_stride = S;
+  cols.data_len = reinterpret_cast<uint32_t*>(dlen);
+  cols.sig = sig;
+  cols.proof = proof;
+  cols.proof_stride = kPipeProofBytes;
+  cols.height = reinterpret_cast<uint32_t*>(height);
+  // 1. network::deserialize
+  if (ag::launch_shred_deserialize(packets, packet_stride, packet_lens, N, cols, wire, c->stream) != hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  // 2. ValidatedShred::try_new with the blockstore's cached commitment (the Regular pipeline's
+  //    steps 2-3 with this shredder's data / coding layout)
+  uint8_t *pick, *gdata, *gproof, *gslot, *gsidx, *glast, *gidx, *gsig, *pstat, *commits, *hasc, *plaus;
+  if ((st = pipe_buf(c, 12, n, &pick)) || (st = pipe_buf(c, 13, n * S, &gdata)) ||
+      (st = pipe_buf(c, 14, kPipeProofBytes * n, &gproof)) || (st = pipe_buf(c, 15, 8 * n, &gslot)) ||
+      (st = pipe_buf(c, 16, 8 * n, &gsidx)) || (st = pipe_buf(c, 17, n, &glast)) || (st = pipe_buf(c, 18, 4 * n, &gidx)) ||
+      (st = pipe_buf(c, 19, 64 * n, &gsig)) || (st = pipe_buf(c, 20, n, &pstat)) ||
+      (st = pipe_buf(c, 21, ag::kSliceCommitmentLen * n, &commits)) || (st = pipe_buf(c, 22, n, &hasc)) ||
+      (st = pipe_buf(c, 24, N, &plaus)))
+    return st;
+  ag::PipePickParams pp{};
+  pp.nslices = n;
+  pp.shred_bytes = static_cast<uint32_t>(S);
+  pp.num_data = k.num_data;
+  pp.wire_status = wire;
+  pp.cols = cols;
+  pp.pick = pick;
+  pp.g_data = gdata;
+  pp.g_proof = gproof;
+  pp.g_slot = reinterpret_cast<uint64_t*>(gslot);
+  pp.g_slice_index = reinterpret_cast<uint64_t*>(gsidx);
+  pp.g_is_last = glast;
+  pp.g_shred_index = reinterpret_cast<uint32_t*>(gidx);
+  pp.g_sig = gsig;
+  pp.plausible = plaus;
+  AG_HIP(hipMemsetAsync(gdata, 0, n * S, c->stream));
+  AG_HIP(hipMemsetAsync(gidx, 0, 4 * n, c->stream));
+  if (ag::launch_pipe_pick(pp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  if ((st = shred_validate_impl(c, n, gdata, S, S, pp.g_shred_index, gproof, kPipeProofBytes, ag::kPipeHeight,
+                                pp.g_slot, pp.g_slice_index, glast, gsig, 64, pk, nullptr, nullptr, 1, nullptr, pstat,
+                                nullptr, commits)))
+    return st;
+  if (ag::launch_pipe_cache_flags(pick, pstat, n, hasc, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  if ((st = shred_validate_impl(c, N, rows, S, S, cols.shred_index, proof, kPipeProofBytes, ag::kPipeHeight,
+                                cols.slot, cols.slice_index, last, sig, 64, pk, commits, hasc, ag::kPipeShreds, plaus,
+                                vstat, roots, nullptr)))
+    return st;
+  // 3. per slice: the shreds kept, the root, header and signature
+  uint8_t* per_slice;
+  if ((st = pipe_buf(c, 23, (8 + 8 + 8 + 32 + 32 + 64 + 8) * n, &per_slice))) return st;
+  uint8_t* sroot = per_slice;
+  uint8_t* roots2 = sroot + 32 * n;
+  uint8_t* ssig = roots2 + 32 * n;
+  uint64_t* d_present = reinterpret_cast<uint64_t*>(ssig + 64 * n);
+  uint64_t* d_slot = d_present + n;
+  uint8_t* ssidx = reinterpret_cast<uint8_t*>(d_slot + n);
+  uint8_t* slast = ssidx + 8 * n;
+  ag::PipeCheckParams kp{};
+  kp.nslices = n;
+  kp.shred_bytes = static_cast<uint32_t>(S);
+  kp.num_data = k.num_data;
+  kp.wire_status = wire;
+  kp.val_status = vstat;
+  kp.roots = roots;
+  kp.cols = cols;
+  kp.present = d_present;
+  kp.root = sroot;
+  kp.slot = d_slot;
+  kp.slice_index = reinterpret_cast<uint64_t*>(ssidx);
+  kp.is_last = slast;
+  kp.sig = ssig;
+  if (ag::launch_pipe_check(kp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  std::vector<uint64_t> h_present(n), h_slot(n), h_sidx(n);
+  std::vector<uint8_t> h_last(n);
+  AG_HIP(hipMemcpyAsync(h_present.data(), d_present, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipMemcpyAsync(h_slot.data(), d_slot, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipMemcpyAsync(h_sidx.data(), ssidx, 8 * n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipMemcpyAsync(h_last.data(), slast, n, hipMemcpyDeviceToHost, c->stream));
+  AG_HIP(hipStreamSynchronize(c->stream));
+  // 4. deshred_validated_shreds: ReedSolomonCoder::deshred with the crate's decoder over every
+  //    kept shred (EXACT; the kept output rows scattered to their codeword rows), then
+  //    decrypt_payload (PETS / AONT) after the raw shreds are taken
+  if ((st = copy_runs(c, k, n, S, rows, codewords, cw_stride, false))) return st;
+  std::vector<uint8_t> dp(n * kDataShreds, 0), cp(n * k.m, 0);
+  for (size_t s = 0; s < n; ++s)
+    for (int i = 0; i < k.nruns; ++i)
+      for (uint32_t u = 0; u < k.runs[i].count; ++u) {
+        const uint32_t j = k.runs[i].out0 + u, r = k.runs[i].row0 + u;
+        const uint8_t bit = static_cast<uint8_t>((h_present[s] >> j) & 1);
+        if (r < kDataShreds) dp[s * kDataShreds + r] = bit;
+        else cp[s * k.m + (r - kDataShreds)] = bit;
+      }
+  std::vector<int64_t> plen(n);
+  if ((st = ag_rs_coder_deshred_batch(c, k.m, n, S, codewords, cw_stride, dp.data(), cp.data(), AG_RS_DECODE_EXACT,
+                                      plen.data())))
+    return st;
+  // the raw shreds of the output (restored data, re-encoded coding) back to rows: 5. rebuilds
+  // the tree over them, 7. serializes the absent ones
+  if ((st = copy_runs(c, k, n, S, rows, codewords, cw_stride, true))) return st;
+  if (k.aon >= 0) {
+    std::vector<uint32_t> cl(n);
+    for (size_t s = 0; s < n; ++s) cl[s] = plen[s] >= 0 ? static_cast<uint32_t>(plen[s]) : 0;
+    std::vector<int64_t> pl(n);
+    if ((st = ag_aon_decrypt_batch(c, k.aon, n, codewords, cw_stride, cl.data(), pl.data()))) return st;
+    for (size_t s = 0; s < n; ++s)
+      if (plen[s] >= 0) plen[s] = pl[s];  // decrypt_payload's BadEncoding for a tail-less buffer
+  }
+  // 5. check_merkle_tree over the raw output shreds
+  const size_t nodes_stride = (32 * ag_merkle_node_count(ag::kPipeShreds) + 255) / 256 * 256;
+  if ((st = c->d_merkle_nodes.ensure(n * nodes_stride, c->stream)) || (st = ensure_empty_roots(c))) return st;
+  {
+    ag::MerkleBuildParams mb{};
+    mb.leaves = rows;
+    mb.leaf_stride = S;
+    mb.slice_stride = ag::kPipeShreds * S;
+    mb.leaf_bytes = static_cast<uint32_t>(S);
+    mb.n_leaves = ag::kPipeShreds;
+    mb.nslices = n;
+    mb.empty_roots = c->d_empty_roots.as<uint32_t>();
+    mb.roots = roots2;
+    mb.proofs = proof;
+    mb.proofs_stride = ag::kPipeShreds * kPipeProofBytes;
+    if (ag::launch_merkle_build(mb, c->d_merkle_nodes.as<uint8_t>(), nodes_stride, c->stream) != hipSuccess)
+      return AG_RS_ERR_DEVICE;
+  }
+  uint8_t* same = pstat;
+  if (ag::launch_pipe_root_cmp(roots2, sroot, n, same, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  std::vector<uint8_t> h_same(n);
+  AG_HIP(hipMemcpyAsync(h_same.data(), same, n, hipMemcpyDeviceToHost, c->stream));
+  // 6. SlicePayload::try_from on the (decrypted) payload
+  std::vector<uint8_t> sstat(n);
+  if ((st = ag_slice_parse_batch(c, n, codewords, cw_stride, plen.data(), sstat.data(), parent_flags_out,
+                                 parent_ids_out, data_offsets_out, data_lens_out)))
+    return st;  // synchronous: h_same has landed
+  std::vector<uint8_t> ok(n);
+  for (size_t s = 0; s < n; ++s) {
+    int32_t r = AG_RS_OK;
+    if (plen[s] < 0) {
+      r = -plen[s] == AG_RS_ERR_INVALID_PADDING ? AG_RS_ERR_BAD_ENCODING : static_cast<int32_t>(-plen[s]);
+    } else if (!h_same[s]) {
+      r = AG_RS_ERR_INVALID_MERKLE_TREE;
+    } else if (sstat[s] == AG_SLICE_TOO_LARGE) {
+      r = AG_RS_ERR_TOO_MUCH_DATA;
+    } else if (sstat[s] != AG_SLICE_OK) {
+      r = AG_RS_ERR_BAD_ENCODING;
+    }
+    status[s] = r;
+    ok[s] = r == AG_RS_OK;
+    slots_out[s] = ok[s] ? h_slot[s] : 0;
+    slice_indices_out[s] = ok[s] ? h_sidx[s] : 0;
+    is_last_out[s] = ok[s] ? h_last[s] : 0;
+  }
+  // 7. fill_missing_shreds
+  uint8_t *d_ok, *fresh;
+  if ((st = pipe_buf(c, 20, n, &d_ok)) || (st = pipe_buf(c, 10, 4 * N, &fresh))) return st;
+  AG_HIP(hipMemcpyAsync(d_ok, ok.data(), n, hipMemcpyHostToDevice, c->stream));
+  ag::PipeExpandParams ep{};
+  ep.nslices = n;
+  ep.shred_bytes = static_cast<uint32_t>(S);
+  ep.num_data = k.num_data;
+  ep.skip = d_present;
+  ep.slice_ok = d_ok;
+  ep.kind = kcol;
+  ep.shred_index = cols.shred_index;
+  ep.data_len = cols.data_len;
+  ep.height = cols.height;
+  if (ag::launch_pipe_expand(ep, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  ag::ShredColumns fc = cols;
+  fc.slot = d_slot;
+  fc.slice_index = reinterpret_cast<uint64_t*>(ssidx);
+  fc.is_last = slast;
+  fc.sig = ssig;
+  fc.hdr_group = ag::kPipeShreds;
+  if (ag::launch_shred_serialize(fc, N, packets, packet_stride, reinterpret_cast<uint32_t*>(fresh), c->stream) !=
+          hipSuccess ||
+      ag::launch_pipe_merge_lens(reinterpret_cast<uint32_t*>(fresh), d_present, d_ok, n, packet_lens, c->stream) !=
+          hipSuccess)
+    return AG_RS_ERR_DEVICE;
+  AG_HIP(hipStreamSynchronize(c->stream));
   return AG_RS_OK;
 }
 

@@ -20,16 +20,16 @@ __global__ __launch_bounds__(256) void pipe_expand_kernel(const PipeExpandParams
   const uint64_t s = t / kPipeShreds;
   const uint32_t j = static_cast<uint32_t>(t % kPipeShreds);
   const bool skip = (p.skip && ((p.skip[s] >> j) & 1)) || (p.slice_ok && !p.slice_ok[s]);
-  p.kind[t] = j >= kPipeData ? 1 : 0;
+  p.kind[t] = j >= p.num_data ? 1 : 0;
   p.shred_index[t] = j;
   p.data_len[t] = skip ? 0xFFFFFFFFu : p.shred_bytes;
   p.height[t] = kPipeHeight;
 }
 
-// shred t fits slot j of its slice: parsed, index j, Data for j < 32, S bytes, 6 digests
+// shred t fits slot j of its slice: parsed, index j, Data for j < num_data, S bytes, 6 digests
 __device__ __forceinline__ bool plausible(const ShredColumns& c, const uint8_t* wire_status, uint64_t t, uint32_t j,
-                                          uint32_t S) {
-  return wire_status[t] == kWireOk && c.shred_index[t] == j && c.kind[t] == (j >= kPipeData ? 1 : 0) &&
+                                          uint32_t S, uint32_t num_data) {
+  return wire_status[t] == kWireOk && c.shred_index[t] == j && c.kind[t] == (j >= num_data ? 1 : 0) &&
          c.data_len[t] == S && c.height[t] == kPipeHeight;
 }
 
@@ -38,7 +38,7 @@ __global__ __launch_bounds__(64) void pipe_pick_kernel(const PipePickParams p) {
   const uint64_t s = blockIdx.x;
   const uint32_t j = threadIdx.x;
   const uint64_t t = s * kPipeShreds + j;
-  const bool fits = plausible(p.cols, p.wire_status, t, j, p.shred_bytes);
+  const bool fits = plausible(p.cols, p.wire_status, t, j, p.shred_bytes, p.num_data);
   p.plausible[t] = fits ? 1 : 0;
   const uint64_t ok = __builtin_amdgcn_ballot_w64(fits);
   const uint32_t pick = ok ? static_cast<uint32_t>(__builtin_ctzll(ok)) : kPipeNone;
@@ -71,7 +71,7 @@ __global__ __launch_bounds__(64) void pipe_check_kernel(const PipeCheckParams p)
   const uint64_t s = blockIdx.x;
   const uint32_t j = threadIdx.x;
   const uint64_t t = s * kPipeShreds + j;
-  const bool valid = plausible(p.cols, p.wire_status, t, j, p.shred_bytes) && p.val_status[t] == 0;
+  const bool valid = plausible(p.cols, p.wire_status, t, j, p.shred_bytes, p.num_data) && p.val_status[t] == 0;
   const uint64_t v = __builtin_amdgcn_ballot_w64(valid);
   if (v == 0) {
     if (j == 0) p.present[s] = 0;

@@ -21,6 +21,7 @@ constexpr uint32_t kPipeNone = 0xFFu;  // no shred picked
 struct PipeExpandParams {
   uint64_t nslices;
   uint32_t shred_bytes;
+  uint32_t num_data;      // data output shreds (kind Data below it): 32 Regular / AONT, 31 PETS, 0 CodingOnly
   const uint64_t* skip;   // [nslices] (nullable)
   const uint8_t* slice_ok;  // [nslices] (nullable): rows of slices with 0 are skipped too
   uint8_t* kind;          // [nslices * 64]
@@ -38,6 +39,7 @@ hipError_t launch_pipe_expand(const PipeExpandParams& p, hipStream_t stream);
 struct PipePickParams {
   uint64_t nslices;
   uint32_t shred_bytes;
+  uint32_t num_data;            // data output shreds: slot j < num_data holds a Data shred
   const uint8_t* wire_status;   // [nslices * 64]
   ShredColumns cols;            // deserialized columns (per shred)
   uint8_t* pick;                // [nslices]: picked shred index or kPipeNone
@@ -63,6 +65,7 @@ hipError_t launch_pipe_cache_flags(const uint8_t* pick, const uint8_t* pick_stat
 struct PipeCheckParams {
   uint64_t nslices;
   uint32_t shred_bytes;
+  uint32_t num_data;           // data output shreds (PipePickParams)
   const uint8_t* wire_status;  // [nslices * 64]
   const uint8_t* val_status;   // [nslices * 64]
   const uint8_t* roots;        // [nslices * 64][32]

@@ -83,6 +83,7 @@ EXPORTS = (
     "ag_slice_sign_batch", "ag_shred_deserialize_batch", "ag_shred_serialize_batch",
     "ag_slice_frame_batch", "ag_slice_parse_batch",
     "ag_shredder_shred_batch", "ag_shredder_deshred_batch",
+    "ag_shredder_shred_batch_kind", "ag_shredder_deshred_batch_kind",
 )
 
 
@@ -167,6 +168,8 @@ def load():
         "ag_slice_parse_batch": ([p, sz, p, sz, p, p, p, p, p, p], i),
         "ag_shredder_shred_batch": ([p, sz, sz, p, p, p, sz, p, p, p, p, p, p, p, p, p, p, sz, p], i),
         "ag_shredder_deshred_batch": ([p, sz, sz, p, sz, p, p, p, p, p, p, p, p, p, p, p], i),
+        "ag_shredder_shred_batch_kind": ([p, i, sz, sz, p, p, p, sz, p, p, p, p, p, p, p, p, sz, p, p, p, sz, p], i),
+        "ag_shredder_deshred_batch_kind": ([p, i, sz, sz, p, sz, p, p, p, sz, p, p, p, p, p, p, p, p], i),
     }
     sigs["ag_rs_internal_last_decode_classes"] = ([p, p], i)  # test aid, not in the header
     sigs["ag_rs_internal_last_encode_kernels"] = ([p, p], i)  # test aid, not in the header
@@ -940,6 +943,60 @@ def shredder_deshred_batch(ctx: Context, nslices: int, shred_bytes: int, packets
                                             slots.ctypes.data, sidx.ctypes.data, last.ctypes.data, flags.ctypes.data,
                                             ids.ctypes.data, offs.ctypes.data, dl.ctypes.data),
            "ag_shredder_deshred_batch")
+    parents = [(int.from_bytes(ids[b, :8].tobytes(), "little"), ids[b, 8:].tobytes()) if flags[b] else None
+               for b in range(nslices)]
+    return DeshredBatch(st, slots, sidx, last, parents, offs, dl)
+
+
+# ---- the other shredders of shredder.rs (CodingOnly, PETS, AONT), composed -----------------
+
+SHREDDER_REGULAR, SHREDDER_CODING_ONLY, SHREDDER_PETS, SHREDDER_AONT = 0, 1, 2, 3
+SHREDDER_CODING = {SHREDDER_REGULAR: 32, SHREDDER_CODING_ONLY: 64, SHREDDER_PETS: 33, SHREDDER_AONT: 32}
+SHREDDER_DATA_OUT = {SHREDDER_REGULAR: 32, SHREDDER_CODING_ONLY: 0, SHREDDER_PETS: 31, SHREDDER_AONT: 32}
+
+
+def shredder_shred_batch_kind(ctx: Context, kind: int, nslices: int, shred_bytes: int, parents, data, data_stride: int,
+                              data_lens, slots, slice_indices, is_last, seed, pk, keys, codewords,
+                              codeword_stride: int, packets, packet_stride: int, packet_lens, roots_out=None,
+                              sigs_out=None):
+    """Shredder::shred of CodingOnlyShredder / PetsShredder / AontShredder (or Regular) for a
+    batch of slices of one shred size (ag_shredder_shred_batch_kind).  keys: device, 16 bytes per
+    slice (PETS / AONT: the key encrypt_with_random_key drew; None otherwise); codewords: device,
+    (32 + m) * shred_bytes <= codeword_stride bytes per slice."""
+    import numpy as np
+
+    flags, ids = _parent_arrays(parents, nslices)
+    lens = np.ascontiguousarray(np.asarray(data_lens, dtype=np.uint32))
+    if lens.size != nslices:
+        raise ValueError("data_lens do not match the batch")
+    _check(load().ag_shredder_shred_batch_kind(ctx.handle, kind, nslices, shred_bytes, flags.ctypes.data,
+                                               ids.ctypes.data, _optr(data), data_stride, lens.ctypes.data,
+                                               _ptr(slots), _ptr(slice_indices), _ptr(is_last), _ptr(seed), _ptr(pk),
+                                               _optr(keys), _ptr(codewords), codeword_stride, _optr(roots_out),
+                                               _optr(sigs_out), _ptr(packets), packet_stride, _ptr(packet_lens)),
+           "ag_shredder_shred_batch_kind")
+
+
+def shredder_deshred_batch_kind(ctx: Context, kind: int, nslices: int, shred_bytes: int, packets, packet_stride: int,
+                                packet_lens, pk, codewords, codeword_stride: int) -> DeshredBatch:
+    """Shredder::deshred of the shredder `kind` for a batch (ag_shredder_deshred_batch_kind),
+    results as shredder_deshred_batch (data at codewords + s * codeword_stride + offset)."""
+    import numpy as np
+
+    st = np.zeros(nslices, np.int32)
+    slots = np.zeros(nslices, np.uint64)
+    sidx = np.zeros(nslices, np.uint64)
+    last = np.zeros(nslices, np.uint8)
+    flags = np.zeros(nslices, np.uint8)
+    ids = np.zeros((nslices, BLOCK_ID_BYTES), np.uint8)
+    offs = np.zeros(nslices, np.uint32)
+    dl = np.zeros(nslices, np.uint32)
+    _check(load().ag_shredder_deshred_batch_kind(ctx.handle, kind, nslices, shred_bytes, _ptr(packets), packet_stride,
+                                                 _ptr(packet_lens), _ptr(pk), _ptr(codewords), codeword_stride,
+                                                 st.ctypes.data, slots.ctypes.data, sidx.ctypes.data,
+                                                 last.ctypes.data, flags.ctypes.data, ids.ctypes.data,
+                                                 offs.ctypes.data, dl.ctypes.data),
+           "ag_shredder_deshred_batch_kind")
     parents = [(int.from_bytes(ids[b, :8].tobytes(), "little"), ids[b, 8:].tobytes()) if flags[b] else None
                for b in range(nslices)]
     return DeshredBatch(st, slots, sidx, last, parents, offs, dl)

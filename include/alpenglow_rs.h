@@ -454,6 +454,40 @@ int ag_shredder_deshred_batch(ag_rs_ctx* ctx, size_t nslices, size_t shred_bytes
                               uint8_t* is_last_out, uint8_t* parent_flags_out, uint8_t* parent_ids_out,
                               uint32_t* data_offsets_out, uint32_t* data_lens_out);
 
+/* The other shredders of shredder.rs, composed the same way (round 6):
+ *   AG_SHREDDER_CODING_ONLY  CodingOnlyShredder (:361-394): ReedSolomonCoder::new(64), the 64
+ *                            coding shreds are the output (no data shreds);
+ *   AG_SHREDDER_PETS         PetsShredder (:396-444): payload := AES-128-CTR_key(payload) || key,
+ *                            ReedSolomonCoder::new(33), the data shred holding the key dropped:
+ *                            31 data + 33 coding output shreds;
+ *   AG_SHREDDER_AONT         AontShredder (:446-500): ... || (key ^ SHA-256(ciphertext)[0..16)),
+ *                            ReedSolomonCoder::new(32): 32 data + 32 coding output shreds;
+ *   AG_SHREDDER_REGULAR      forwards to ag_shredder_shred_batch / _deshred_batch
+ *                            (codeword_stride must then be 64 * S).
+ * Output shred j is codeword row j (AONT), 32 + j (CodingOnly), or j < 31 / 32 + (j - 31)
+ * (PETS) of a codeword of 32 data + m coding shards at codewords + s * codeword_stride
+ * (codeword_stride >= (32 + m) * S, a multiple of 4).  keys (DEVICE, 16 bytes per slice; PETS /
+ * AONT only): the key cipher::encrypt_with_random_key drew (crypto/cipher.rs) -- the caller
+ * supplies it, so the output is reproducible.  MAX_DATA_SIZE is 16 bytes less for PETS / AONT
+ * (TooMuchData).  The deshred side decodes with the crate's decoder over every kept shred
+ * (EXACT), decrypts after the raw shreds are taken (decrypt_payload: BadEncoding for a
+ * buffer shorter than the key, :512-528), then check_merkle_tree, SlicePayload::try_from and
+ * fill_missing_shreds exactly as ag_shredder_deshred_batch; the parsed data is at codewords +
+ * s * codeword_stride + data_offsets_out[s].  Arguments otherwise as the Regular calls. */
+enum { AG_SHREDDER_REGULAR = 0, AG_SHREDDER_CODING_ONLY = 1, AG_SHREDDER_PETS = 2, AG_SHREDDER_AONT = 3 };
+int ag_shredder_shred_batch_kind(ag_rs_ctx* ctx, int kind, size_t nslices, size_t shred_bytes,
+                                 const uint8_t* parent_flags, const uint8_t* parent_ids, const uint8_t* data,
+                                 size_t data_stride, const uint32_t* data_lens, const uint64_t* slots,
+                                 const uint64_t* slice_indices, const uint8_t* is_last, const uint8_t* seed,
+                                 const uint8_t* pk, const uint8_t* keys, uint8_t* codewords, size_t codeword_stride,
+                                 uint8_t* roots_out, uint8_t* sigs_out, uint8_t* packets, size_t packet_stride,
+                                 uint32_t* packet_lens);
+int ag_shredder_deshred_batch_kind(ag_rs_ctx* ctx, int kind, size_t nslices, size_t shred_bytes, uint8_t* packets,
+                                   size_t packet_stride, uint32_t* packet_lens, const uint8_t* pk,
+                                   uint8_t* codewords, size_t codeword_stride, int32_t* status, uint64_t* slots_out,
+                                   uint64_t* slice_indices_out, uint8_t* is_last_out, uint8_t* parent_flags_out,
+                                   uint8_t* parent_ids_out, uint32_t* data_offsets_out, uint32_t* data_lens_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,6 +1,6 @@
-"""CPU composition of the reference's RegularShredder (TEST INFRASTRUCTURE ONLY: imported by
-tests/ as the checker of ag_shredder_shred_batch / ag_shredder_deshred_batch; never by the
-product path).
+"""CPU composition of the reference's four shredders (TEST INFRASTRUCTURE ONLY: imported by
+tests/ as the checker of ag_shredder_shred_batch(_kind) / ag_shredder_deshred_batch(_kind);
+never by the product path).
 
 Follows /root/reference/src/shredder.rs:
   RegularShredder::shred (:337-345) = ReedSolomonCoder::shred(slice.payload_bytes())
@@ -17,11 +17,16 @@ Follows /root/reference/src/shredder.rs:
     shred of a slice is checked by signature and caches its commitment -- and the shreds kept
     for the slice: the valid ones with the first valid one's commitment.  This is the
     receive model ag_shredder_deshred_batch documents (include/alpenglow_rs.h section 9).
+  CodingOnlyShredder / PetsShredder / AontShredder (:361-500, deshred_validated_shreds
+    :512-528): shred_kind / deshred_kind -- the same composition with the coder's coding count
+    (64 / 33 / 32), the output data shreds (0 / 31 / 32) and PETS / AONT encryption
+    (cipher_oracle, pinned separately).
 Datagrams are network::serialize(&Shred) (shred_wire_oracle).  Each stage is the pinned or
 restated oracle of its own row (slice_oracle, rs_oracle, merkle_oracle, ed25519_oracle,
 shred_wire_oracle); this module only composes them.
 """
 
+import cipher_oracle as ci
 import ed25519_oracle as ed
 import merkle_oracle as mk
 import rs_oracle as o
@@ -29,6 +34,12 @@ import shred_wire_oracle as wire
 import slice_oracle as so
 
 DATA_SHREDS, TOTAL_SHREDS = 32, 64
+
+# The four shredders of shredder.rs (include/alpenglow_rs.h AG_SHREDDER_*): the coder's coding
+# shreds m and the data output shreds (DATA_OUTPUT_SHREDS)
+REGULAR, CODING_ONLY, PETS, AONT = 0, 1, 2, 3
+CODING = {REGULAR: 32, CODING_ONLY: 64, PETS: 33, AONT: 32}
+DATA_OUT = {REGULAR: 32, CODING_ONLY: 0, PETS: 31, AONT: 32}
 
 
 def datagrams(raw_data, raw_coding, slot: int, slice_index: int, is_last: bool, seed: bytes):
@@ -50,6 +61,31 @@ def shred(parent, data: bytes, slot: int, slice_index: int, is_last: bool, seed:
     return pkts, raw, root, sig
 
 
+def output_raw(kind: int, raw):
+    """The output raw shreds of the coder's RawShreds: CodingOnly drops the data shreds
+    (shredder.rs:372-373, 385-386), PETS the data shred holding the key (:420-421, 432-433)."""
+    if kind == CODING_ONLY:
+        return o.RawShreds(data=[], coding=list(raw.coding))
+    if kind == PETS:
+        return o.RawShreds(data=list(raw.data[:-1]), coding=list(raw.coding))
+    return raw
+
+
+def shred_kind(kind: int, parent, data: bytes, slot: int, slice_index: int, is_last: bool, seed: bytes,
+               key: bytes = None):
+    """Shredder::shred of RegularShredder / CodingOnlyShredder / PetsShredder / AontShredder
+    (shredder.rs:336-500) for one slice; PETS / AONT take the key encrypt_with_random_key would
+    draw.  -> (datagrams, output RawShreds, root, sig); raises RSError(TooMuchData)."""
+    payload = so.payload_bytes(parent, data)
+    if kind == PETS:
+        payload = ci.pets_encrypt(payload, key)   # :414-418
+    elif kind == AONT:
+        payload = ci.aont_encrypt(payload, key)   # :463-469
+    raw = output_raw(kind, o.coder_shred(payload, CODING[kind]))
+    pkts, root, sig = datagrams(raw.data, raw.coding, slot, slice_index, is_last, seed)
+    return pkts, raw, root, sig
+
+
 # ---- the receive side ---------------------------------------------------------------------
 
 HEIGHT = 6  # Merkle path length of a 64-leaf slice tree
@@ -58,14 +94,15 @@ HEIGHT = 6  # Merkle path length of a 64-leaf slice tree
 OK, NOT_ENOUGH_SHARDS, TOO_MUCH_DATA, BAD_ENCODING, INVALID_MERKLE_TREE = 0, 9, 20, 23, 24
 
 
-def receive(rows, pk: bytes, shred_bytes: int):
+def receive(rows, pk: bytes, shred_bytes: int, num_data: int = DATA_SHREDS):
     """The shreds a receiver keeps for one slice from its 64 datagram slots (bytes or None):
-    a list of 64 entries, None or dict(kind, slot, slice_index, is_last, data, sig, root)."""
+    a list of 64 entries, None or dict(kind, slot, slice_index, is_last, data, sig, root).
+    num_data: the shredder's data output shreds (slot j < num_data holds a Data shred)."""
     parsed = [wire.deserialize(p) if p else None for p in rows]
 
     def fits(j):
         x = parsed[j]
-        return (x is not None and x[4] == j and x[0] == (wire.CODING if j >= DATA_SHREDS else wire.DATA) and
+        return (x is not None and x[4] == j and x[0] == (wire.CODING if j >= num_data else wire.DATA) and
                 len(x[5]) == shred_bytes and len(x[7]) == HEIGHT)
 
     commit, root = [None] * TOTAL_SHREDS, [None] * TOTAL_SHREDS
@@ -111,5 +148,42 @@ def deshred(kept):
     dgrams = [wire.serialize(wire.DATA if j < DATA_SHREDS else wire.CODING, any_shred["slot"],
                              any_shred["slice_index"], any_shred["is_last"], j, shards[j], any_shred["sig"],
                              tree.create_proof(j)) for j in range(TOTAL_SHREDS)]
+    return OK, dict(parent=parent, data=data, raw=raw, header=(any_shred["slot"], any_shred["slice_index"],
+                                                               any_shred["is_last"]), datagrams=dgrams)
+
+
+def deshred_kind(kept, kind: int):
+    """Shredder::deshred (shredder.rs:282-311) of the shredder `kind`: ValidatedShreds with its
+    layout, deshred_validated_shreds (the coder over every kept shred, then decrypt_payload for
+    PETS / AONT, :512-528), check_merkle_tree over the output raw shreds, SlicePayload, and the
+    64 datagrams with the missing ones filled in.  (status, result) as deshred."""
+    if kind == REGULAR:
+        return deshred(kept)
+    if all(x is None for x in kept):
+        return NOT_ENOUGH_SHARDS, None
+    nd = DATA_OUT[kind]
+    shreds = [(j < nd, x["data"]) if x is not None else None for j, x in enumerate(kept)]
+    try:
+        buf, raw = o.coder_deshred(shreds, nd, CODING[kind])
+    except o.RSError as e:
+        return {"NotEnoughShreds": NOT_ENOUGH_SHARDS, "TooMuchData": TOO_MUCH_DATA,
+                "InvalidPadding": BAD_ENCODING}[e.kind], None
+    raw = output_raw(kind, raw)
+    payload = buf
+    if kind in (PETS, AONT):
+        payload = ci.decrypt_payload(buf, kind == AONT)
+        if payload is None:
+            return BAD_ENCODING, None
+    any_shred = next(x for x in kept if x is not None)
+    tree = mk.slice_tree(raw.data, raw.coding)
+    if tree.root() != any_shred["root"]:
+        return INVALID_MERKLE_TREE, None
+    st, parent, data = so.try_from(payload)
+    if st != so.OK:
+        return (TOO_MUCH_DATA if st == so.TOO_LARGE else BAD_ENCODING), None
+    shards = raw.data + raw.coding
+    dgrams = [wire.serialize(wire.DATA if j < nd else wire.CODING, any_shred["slot"], any_shred["slice_index"],
+                             any_shred["is_last"], j, shards[j], any_shred["sig"], tree.create_proof(j))
+              for j in range(TOTAL_SHREDS)]
     return OK, dict(parent=parent, data=data, raw=raw, header=(any_shred["slot"], any_shred["slice_index"],
                                                                any_shred["is_last"]), datagrams=dgrams)

@@ -55,3 +55,59 @@ def test_exact_and_any_k_disagree_on_non_codeword():
     any32 = [kept[j] if j < 48 else None for j in range(64)]
     st, _ = so.deshred(any32)
     assert st == so.INVALID_MERKLE_TREE
+
+
+import pytest  # noqa: E402
+
+import cipher_oracle as ci  # noqa: E402
+
+
+@pytest.mark.parametrize("kind", [so.CODING_ONLY, so.PETS, so.AONT])
+def test_other_shredders_roundtrip(kind):
+    """CodingOnlyShredder / PetsShredder / AontShredder (shredder.rs:361-500): the output layout
+    (0 / 31 / 32 data shreds first), the payload transform (PETS: ciphertext || key; AONT:
+    ciphertext || key ^ SHA-256(ciphertext)), and the receive + deshred round trip from a random
+    32 of the 64 datagrams; a receiver with the Regular layout rejects the datagrams of a
+    shredder with another one."""
+    rng = random.Random(40 + kind)
+    Sk = 64
+    parent = (rng.randrange(1 << 40), bytes(rng.randrange(256) for _ in range(32))) if kind != so.AONT else None
+    extra = 16 if kind in (so.PETS, so.AONT) else 0
+    data = bytes(rng.randrange(256) for _ in range(32 * Sk - 40 - extra - sl.header_len(parent)))
+    key = bytes(rng.randrange(256) for _ in range(16))
+    pkts, raw, root, sig = so.shred_kind(kind, parent, data, 77, 5, True, SEED, key)
+    assert len(raw.data) == so.DATA_OUT[kind] and len(raw.data) + len(raw.coding) == 64
+    payload = sl.payload_bytes(parent, data)
+    if kind == so.PETS:
+        enc = ci.pets_encrypt(payload, key)
+        assert enc[-16:] == key and enc[:-16] != payload
+    elif kind == so.AONT:
+        enc = ci.aont_encrypt(payload, key)
+        assert bytes(a ^ b for a, b in zip(enc[-16:], ci.sha256(enc[:-16]))) == key
+    else:
+        enc = payload
+    full = o.coder_shred(enc, so.CODING[kind])
+    assert raw.coding == full.coding and raw.data == full.data[:so.DATA_OUT[kind]]
+    keep = set(rng.sample(range(64), 32))
+    rows = [pkts[j] if j in keep else None for j in range(64)]
+    pkb = ed.secret_to_public(SEED)
+    kept = so.receive(rows, pkb, Sk, so.DATA_OUT[kind])
+    assert [j for j in range(64) if kept[j] is not None] == sorted(keep)
+    st, res = so.deshred_kind(kept, kind)
+    assert st == so.OK and res["data"] == data and res["parent"] == parent
+    assert res["datagrams"] == pkts and res["header"] == (77, 5, True)
+    # the Regular receiver's layout check drops the shreds whose kind does not fit its slots
+    wrong = so.receive(rows, pkb, Sk)
+    mism = [j for j in keep if (j < 32) != (j < so.DATA_OUT[kind])]
+    assert all(wrong[j] is None for j in mism)
+
+
+def test_pets_aont_too_much_data_and_short_buffer():
+    """MAX_DATA_SIZE is 16 bytes less for PETS / AONT (shredder.rs:409, 457); decrypt_payload of a
+    buffer shorter than the key is BadEncoding (:517-521)."""
+    data = bytes(32767 - 9 - 16 + 1)  # framed + 16 = 32768 > MAX_DATA_PER_SLICE
+    for kind in (so.PETS, so.AONT):
+        with pytest.raises(o.RSError):
+            so.shred_kind(kind, None, data, 1, 0, False, SEED, bytes(16))
+    so.shred_kind(so.PETS, None, data[:-1], 1, 0, False, SEED, bytes(16))  # fits exactly
+    assert ci.decrypt_payload(bytes(15), True) is None and ci.decrypt_payload(bytes(15), False) is None

@@ -260,3 +260,156 @@ def test_pipeline_roundtrip_random_arrival(ctx, dev, S):
     for b, (parent, data, *_r) in enumerate(slices):
         off, ln = int(res.data_offsets[b]), int(res.data_lens[b])
         assert res.parents[b] == parent and cw2[b, off:off + ln].tobytes() == data
+
+
+# ---- the other shredders: CodingOnly, PETS, AONT (ag_shredder_*_batch_kind) ----------------
+
+KINDS = [so.CODING_ONLY, so.PETS, so.AONT]
+
+
+def _stride(kind, S):
+    return (32 + so.CODING[kind]) * S + 12  # a padded codeword stride (multiple of 4, not of S)
+
+
+def _slices_kind(rng, n, S, kind):
+    """n slices whose framed payloads (+ the 16-byte key tail for PETS / AONT) pad to S."""
+    extra = 16 if kind in (so.PETS, so.AONT) else 0
+    lo, hi = 32 * S - 64 - extra, 32 * S - 1 - extra
+    out = []
+    for i in range(n):
+        parent = (rng.randrange(1 << 40), bytes(rng.randrange(256) for _ in range(32))) if i % 2 else None
+        framed = rng.randrange(max(lo, sl.header_len(parent)), min(hi, sl.MAX_DATA_PER_SLICE - extra) + 1)
+        data = bytes(rng.randrange(256) for _ in range(framed - sl.header_len(parent)))
+        out.append((parent, data, rng.randrange(1 << 32), rng.randrange(1024), bool(i % 3 == 2),
+                    bytes(rng.randrange(256) for _ in range(16))))
+    return out
+
+
+def _gpu_shred_kind(ctx, dev, kind, slices, S):
+    n = len(slices)
+    maxd = max(len(d) for _, d, *_ in slices)
+    data = np.zeros((n, maxd), np.uint8)
+    for b, s_ in enumerate(slices):
+        data[b, :len(s_[1])] = np.frombuffer(s_[1], np.uint8)
+    stride = _stride(kind, S)
+    cw = torch.zeros((n, stride), dtype=torch.uint8, device=dev)
+    pk_buf = torch.zeros((n * 64, PKT), dtype=torch.uint8, device=dev)
+    lens = torch.zeros(n * 64, dtype=torch.int32, device=dev)
+    roots = torch.zeros((n, 32), dtype=torch.uint8, device=dev)
+    sigs = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+    pk = _dev(np.frombuffer(ed.secret_to_public(SEED), np.uint8), dev)
+    keys = _dev(np.frombuffer(b"".join(s_[5] for s_ in slices), np.uint8), dev)
+    rs.shredder_shred_batch_kind(ctx, kind, n, S, [s_[0] for s_ in slices], _dev(data, dev), maxd,
+                                 [len(s_[1]) for s_ in slices], _dev(np.array([s_[2] for s_ in slices], np.uint64), dev),
+                                 _dev(np.array([s_[3] for s_ in slices], np.uint64), dev),
+                                 _dev(np.array([s_[4] for s_ in slices], np.uint8), dev),
+                                 _dev(np.frombuffer(SEED, np.uint8), dev), pk, keys, cw, stride, pk_buf, PKT, lens,
+                                 roots_out=roots, sigs_out=sigs)
+    torch.cuda.synchronize()
+    return cw, pk_buf, lens, roots, sigs, pk
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("S", [1024, 64])
+def test_shred_batch_kind_matches_oracle(ctx, dev, kind, S):
+    """CodingOnlyShredder / PetsShredder / AontShredder::shred (shredder.rs:361-500) composed on
+    the device: datagrams (the shredder's data / coding layout), roots and signatures byte-exact
+    against the oracle composition with the same keys."""
+    rng = random.Random(S * 7 + kind)
+    slices = _slices_kind(rng, 5, S, kind)
+    cw, pk_buf, lens, roots, sigs, _ = _gpu_shred_kind(ctx, dev, kind, slices, S)
+    got = _packets(pk_buf, lens, len(slices))
+    for b, (parent, data, slot, si, last, key) in enumerate(slices):
+        want, raw, root, sig = so.shred_kind(kind, parent, data, slot, si, last, SEED, key)
+        assert roots[b].cpu().numpy().tobytes() == root, b
+        assert sigs[b].cpu().numpy().tobytes() == sig, b
+        assert got[b] == want, b
+
+
+def _deshred_kind(ctx, dev, kind, rows, pk, S):
+    n = len(rows)
+    buf = np.zeros((n * 64, PKT), np.uint8)
+    ln = np.zeros(n * 64, np.int32)
+    for b, r in enumerate(rows):
+        for j, p in enumerate(r):
+            if p is not None:
+                buf[b * 64 + j, :len(p)] = np.frombuffer(p, np.uint8)
+                ln[b * 64 + j] = len(p)
+    d_buf, d_ln = _dev(buf, dev), _dev(ln, dev)
+    stride = _stride(kind, S)
+    cw = torch.zeros((n, stride), dtype=torch.uint8, device=dev)
+    res = rs.shredder_deshred_batch_kind(ctx, kind, n, S, d_buf, PKT, d_ln, pk, cw, stride)
+    return res, _packets(d_buf, d_ln, n), cw.cpu().numpy()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("S", [1024, 64])
+def test_deshred_batch_kind_matches_oracle(ctx, dev, kind, S):
+    """Shredder::deshred of the other three shredders behind the receiver's checks: 12 slices,
+    every third from a leader that altered one shred after encoding, each received as a random
+    32..64 of its datagrams (every other one exactly 32), one with 31 shreds and one with a
+    tampered datagram; verdicts, filled datagrams and the parsed payload equal the oracle's
+    (receive with the shredder's layout + deshred_kind: the crate's decoder over every kept
+    shred, decrypt_payload, check_merkle_tree, SlicePayload)."""
+    rng = random.Random(S * 11 + kind)
+    slices = _slices_kind(rng, 12, S, kind)
+    nd = so.DATA_OUT[kind]
+    pk_bytes = ed.secret_to_public(SEED)
+    inp = []
+    for b, (parent, data, slot, si, last, key) in enumerate(slices):
+        rows, raw, _, _ = so.shred_kind(kind, parent, data, slot, si, last, SEED, key)
+        if b % 3 == 1:  # a leader that signs a non-codeword
+            t = rng.randrange(64)
+            shards = list(raw.data) + list(raw.coding)
+            shards[t] = bytes(x ^ 0x5A for x in shards[t])
+            rows = so.datagrams(shards[:nd], shards[nd:], slot, si, last, SEED)[0]
+        cnt = 31 if b == 4 else 32 if b % 2 == 0 else rng.randrange(32, 65)
+        keep = set(rng.sample(range(64), cnt))
+        row = [rows[j] if j in keep else None for j in range(64)]
+        if b == 6:
+            t = sorted(keep)[3]
+            bad = bytearray(row[t])
+            bad[40] ^= 1  # no longer derives the signed root: dropped by the receiver
+            row[t] = bytes(bad)
+        inp.append(row)
+    want = []
+    for r in inp:
+        kept = so.receive(r, pk_bytes, S, nd)
+        st, res = so.deshred_kind(kept, kind)
+        slots = ([r[j] if kept[j] is not None else res["datagrams"][j] for j in range(64)] if st == so.OK
+                 else [x if x is not None else b"" for x in r])
+        want.append((st, res, slots))
+    assert want[4][0] == so.NOT_ENOUGH_SHARDS and sum(w[0] == so.OK for w in want) >= 6
+    pk = _dev(np.frombuffer(pk_bytes, np.uint8), dev)
+    res, out, cw = _deshred_kind(ctx, dev, kind, inp, pk, S)
+    assert res.status.tolist() == [w[0] for w in want]
+    stride = _stride(kind, S)
+    for b, (st, r, slots) in enumerate(want):
+        assert out[b] == slots, b
+        if st != so.OK:
+            continue
+        assert (int(res.slots[b]), int(res.slice_indices[b]), bool(res.is_last[b])) == r["header"]
+        assert res.parents[b] == r["parent"]
+        off, ln = int(res.data_offsets[b]), int(res.data_lens[b])
+        assert cw[b, off:off + ln].tobytes() == r["data"]
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_pipeline_kind_roundtrip_random_arrival(ctx, dev, kind):
+    """shred_batch_kind -> a random 32..64 of each slice's datagrams -> deshred_batch_kind
+    restores every payload and every datagram (96 slices of 1 KiB shreds)."""
+    S, n = 1024, 96
+    rng = random.Random(900 + kind)
+    slices = _slices_kind(rng, n, S, kind)
+    cw, pk_buf, lens, _, _, pk = _gpu_shred_kind(ctx, dev, kind, slices, S)
+    full = _packets(pk_buf, lens, n)
+    inp = []
+    for b in range(n):
+        keep = set(rng.sample(range(64), 32 if b % 2 else rng.randrange(32, 65)))
+        inp.append([full[b][j] if j in keep else None for j in range(64)])
+    res, out, cw2 = _deshred_kind(ctx, dev, kind, inp, pk, S)
+    assert (res.status == 0).all()
+    assert out == full
+    for b, (parent, data, *_r) in enumerate(slices):
+        off, ln = int(res.data_offsets[b]), int(res.data_lens[b])
+        assert res.parents[b] == parent and cw2[b, off:off + ln].tobytes() == data
