@@ -27,6 +27,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 GIB = float(1 << 30)
 PKT = 1344  # datagram slot (1325 bytes for a 1 KiB shred, rounded to 64)
+# name -> (AG_SHREDDER_*, coding shreds of its coder, key bytes appended to the payload)
+NAMES = {"regular": "RegularShredder", "coding_only": "CodingOnlyShredder", "pets": "PetsShredder",
+         "aont": "AontShredder"}
+KINDS = {"regular": (0, 32, 0), "coding_only": (1, 64, 0), "pets": (2, 33, 16), "aont": (3, 32, 16)}
 
 
 def main():
@@ -36,6 +40,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--arrived", type=int, default=32, help="datagrams received per slice before deshred (32..64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--kind", choices=list(KINDS), default="regular",
+                    help="the shredder (shredder.rs:336-500); the CPU baseline is timed for regular only")
     args = ap.parse_args()
     import numpy as np
     import torch
@@ -49,7 +55,9 @@ def main():
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
     n, S = args.slices, 1024
-    D = 32 * S - 1 - 9  # data bytes: framed payload = MAX_DATA_PER_SLICE
+    kind, m, extra = KINDS[args.kind]
+    D = 32 * S - 1 - 9 - extra  # data bytes: framed payload (+ key) = MAX_DATA_PER_SLICE
+    stride = (32 + m) * S
     data = torch.empty((n, 32 * S), dtype=torch.uint8, device=dev)
     rs.fill_splitmix(ctx, data, n, 32 * S, 32 * S, 0x5EED0000)
     g = torch.Generator(device="cpu").manual_seed(0xA221)
@@ -59,7 +67,8 @@ def main():
     seed = torch.arange(32, dtype=torch.uint8).to(dev)
     pk = torch.empty(32, dtype=torch.uint8, device=dev)
     rs.ed25519_public_key_batch(ctx, 1, seed, pk)
-    cw = torch.empty((n, 64 * S), dtype=torch.uint8, device=dev)
+    cw = torch.empty((n, stride), dtype=torch.uint8, device=dev)
+    keys = torch.randint(0, 256, (n * 16,), generator=g, dtype=torch.uint8).to(dev)
     pkts = torch.zeros((n * 64, PKT), dtype=torch.uint8, device=dev)
     lens = torch.zeros(n * 64, dtype=torch.int32, device=dev)
     parents, dlens = [None] * n, np.full(n, D, np.uint32)
@@ -70,11 +79,17 @@ def main():
     keep = keep.reshape(-1).to(dev)
 
     def shred():
-        rs.shredder_shred_batch(ctx, n, S, parents, data, 32 * S, dlens, slots, sidx, last, seed, pk, cw, pkts, PKT,
-                                lens)
+        if kind == 0:
+            rs.shredder_shred_batch(ctx, n, S, parents, data, 32 * S, dlens, slots, sidx, last, seed, pk, cw, pkts,
+                                    PKT, lens)
+        else:
+            rs.shredder_shred_batch_kind(ctx, kind, n, S, parents, data, 32 * S, dlens, slots, sidx, last, seed, pk,
+                                         keys, cw, stride, pkts, PKT, lens)
 
     def deshred():
-        return rs.shredder_deshred_batch(ctx, n, S, pkts, PKT, lens, pk, cw)
+        if kind == 0:
+            return rs.shredder_deshred_batch(ctx, n, S, pkts, PKT, lens, pk, cw)
+        return rs.shredder_deshred_batch_kind(ctx, kind, n, S, pkts, PKT, lens, pk, cw, stride)
 
     shred()
     torch.cuda.synchronize()
@@ -100,20 +115,22 @@ def main():
         t_de += d - c
     ok = bool((res.status == 0).all()) and bool(torch.equal(lens, full_lens)) and \
         bool(torch.equal(pkts[: 64 * 8], full_pkts)) and bool((res.data_lens == D).all())
-    ok = ok and bool(torch.equal(cw[:, 9:9 + D][:64], data[:64, :D]))
+    off = res.data_offsets[:64].tolist()
+    ok = ok and all(torch.equal(cw[b, off[b]:off[b] + D], data[b, :D]) for b in range(64))
     # spot check: two slices against the CPU composition of the reference (checker only)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import shredder_oracle as so
     hp, hl = pkts[:128].cpu().numpy(), lens[:128].cpu().numpy()
+    hk = keys[:32].cpu().numpy().tobytes()
     sl, si, ls = slots[:2].cpu().tolist(), sidx[:2].cpu().tolist(), last[:2].cpu().tolist()
     spot = True
     for b in range(2):
-        want, *_ = so.shred(None, data[b, :D].cpu().numpy().tobytes(), sl[b], si[b], bool(ls[b]),
-                            bytes(range(32)))
+        want, *_ = so.shred_kind(kind, None, data[b, :D].cpu().numpy().tobytes(), sl[b], si[b], bool(ls[b]),
+                                 bytes(range(32)), hk[16 * b:16 * b + 16])
         spot &= all(hp[b * 64 + j, :hl[b * 64 + j]].tobytes() == want[j] for j in range(64))
     steps = args.steps
     line = {
-        "metric": "slices/s composed RegularShredder shred + deshred (datagrams in, datagrams out), max slices",
+        "metric": f"slices/s composed {NAMES[args.kind]} shred + deshred (datagrams in, datagrams out), max slices",
         "value": n * steps / (t_sh + t_de),
         "unit": "slices/s",
         "n_gpus": 1,
@@ -133,7 +150,7 @@ def main():
         "deshred_slices_per_s": n * steps / t_de,
         "verify": {"roundtrip_restores_everything": ok, "datagrams_match_oracle": bool(spot)},
     }
-    if not args.no_cpu_baseline:
+    if not args.no_cpu_baseline and kind == 0:
         line["cpu_baseline"] = _cpu_baseline(args, data, slots, sidx, last, cw, pkts, D, S)
     print(json.dumps(line), flush=True)
     ctx.close()
