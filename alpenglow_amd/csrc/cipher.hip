@@ -12,10 +12,12 @@
 // The random key itself comes from the host (encrypt_with_random_key, cipher.rs:35-40).
 //
 // Kernels
-//   aes_ctr_kernel      one workgroup per 4 KiB segment of a buffer, one thread per 16-byte
-//                       block: AES-128 with T-tables in LDS (Te0 + rotations, S-box), round
-//                       keys expanded per workgroup in LDS.  LDS-lookup bound.
-//   sha256_buf_kernel   one thread per buffer (SHA-256 is sequential within a message).
+//   aes_ctr_kernel      one workgroup per 32 KiB segment of a buffer, eight 16-byte blocks per
+//                       thread: AES-128 with Te0 in LDS, one copy per bank (conflict-free
+//                       lookups; rotations for Te1..3, byte 1 as the S-box), round keys
+//                       expanded per workgroup and held in scalar registers.
+//   sha256_buf_kernel   one thread per buffer (SHA-256 is sequential within a message), the
+//                       next block's loads in flight during each block's rounds.
 //   key tail / derive   one thread per buffer.
 #include <hip/hip_runtime.h>
 
@@ -23,6 +25,7 @@
 
 #include "cipher.hpp"
 #include "sha256.hpp"
+#include "unaligned.hpp"
 
 namespace ag {
 namespace aes {
@@ -132,81 +135,132 @@ void aes128_encrypt_block(const uint8_t key[16], const uint8_t in[16], uint8_t o
 
 namespace {
 
-constexpr uint32_t kSegBytes = 4096;  // per workgroup: 256 threads x one 16-byte block
+constexpr uint32_t kAesThreads = 256, kAesPer = 8;           // 16-byte blocks per thread
+constexpr uint32_t kSegBytes = kAesThreads * kAesPer * 16;  // 32 KiB per workgroup
+constexpr uint32_t kTeCopies = 32;                          // one Te0 copy per LDS bank of ds_read_b32
+
+// Te0 entry of the byte at bit `sh` of s, from the lane's own bank copy: byte address
+// byte * 128 + (lane & 31) * 4, so the 32 lanes of a ds_read_b32 group never share a bank (a
+// random lookup into one shared table costs ~3.5 LDS cycles per group instead of 1).
+template <int SH>
+__device__ __forceinline__ uint32_t te_at(const uint32_t* te, uint32_t s, uint32_t lane4) {
+  const uint32_t a = (SH >= 7 ? (s >> (SH - 7)) : (s << (7 - SH))) & 0x7F80u;
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(te) + (a | lane4));
+}
 
 __global__ __launch_bounds__(256) void aes_ctr_kernel(const BufferBatch bb, const uint8_t* __restrict__ keys,
                                                       uint32_t lens_delta, uint32_t segs) {
-  __shared__ uint32_t te[256];
-  __shared__ uint8_t sb[256];
-  __shared__ uint32_t rk[44];
+  __shared__ uint32_t te[256 * kTeCopies];  // entry i, copy c at i * 32 + c (32 KiB)
+  __shared__ uint32_t rk_s[44];
   const uint64_t b = blockIdx.x / segs;
   const uint32_t seg = blockIdx.x - static_cast<uint32_t>(b * segs);
   if (b >= bb.n) return;
   const uint32_t lenb = bb.lens[b];
   const uint32_t len = lenb > lens_delta ? lenb - lens_delta : 0;
   if (static_cast<uint64_t>(seg) * kSegBytes >= len) return;  // whole workgroup
-  te[threadIdx.x] = aes::kDevTables.te0[threadIdx.x];
-  sb[threadIdx.x] = aes::kDevTables.sbox[threadIdx.x];
+#pragma unroll
+  for (uint32_t k = 0; k < kTeCopies; ++k) {  // lane-consecutive words: conflict-free stores
+    const uint32_t w = threadIdx.x + kAesThreads * k;
+    te[w] = aes::kDevTables.te0[w / kTeCopies];
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint8_t key[16];
     for (int i = 0; i < 16; ++i) key[i] = keys[16 * b + i];
-    aes::expand(key, rk, [&](uint32_t i) { return sb[i]; });
+    aes::expand(key, rk_s, [&](uint32_t i) { return (te[i * kTeCopies] >> 8) & 0xFFu; });  // S-box = byte 1
   }
   __syncthreads();
-  const uint64_t blk = static_cast<uint64_t>(seg) * (kSegBytes / 16) + threadIdx.x;  // counter
-  const uint64_t off = 16 * blk;
-  if (off >= len) return;
-  // Ctr64LE with a zero IV: block = LE64(counter) || 0^8 (state words big-endian)
-  uint32_t s[4] = {sha::bswap(static_cast<uint32_t>(blk)), sha::bswap(static_cast<uint32_t>(blk >> 32)), 0u, 0u};
-  aes::encrypt(s, rk, [&](uint32_t i) { return te[i]; }, [&](uint32_t i) { return sb[i]; });
-  uint8_t* p = bb.base + b * bb.stride + off;
-  const uint32_t nb = len - off >= 16 ? 16u : static_cast<uint32_t>(len - off);
-  if (nb == 16 && (reinterpret_cast<uintptr_t>(p) & 15) == 0) {
-    uint4 x = *reinterpret_cast<const uint4*>(p);
-    x.x ^= sha::bswap(s[0]);
-    x.y ^= sha::bswap(s[1]);
-    x.z ^= sha::bswap(s[2]);
-    x.w ^= sha::bswap(s[3]);
-    *reinterpret_cast<uint4*>(p) = x;
-  } else {
-    for (uint32_t i = 0; i < nb; ++i) p[i] ^= static_cast<uint8_t>(s[i >> 2] >> (24 - 8 * (i & 3)));
+  uint32_t rk[44];
+#pragma unroll
+  for (int i = 0; i < 44; ++i) rk[i] = __builtin_amdgcn_readfirstlane(rk_s[i]);
+  const uint32_t l4 = (threadIdx.x & 31) * 4;
+  uint8_t* const base = bb.base + b * bb.stride;
+  for (uint32_t k = 0; k < kAesPer; ++k) {
+    const uint64_t blk = static_cast<uint64_t>(seg) * (kSegBytes / 16) + k * kAesThreads + threadIdx.x;  // counter
+    const uint64_t off = 16 * blk;
+    if (off >= len) break;
+    // Ctr64LE with a zero IV: block = LE64(counter) || 0^8 (state words big-endian)
+    uint32_t s0 = sha::bswap(static_cast<uint32_t>(blk)) ^ rk[0], s1 = sha::bswap(static_cast<uint32_t>(blk >> 32)) ^ rk[1];
+    uint32_t s2 = rk[2], s3 = rk[3];
+#pragma unroll
+    for (int r = 1; r < 10; ++r) {
+      const uint32_t t0 = te_at<24>(te, s0, l4) ^ aes::rotr(te_at<16>(te, s1, l4), 8) ^
+                          aes::rotr(te_at<8>(te, s2, l4), 16) ^ aes::rotr(te_at<0>(te, s3, l4), 24) ^ rk[4 * r];
+      const uint32_t t1 = te_at<24>(te, s1, l4) ^ aes::rotr(te_at<16>(te, s2, l4), 8) ^
+                          aes::rotr(te_at<8>(te, s3, l4), 16) ^ aes::rotr(te_at<0>(te, s0, l4), 24) ^ rk[4 * r + 1];
+      const uint32_t t2 = te_at<24>(te, s2, l4) ^ aes::rotr(te_at<16>(te, s3, l4), 8) ^
+                          aes::rotr(te_at<8>(te, s0, l4), 16) ^ aes::rotr(te_at<0>(te, s1, l4), 24) ^ rk[4 * r + 2];
+      const uint32_t t3 = te_at<24>(te, s3, l4) ^ aes::rotr(te_at<16>(te, s0, l4), 8) ^
+                          aes::rotr(te_at<8>(te, s1, l4), 16) ^ aes::rotr(te_at<0>(te, s2, l4), 24) ^ rk[4 * r + 3];
+      s0 = t0;
+      s1 = t1;
+      s2 = t2;
+      s3 = t3;
+    }
+    // last round: SubBytes + ShiftRows; the S-box value is byte 1 of the Te0 entry
+    auto last = [&](uint32_t a, uint32_t bq, uint32_t c, uint32_t d) __attribute__((always_inline)) {
+      return ((te_at<24>(te, a, l4) & 0xFF00u) << 16) | (te_at<16>(te, bq, l4) & 0xFF0000u) |
+             (te_at<8>(te, c, l4) & 0xFF00u) | ((te_at<0>(te, d, l4) >> 8) & 0xFFu);
+    };
+    const uint32_t k0 = sha::bswap(last(s0, s1, s2, s3) ^ rk[40]), k1 = sha::bswap(last(s1, s2, s3, s0) ^ rk[41]);
+    const uint32_t k2 = sha::bswap(last(s2, s3, s0, s1) ^ rk[42]), k3 = sha::bswap(last(s3, s0, s1, s2) ^ rk[43]);
+    uint8_t* p = base + off;
+    if (len - off >= 16) {
+      uint4 x = ld16u(p);
+      x.x ^= k0;
+      x.y ^= k1;
+      x.z ^= k2;
+      x.w ^= k3;
+      st16u(p, x);
+    } else {
+      const uint32_t ks[4] = {k0, k1, k2, k3};
+      for (uint32_t i = 0; i < len - off; ++i) p[i] ^= static_cast<uint8_t>(ks[i >> 2] >> (8 * (i & 3)));
+    }
   }
 }
 
-// SHA-256 of p[0..L) (message words big-endian; any alignment).
+// SHA-256 of p[0..L) (message words big-endian; any alignment).  One message per lane (a
+// batch's messages are the parallelism): the next whole block's four 16-byte loads are issued
+// before this block's rounds, so the rounds hide the load latency.
 __device__ void sha256_bytes(const uint8_t* __restrict__ p, uint32_t L, uint32_t out[8]) {
   uint32_t st[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) st[i] = sha::kIv[i];
-  const uint32_t nblk = (L + 9 + 63) / 64;
-  const bool a4 = (reinterpret_cast<uintptr_t>(p) & 3) == 0;
-  for (uint32_t b = 0; b < nblk; ++b) {
+  const uint32_t nblk = (L + 9 + 63) / 64, nfull = L / 64;
+  uint4 nx[4];
+  auto fetch = [&](uint32_t b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) nx[q] = ld16u(p + 64 * b + 16 * q);
+  };
+  if (nfull) fetch(0);
+  for (uint32_t b = 0; b < nfull; ++b) {
+    uint32_t w[16];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      w[4 * q] = sha::bswap(nx[q].x);
+      w[4 * q + 1] = sha::bswap(nx[q].y);
+      w[4 * q + 2] = sha::bswap(nx[q].z);
+      w[4 * q + 3] = sha::bswap(nx[q].w);
+    }
+    if (b + 1 < nfull) fetch(b + 1);
+    sha::compress(st, w);
+  }
+  for (uint32_t b = nfull; b < nblk; ++b) {  // the padding blocks
     uint32_t w[16];
     const uint32_t o0 = 64 * b;
-    if (o0 + 64 <= L) {
-      if (a4) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = sha::bswap(reinterpret_cast<const uint32_t*>(p + o0)[i]);
-      } else {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) w[i] = aes::getu32(p + o0 + 4 * i);
-      }
-    } else {
-      for (int i = 0; i < 16; ++i) {
-        const uint32_t o = o0 + 4 * i;
-        uint32_t v = 0;
-        if (b == nblk - 1 && i == 15) {
-          v = L * 8;
-        } else if (!(b == nblk - 1 && i == 14)) {
-          for (uint32_t k = 0; k < 4; ++k) {
-            const uint32_t ob = o + k;
-            const uint32_t bv = ob < L ? p[ob] : (ob == L ? 0x80u : 0u);
-            v |= bv << (24 - 8 * k);
-          }
+    for (int i = 0; i < 16; ++i) {
+      const uint32_t o = o0 + 4 * i;
+      uint32_t v = 0;
+      if (b == nblk - 1 && i == 15) {
+        v = L * 8;
+      } else if (!(b == nblk - 1 && i == 14)) {
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t ob = o + k;
+          const uint32_t bv = ob < L ? p[ob] : (ob == L ? 0x80u : 0u);
+          v |= bv << (24 - 8 * k);
         }
-        w[i] = v;
       }
+      w[i] = v;
     }
     sha::compress(st, w);
   }
