@@ -137,7 +137,8 @@ __global__ __launch_bounds__(256) void merkle_leaf_kernel(const MerkleBuildParam
   }
   const uint64_t s = t / p.n_leaves, j = t - s * p.n_leaves;
   uint32_t h[8];
-  leaf_hash<A4>(p.leaves + s * p.slice_stride + j * p.leaf_stride, p.leaf_bytes, h);
+  const uint64_t jr = j + (p.skip_leaf && j >= p.skip_leaf ? 1u : 0u);
+  leaf_hash<A4>(p.leaves + s * p.slice_stride + jr * p.leaf_stride, p.leaf_bytes, h);
   store_digest(nodes + s * nodes_stride + 32 * j, h);
   if (p.n_leaves == 1) store_digest(p.roots + 32 * s, h);  // a one-leaf tree's root is the leaf
 }
@@ -207,7 +208,7 @@ __global__ __launch_bounds__(256) void merkle_verify_kernel(const MerkleVerifyPa
     if (t >= p.n || (p.active && !p.active[t])) return;
   }
   uint32_t node[8];
-  leaf_hash<A4>(p.leaves + t * p.leaf_stride, p.leaf_bytes, node);
+  leaf_hash<A4>(p.leaves + grouped_row_offset(t, p.leaf_stride, p.group_stride, p.skip_row), p.leaf_bytes, node);
   if (p.leaf_nodes)
     store_digest(p.leaf_nodes + (t / p.leaves_per_tree) * p.leaf_nodes_stride + 32 * (t % p.leaves_per_tree), node);
   uint32_t idx = p.index[t];
@@ -300,7 +301,7 @@ hipError_t launch_merkle_verify(const MerkleVerifyParams& p, hipStream_t stream)
   if (p.n == 0) return hipSuccess;
   const uint64_t groups = (p.n + 255) / 256;
   if (groups > 0x7FFFFFFFull) return hipErrorInvalidValue;
-  const bool a16 = (reinterpret_cast<uintptr_t>(p.leaves) | p.leaf_stride) % 16 == 0;
+  const bool a16 = (reinterpret_cast<uintptr_t>(p.leaves) | p.leaf_stride | p.group_stride) % 16 == 0;
   const dim3 grid(static_cast<unsigned>(groups));
   if (p.active && p.list && p.n < 0xFFFFFFFFull) {
     if (hipMemsetAsync(p.list + p.n, 0, 4, stream) != hipSuccess) return hipErrorInvalidValue;

@@ -8,6 +8,17 @@ namespace ag {
 
 // TOTAL_SHREDS (shredder.rs:47): every shredder's slice tree has 64 leaves.
 constexpr uint32_t kMerkleMaxLeaves = 64;
+
+// Row t of a per-shred table (data rows, leaves): t * stride, or -- with group_stride set --
+// grouped by slice: row j of slice g = t / 64 at g * group_stride + (j + (j >= skip)) * stride
+// (skip 0: none).  The composed shredders address their output shreds in the caller's codeword
+// buffer this way (CodingOnly: the coding rows; PETS: every row but the withheld data shard).
+__host__ __device__ inline uint64_t grouped_row_offset(uint64_t t, uint64_t stride, uint64_t group_stride,
+                                                       uint32_t skip) {
+  if (!group_stride) return t * stride;
+  const uint64_t j = t & (kMerkleMaxLeaves - 1);
+  return (t / kMerkleMaxLeaves) * group_stride + (j + (skip && j >= skip ? 1u : 0u)) * stride;
+}
 // MAX_MERKLE_TREE_HEIGHT (merkle.rs:33)
 constexpr int kMerkleMaxHeight = 32;
 
@@ -31,6 +42,7 @@ struct MerkleBuildParams {
   // leaves' digests must already be in nodes (a proof check's leaf_nodes, same bytes)
   const uint8_t* hash_leaf;
   uint32_t* list;
+  uint32_t skip_leaf;  // > 0: leaf j >= skip_leaf sits at (j + 1) * leaf_stride (a withheld row)
 };
 // nodes: the node digests (reference order, nodes_stride per slice; the caller's buffer or
 // scratch) -- the levels are built there.
@@ -58,6 +70,8 @@ struct MerkleVerifyParams {
   uint8_t* leaf_nodes;    // nullable: leaf t's digest also to leaf_nodes + (t / leaves_per_tree) *
   uint64_t leaf_nodes_stride;  // leaf_nodes_stride + 32 (t % leaves_per_tree) (a later build's
   uint32_t leaves_per_tree;    // level 0, launch_merkle_build's nodes layout)
+  uint64_t group_stride;       // leaf t at leaves + grouped_row_offset(t, leaf_stride, group_stride,
+  uint32_t skip_row;           // skip_row) (group_stride 0: t * leaf_stride)
 };
 hipError_t launch_merkle_verify(const MerkleVerifyParams& p, hipStream_t stream);
 

@@ -2408,7 +2408,8 @@ __attribute__((target("avx2"))) uint32_t nonzero_mask32_avx2(const uint8_t* f) {
     q[0] = uint64_t{MASK32(dpres + b * kDataShreds)} | (uint64_t{MASK32(cpres + b * m)} << 32); \
     int cnt = __builtin_popcountll(q[0]);                                         \
     if (wps == 2) {                                                               \
-      q[1] = MASK32(cpres + b * m + 32);                                          \
+      q[1] = m == 2 * kDataShreds ? MASK32(cpres + b * m + 32)                    \
+                                  : pack_flags(cpres + b * m + 32, m - 32);       \
       cnt += __builtin_popcountll(q[1]);                                          \
     }                                                                             \
     surplus |= cnt > static_cast<int>(kDataShreds);                               \
@@ -2533,8 +2534,9 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   // the packing.  ANY_K, or EXACT where no slice holds more than 32 shreds (k shreds fix the
   // codeword, so both decoders agree).  One pattern for the whole batch stays on the host
   // path below (a single transform launch).
-  // CodingOnlyShredder's 32:64 (LowRate) takes the same path with the W = 128 window.
-  if ((m == kDataShreds || m == 2 * kDataShreds) && S % 64 == 0 && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
+  // CodingOnlyShredder's 32:64 and PetsShredder's 32:33 (LowRate, 32 < m <= 64) take the same
+  // path with the W = 128 window (positions of coding shreds past m are simply never present).
+  if (m >= kDataShreds && m <= 2 * kDataShreds && S % 64 == 0 && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
     const size_t wps = m == kDataShreds ? 1 : 2;  // present words per slice
     // packed straight into pinned staging, so the upload is one DMA with no pageable bounce
     // (once the previous call's upload of it has completed)
@@ -2627,7 +2629,8 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
                         const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
                         const uint8_t* has_cached, uint32_t cached_group, const uint8_t* active, uint8_t* status,
                         uint8_t* roots_out, uint8_t* commitments_out, uint8_t* leaf_nodes = nullptr,
-                        size_t leaf_nodes_stride = 0, uint32_t leaves_per_tree = 0);
+                        size_t leaf_nodes_stride = 0, uint32_t leaves_per_tree = 0, size_t group_stride = 0,
+                        uint32_t skip_row = 0);
 }  // namespace
 
 int ag_ed25519_public_key_batch(ag_rs_ctx* c, size_t n, const uint8_t* seeds, uint8_t* pks) {
@@ -2711,7 +2714,7 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
                         const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
                         const uint8_t* has_cached, uint32_t cached_group, const uint8_t* active, uint8_t* status,
                         uint8_t* roots_out, uint8_t* commitments_out, uint8_t* leaf_nodes, size_t leaf_nodes_stride,
-                        uint32_t leaves_per_tree) {
+                        uint32_t leaves_per_tree, size_t group_stride, uint32_t skip_row) {
   if (!c || n >= kMaxSigBatch || data_bytes >= (size_t{1} << 28) ||
       height > static_cast<size_t>(ag::kMerkleMaxHeight) ||
       (n && (!shred_index || !slots || !slice_indices || !is_last || !sigs || !pk || !status ||
@@ -2752,6 +2755,8 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
   mp.leaf_nodes = leaf_nodes;  // the leaf digests for a later Merkle rebuild over the same rows
   mp.leaf_nodes_stride = leaf_nodes_stride;
   mp.leaves_per_tree = leaves_per_tree;
+  mp.group_stride = group_stride;
+  mp.skip_row = skip_row;
   if (ag::launch_merkle_verify(mp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   // 2. SliceCommitment + cached-commitment rule (validated_shred.rs:57-64)
   AG_HIP(hipMemsetAsync(count, 0, 4, c->stream));
@@ -3018,7 +3023,7 @@ int pipe_coder_reserve(ag_rs_ctx* c, size_t ntot, size_t m) {
   if ((st = c->ensure_tables()) || (st = c->d_pipe_few.ensure(ntot, c->stream)) ||
       (st = c->d_pipe_mask.ensure(8 * ntot, c->stream)) || (st = c->d_strip.ensure(8 * ntot, c->stream)))
     return st;
-  if (m == 2 * kDataShreds)
+  if (m > kDataShreds)
     return (st = c->d_x128.ensure(10 * ntot * 8, c->stream)) ? st : c->d_rows128.ensure(ntot * 128 * 4, c->stream);
   if ((st = c->d_xmask.ensure(3 * ntot * 8, c->stream)) || (st = c->d_rows.ensure(ntot * 64 * 4, c->stream))) return st;
   c->xmask_host.clear();  // d_xmask / d_rows no longer hold decode_device's cached patterns
@@ -3038,14 +3043,15 @@ int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_
     return st;
   return pipe_coder_finish(c, n, plen);
 }
-// The same for CodingOnlyShredder's coder (LowRate 32:64, shredder.rs:362-395): every slice
+// The same for CodingOnlyShredder's coder (LowRate 32:64, shredder.rs:362-395) and
+// PetsShredder's (32:33, :403-444; its recovery shards are the first 33 of 32:64's): every slice
 // decodes in the W = 128 window as the two per-lane decode_x16 passes (the class-8 patterns of
 // decode_device, built on the device by launch_pipe_patterns128), then the strip, and the
 // LowRate re-encode of both 32-shard recovery chunks under the per-slice store masks.
 // present: two words per slice (launch_pipe_patterns128).
 int pipe_coder_enqueue_lowrate(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
-                               const uint64_t* d_present) {
-  constexpr size_t k = kDataShreds, m = 2 * kDataShreds;
+                               const uint64_t* d_present, size_t m) {
+  constexpr size_t k = kDataShreds;
   const size_t cps = S / 64;
   uint64_t* xm = c->d_x128.as<uint64_t>() + 10 * s0;
   uint32_t* rows = c->d_rows128.as<uint32_t>() + 128 * s0;
@@ -3094,7 +3100,7 @@ int pipe_coder_enqueue_lowrate(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint
     xp.chunks_per_shard = static_cast<uint32_t>(cps);
     xp.total_columns = static_cast<uint64_t>(n) * cps;
     const bool pair = j % 2 == 0 && (j + 1) * 32 < m && j < 4;
-    xp.n_out = pair ? static_cast<uint32_t>(std::min<size_t>(64, m - 32 * j)) : 32;
+    xp.n_out = static_cast<uint32_t>(std::min<size_t>(pair ? 64 : 32, m - 32 * j));
     if ((pair ? ag::launch_xform_lowrate2(j / 2, xp, c->stream) : ag::launch_xform_lowrate(32, j, xp, c->stream)) !=
         hipSuccess)
       return AG_RS_ERR_DEVICE;
@@ -3108,7 +3114,7 @@ int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw,
   constexpr size_t k = kDataShreds;
   const size_t cps = S / 64;
   if (n == 0) return AG_RS_OK;
-  if (m == 2 * kDataShreds) return pipe_coder_enqueue_lowrate(c, s0, n, S, cw, cw_stride, d_present);
+  if (m > kDataShreds) return pipe_coder_enqueue_lowrate(c, s0, n, S, cw, cw_stride, d_present, m);
   constexpr size_t W = 64;
   uint64_t* xm = c->d_xmask.as<uint64_t>() + 3 * s0;
   uint32_t* rows = c->d_rows.as<uint32_t>() + W * s0;
@@ -3541,40 +3547,53 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
 namespace {
 // Output shred j of a slice <-> codeword row (data rows 0..31, coding rows 32..32+m-1):
 // Regular / AONT: j; CodingOnly: 32 + j (the 64 coding shreds, no data shreds: shredder.rs:
-// 367-376); PETS: j for j < 31, 32 + (j - 31) after (the data shred holding the key dropped,
-// :414-422).  A run [out0, out0 + count) of output rows is codeword rows [row0, row0 + count).
-struct OutRun {
-  uint32_t out0, row0, count;
-};
+// 367-376); PETS: j for j < 31, j + 1 after (the data shred holding the key withheld,
+// :414-422).  The pipeline addresses the output rows in the caller's codeword buffer itself
+// (grouped_row_offset: base row row0, slice stride cw_stride, row `skip` and later one shard
+// further), so no row is copied between the coder's layout and the datagrams'.
 struct ShredderKind {
   uint32_t m;         // coding shreds of the coder (ReedSolomonCoder::new(CODING_OUTPUT_SHREDS))
   uint32_t num_data;  // DATA_OUTPUT_SHREDS
   int aon;            // AG_AON_* or -1
-  OutRun runs[2];
-  int nruns;
+  uint32_t row0;      // codeword row of output shred 0
+  uint32_t skip;      // output shreds >= skip sit one row further (0: none)
 };
 bool shredder_kind(int kind, ShredderKind* k) {
   switch (kind) {
-    case AG_SHREDDER_CODING_ONLY: *k = {64, 0, -1, {{0, 32, 64}, {0, 0, 0}}, 1}; return true;
-    case AG_SHREDDER_PETS: *k = {33, 31, AG_AON_PETS, {{0, 0, 31}, {31, 32, 33}}, 2}; return true;
-    case AG_SHREDDER_AONT: *k = {32, 32, AG_AON_AONT, {{0, 0, 64}, {0, 0, 0}}, 1}; return true;
+    case AG_SHREDDER_CODING_ONLY: *k = {64, 0, -1, kDataShreds, 0}; return true;
+    case AG_SHREDDER_PETS: *k = {33, 31, AG_AON_PETS, 0, 31}; return true;
+    case AG_SHREDDER_AONT: *k = {32, 32, AG_AON_AONT, 0, 0}; return true;
     default: return false;
   }
 }
-// rows (64 * S per slice) <-> codewords (cw_stride per slice), every run of the map
-int copy_runs(ag_rs_ctx* c, const ShredderKind& k, size_t n, size_t S, uint8_t* rows, uint8_t* cw, size_t cw_stride,
-              bool to_rows) {
-  for (int i = 0; i < k.nruns; ++i) {
-    const OutRun& r = k.runs[i];
-    uint8_t* a = rows + r.out0 * S;
-    uint8_t* b = cw + r.row0 * S;
-    const hipError_t e = to_rows ? hipMemcpy2DAsync(a, ag::kPipeShreds * S, b, cw_stride, r.count * S, n,
-                                                    hipMemcpyDeviceToDevice, c->stream)
-                                 : hipMemcpy2DAsync(b, cw_stride, a, ag::kPipeShreds * S, r.count * S, n,
-                                                    hipMemcpyDeviceToDevice, c->stream);
-    if (e != hipSuccess) return AG_RS_ERR_DEVICE;
-  }
-  return AG_RS_OK;
+uint32_t kind_row(const ShredderKind& k, uint32_t j) { return k.row0 + j + (k.skip && j >= k.skip ? 1u : 0u); }
+// the Merkle tree over the 64 output rows of each slice: roots, proofs (nodes in context scratch)
+int kind_merkle(ag_rs_ctx* c, const ShredderKind& k, size_t n, size_t S, const uint8_t* codewords, size_t cw_stride,
+                uint8_t* roots, uint8_t* proofs) {
+  const size_t nodes_stride = (32 * ag_merkle_node_count(ag::kPipeShreds) + 255) / 256 * 256;
+  int st;
+  if ((st = c->d_merkle_nodes.ensure(n * nodes_stride, c->stream)) || (st = ensure_empty_roots(c))) return st;
+  ag::MerkleBuildParams mb{};
+  mb.leaves = codewords + k.row0 * S;
+  mb.leaf_stride = S;
+  mb.slice_stride = cw_stride;
+  mb.skip_leaf = k.skip;
+  mb.leaf_bytes = static_cast<uint32_t>(S);
+  mb.n_leaves = ag::kPipeShreds;
+  mb.nslices = n;
+  mb.empty_roots = c->d_empty_roots.as<uint32_t>();
+  mb.roots = roots;
+  mb.proofs = proofs;
+  mb.proofs_stride = ag::kPipeShreds * kPipeProofBytes;
+  return ag::launch_merkle_build(mb, c->d_merkle_nodes.as<uint8_t>(), nodes_stride, c->stream) == hipSuccess
+             ? AG_RS_OK
+             : AG_RS_ERR_DEVICE;
+}
+void kind_rows(const ShredderKind& k, uint8_t* codewords, size_t S, size_t cw_stride, ag::ShredColumns* cols) {
+  cols->data = codewords + k.row0 * S;
+  cols->data_stride = S;
+  cols->group_stride = cw_stride;
+  cols->skip_row = k.skip;
 }
 }  // namespace
 
@@ -3618,19 +3637,15 @@ int ag_shredder_shred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_t 
     for (uint32_t& l : lens) l += static_cast<uint32_t>(ag::kCipherKeyBytes);
   }
   if ((st = ag_rs_coder_shred_batch(c, k.m, n, S, nullptr, 0, lens.data(), codewords, cw_stride))) return st;
-  // 4. the 64 output shreds (data first) as rows; Merkle tree, signature, datagrams over them
-  uint8_t *rows, *roots = roots_out, *sigs = sigs_out, *proofs, *kcol, *sidx, *dlen, *height;
-  if ((st = pipe_buf(c, 27, N * S, &rows))) return st;
-  if ((st = copy_runs(c, k, n, S, rows, codewords, cw_stride, true))) return st;
+  // 4. the 64 output shreds (data first) in place: Merkle tree, signature, datagrams over them
+  uint8_t *roots = roots_out, *sigs = sigs_out, *proofs, *kcol, *sidx, *dlen, *height;
   if (!roots && (st = pipe_buf(c, 0, 32 * n, &roots))) return st;
   if (!sigs && (st = pipe_buf(c, 1, 64 * n, &sigs))) return st;
   if ((st = pipe_buf(c, 2, kPipeProofBytes * N, &proofs)) || (st = pipe_buf(c, 3, N, &kcol)) ||
       (st = pipe_buf(c, 4, 4 * N, &sidx)) || (st = pipe_buf(c, 5, 4 * N, &dlen)) ||
       (st = pipe_buf(c, 6, 4 * N, &height)))
     return st;
-  if ((st = ag_merkle_build_batch(c, ag::kPipeShreds, S, n, rows, S, ag::kPipeShreds * S, roots, nullptr, 0, proofs,
-                                  ag::kPipeShreds * kPipeProofBytes)))
-    return st;
+  if ((st = kind_merkle(c, k, n, S, codewords, cw_stride, roots, proofs))) return st;
   if ((st = ag_slice_sign_batch(c, n, seed, pk, slots, slice_indices, is_last, roots, sigs, nullptr))) return st;
   ag::PipeExpandParams ep{};
   ep.nslices = n;
@@ -3647,8 +3662,7 @@ int ag_shredder_shred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_t 
   cols.slice_index = const_cast<uint64_t*>(slice_indices);
   cols.is_last = const_cast<uint8_t*>(is_last);
   cols.shred_index = ep.shred_index;
-  cols.data = rows;
-  cols.data_stride = S;
+  kind_rows(k, codewords, S, cw_stride, &cols);
   cols.data_len = ep.data_len;
   cols.sig = sigs;
   cols.proof = proofs;
@@ -3681,9 +3695,9 @@ int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_
   if (c->enter()) return AG_RS_ERR_DEVICE;
   const size_t n = nslices, N = n * ag::kPipeShreds;
   int st;
-  // per-shred columns; payload rows into `rows` (row 64 s + j = output shred j of slice s)
-  uint8_t *rows, *kcol, *slot, *sidx, *last, *shidx, *dlen, *sig, *proof, *height, *wire, *vstat, *roots;
-  if ((st = pipe_buf(c, 27, N * S, &rows)) || (st = pipe_buf(c, 0, N, &kcol)) || (st = pipe_buf(c, 1, 8 * N, &slot)) ||
+  // per-shred columns; payloads parsed straight into their codeword rows
+  uint8_t *kcol, *slot, *sidx, *last, *shidx, *dlen, *sig, *proof, *height, *wire, *vstat, *roots;
+  if ((st = pipe_buf(c, 0, N, &kcol)) || (st = pipe_buf(c, 1, 8 * N, &slot)) ||
       (st = pipe_buf(c, 2, 8 * N, &sidx)) || (st = pipe_buf(c, 3, N, &last)) || (st = pipe_buf(c, 4, 4 * N, &shidx)) ||
       (st = pipe_buf(c, 5, 4 * N, &dlen)) || (st = pipe_buf(c, 6, 64 * N, &sig)) ||
       (st = pipe_buf(c, 7, kPipeProofBytes * N, &proof)) || (st = pipe_buf(c, 8, 4 * N, &height)) ||
@@ -3695,183 +3709,227 @@ int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_
   cols.slice_index = reinterpret_cast<uint64_t*>(sidx);
   cols.is_last = last;
   cols.shred_index = reinterpret_cast<uint32_t*>(shidx);
-  cols.data = rows;
-  cols.data_stride = S;
+  kind_rows(k, codewords, S, cw_stride, &cols);
   cols.data_len = reinterpret_cast<uint32_t*>(dlen);
   cols.sig = sig;
   cols.proof = proof;
   cols.proof_stride = kPipeProofBytes;
   cols.height = reinterpret_cast<uint32_t*>(height);
-  // 1. network::deserialize
-  if (ag::launch_shred_deserialize(packets, packet_stride, packet_lens, N, cols, wire, c->stream) != hipSuccess)
-    return AG_RS_ERR_DEVICE;
-  // 2. ValidatedShred::try_new with the blockstore's cached commitment (the Regular pipeline's
-  //    steps 2-3 with this shredder's data / coding layout)
-  uint8_t *pick, *gdata, *gproof, *gslot, *gsidx, *glast, *gidx, *gsig, *pstat, *commits, *hasc, *plaus;
-  if ((st = pipe_buf(c, 12, n, &pick)) || (st = pipe_buf(c, 13, n * S, &gdata)) ||
-      (st = pipe_buf(c, 14, kPipeProofBytes * n, &gproof)) || (st = pipe_buf(c, 15, 8 * n, &gslot)) ||
-      (st = pipe_buf(c, 16, 8 * n, &gsidx)) || (st = pipe_buf(c, 17, n, &glast)) || (st = pipe_buf(c, 18, 4 * n, &gidx)) ||
-      (st = pipe_buf(c, 19, 64 * n, &gsig)) || (st = pipe_buf(c, 20, n, &pstat)) ||
-      (st = pipe_buf(c, 21, ag::kSliceCommitmentLen * n, &commits)) || (st = pipe_buf(c, 22, n, &hasc)) ||
-      (st = pipe_buf(c, 24, N, &plaus)))
-    return st;
-  ag::PipePickParams pp{};
-  pp.nslices = n;
-  pp.shred_bytes = static_cast<uint32_t>(S);
-  pp.num_data = k.num_data;
-  pp.wire_status = wire;
-  pp.cols = cols;
-  pp.pick = pick;
-  pp.g_data = gdata;
-  pp.g_proof = gproof;
-  pp.g_slot = reinterpret_cast<uint64_t*>(gslot);
-  pp.g_slice_index = reinterpret_cast<uint64_t*>(gsidx);
-  pp.g_is_last = glast;
-  pp.g_shred_index = reinterpret_cast<uint32_t*>(gidx);
-  pp.g_sig = gsig;
-  pp.plausible = plaus;
-  AG_HIP(hipMemsetAsync(gdata, 0, n * S, c->stream));
-  AG_HIP(hipMemsetAsync(gidx, 0, 4 * n, c->stream));
-  if (ag::launch_pipe_pick(pp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
-  if ((st = shred_validate_impl(c, n, gdata, S, S, pp.g_shred_index, gproof, kPipeProofBytes, ag::kPipeHeight,
-                                pp.g_slot, pp.g_slice_index, glast, gsig, 64, pk, nullptr, nullptr, 1, nullptr, pstat,
-                                nullptr, commits)))
-    return st;
-  if (ag::launch_pipe_cache_flags(pick, pstat, n, hasc, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
-  if ((st = shred_validate_impl(c, N, rows, S, S, cols.shred_index, proof, kPipeProofBytes, ag::kPipeHeight,
-                                cols.slot, cols.slice_index, last, sig, 64, pk, commits, hasc, ag::kPipeShreds, plaus,
-                                vstat, roots, nullptr)))
-    return st;
-  // 3. per slice: the shreds kept, the root, header and signature
-  uint8_t* per_slice;
-  if ((st = pipe_buf(c, 23, (8 + 8 + 8 + 32 + 32 + 64 + 8) * n, &per_slice))) return st;
-  uint8_t* sroot = per_slice;
-  uint8_t* roots2 = sroot + 32 * n;
-  uint8_t* ssig = roots2 + 32 * n;
-  uint64_t* d_present = reinterpret_cast<uint64_t*>(ssig + 64 * n);
-  uint64_t* d_slot = d_present + n;
-  uint8_t* ssidx = reinterpret_cast<uint8_t*>(d_slot + n);
-  uint8_t* slast = ssidx + 8 * n;
-  ag::PipeCheckParams kp{};
-  kp.nslices = n;
-  kp.shred_bytes = static_cast<uint32_t>(S);
-  kp.num_data = k.num_data;
-  kp.wire_status = wire;
-  kp.val_status = vstat;
-  kp.roots = roots;
-  kp.cols = cols;
-  kp.present = d_present;
-  kp.root = sroot;
-  kp.slot = d_slot;
-  kp.slice_index = reinterpret_cast<uint64_t*>(ssidx);
-  kp.is_last = slast;
-  kp.sig = ssig;
-  if (ag::launch_pipe_check(kp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  // Pass 0 decodes with ANY_K on the device (per-slice window patterns, no host per-slice work);
+  // a slice with surplus kept shreds that then fails some check could decode differently under
+  // the crate's decoder over every kept shred, so the batch is redone with EXACT (pass 1).  A
+  // slice that passes every check decoded the codeword its signed root commits, which every
+  // kept shred matches: EXACT agrees there.  The packets' lengths change only
+  // in step 7 (PETS / AONT serialize the absent datagrams before decrypting, into length-0 slots
+  // that a redo parses as absent), so the redo starts from the same datagrams.
   std::vector<uint64_t> h_present(n), h_slot(n), h_sidx(n);
-  std::vector<uint8_t> h_last(n);
-  AG_HIP(hipMemcpyAsync(h_present.data(), d_present, 8 * n, hipMemcpyDeviceToHost, c->stream));
-  AG_HIP(hipMemcpyAsync(h_slot.data(), d_slot, 8 * n, hipMemcpyDeviceToHost, c->stream));
-  AG_HIP(hipMemcpyAsync(h_sidx.data(), ssidx, 8 * n, hipMemcpyDeviceToHost, c->stream));
-  AG_HIP(hipMemcpyAsync(h_last.data(), slast, n, hipMemcpyDeviceToHost, c->stream));
-  AG_HIP(hipStreamSynchronize(c->stream));
-  // 4. deshred_validated_shreds: ReedSolomonCoder::deshred with the crate's decoder over every
-  //    kept shred (EXACT; the kept output rows scattered to their codeword rows), then
-  //    decrypt_payload (PETS / AONT) after the raw shreds are taken
-  if ((st = copy_runs(c, k, n, S, rows, codewords, cw_stride, false))) return st;
-  std::vector<uint8_t> dp(n * kDataShreds, 0), cp(n * k.m, 0);
-  for (size_t s = 0; s < n; ++s)
-    for (int i = 0; i < k.nruns; ++i)
-      for (uint32_t u = 0; u < k.runs[i].count; ++u) {
-        const uint32_t j = k.runs[i].out0 + u, r = k.runs[i].row0 + u;
-        const uint8_t bit = static_cast<uint8_t>((h_present[s] >> j) & 1);
-        if (r < kDataShreds) dp[s * kDataShreds + r] = bit;
-        else cp[s * k.m + (r - kDataShreds)] = bit;
-      }
-  std::vector<int64_t> plen(n);
-  if ((st = ag_rs_coder_deshred_batch(c, k.m, n, S, codewords, cw_stride, dp.data(), cp.data(), AG_RS_DECODE_EXACT,
-                                      plen.data())))
-    return st;
-  // the raw shreds of the output (restored data, re-encoded coding) back to rows: 5. rebuilds
-  // the tree over them, 7. serializes the absent ones
-  if ((st = copy_runs(c, k, n, S, rows, codewords, cw_stride, true))) return st;
-  if (k.aon >= 0) {
-    std::vector<uint32_t> cl(n);
-    for (size_t s = 0; s < n; ++s) cl[s] = plen[s] >= 0 ? static_cast<uint32_t>(plen[s]) : 0;
-    std::vector<int64_t> pl(n);
-    if ((st = ag_aon_decrypt_batch(c, k.aon, n, codewords, cw_stride, cl.data(), pl.data()))) return st;
-    for (size_t s = 0; s < n; ++s)
-      if (plen[s] >= 0) plen[s] = pl[s];  // decrypt_payload's BadEncoding for a tail-less buffer
-  }
-  // 5. check_merkle_tree over the raw output shreds
-  const size_t nodes_stride = (32 * ag_merkle_node_count(ag::kPipeShreds) + 255) / 256 * 256;
-  if ((st = c->d_merkle_nodes.ensure(n * nodes_stride, c->stream)) || (st = ensure_empty_roots(c))) return st;
-  {
-    ag::MerkleBuildParams mb{};
-    mb.leaves = rows;
-    mb.leaf_stride = S;
-    mb.slice_stride = ag::kPipeShreds * S;
-    mb.leaf_bytes = static_cast<uint32_t>(S);
-    mb.n_leaves = ag::kPipeShreds;
-    mb.nslices = n;
-    mb.empty_roots = c->d_empty_roots.as<uint32_t>();
-    mb.roots = roots2;
-    mb.proofs = proof;
-    mb.proofs_stride = ag::kPipeShreds * kPipeProofBytes;
-    if (ag::launch_merkle_build(mb, c->d_merkle_nodes.as<uint8_t>(), nodes_stride, c->stream) != hipSuccess)
+  std::vector<uint8_t> h_last(n), ok(n), pre_ok(n);
+  uint64_t* d_present = nullptr;
+  uint8_t *sroot = nullptr, *ssig = nullptr, *ssidx = nullptr, *slast = nullptr, *fresh = nullptr;
+  uint64_t* d_slot = nullptr;
+  const bool fast_ok = S % 64 == 0 && n > 1 && k.m >= kDataShreds && k.m <= 2 * kDataShreds;
+  // 7. fill_missing_shreds (part 1): the absent datagrams of the slices in `okv`, lengths into
+  // `fresh` (pipe_merge_lens moves the final slices' lengths into packet_lens)
+  auto serialize_absent = [&](const std::vector<uint8_t>& okv) -> int {
+    uint8_t* d_ok;
+    int e;
+    if ((e = pipe_buf(c, 20, n, &d_ok)) || (e = pipe_buf(c, 26, 4 * N, &fresh))) return e;
+    AG_HIP(hipMemcpyAsync(d_ok, okv.data(), n, hipMemcpyHostToDevice, c->stream));
+    ag::PipeExpandParams ep{};
+    ep.nslices = n;
+    ep.shred_bytes = static_cast<uint32_t>(S);
+    ep.num_data = k.num_data;
+    ep.skip = d_present;
+    ep.slice_ok = d_ok;
+    ep.kind = kcol;
+    ep.shred_index = cols.shred_index;
+    ep.data_len = cols.data_len;
+    ep.height = cols.height;
+    if (ag::launch_pipe_expand(ep, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    ag::ShredColumns fc = cols;
+    fc.slot = d_slot;
+    fc.slice_index = reinterpret_cast<uint64_t*>(ssidx);
+    fc.is_last = slast;
+    fc.sig = ssig;
+    fc.hdr_group = ag::kPipeShreds;
+    if (ag::launch_shred_serialize(fc, N, packets, packet_stride, reinterpret_cast<uint32_t*>(fresh), c->stream) !=
+        hipSuccess)
       return AG_RS_ERR_DEVICE;
-  }
-  uint8_t* same = pstat;
-  if (ag::launch_pipe_root_cmp(roots2, sroot, n, same, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
-  std::vector<uint8_t> h_same(n);
-  AG_HIP(hipMemcpyAsync(h_same.data(), same, n, hipMemcpyDeviceToHost, c->stream));
-  // 6. SlicePayload::try_from on the (decrypted) payload
-  std::vector<uint8_t> sstat(n);
-  if ((st = ag_slice_parse_batch(c, n, codewords, cw_stride, plen.data(), sstat.data(), parent_flags_out,
-                                 parent_ids_out, data_offsets_out, data_lens_out)))
-    return st;  // synchronous: h_same has landed
-  std::vector<uint8_t> ok(n);
-  for (size_t s = 0; s < n; ++s) {
-    int32_t r = AG_RS_OK;
-    if (plen[s] < 0) {
-      r = -plen[s] == AG_RS_ERR_INVALID_PADDING ? AG_RS_ERR_BAD_ENCODING : static_cast<int32_t>(-plen[s]);
-    } else if (!h_same[s]) {
-      r = AG_RS_ERR_INVALID_MERKLE_TREE;
-    } else if (sstat[s] == AG_SLICE_TOO_LARGE) {
-      r = AG_RS_ERR_TOO_MUCH_DATA;
-    } else if (sstat[s] != AG_SLICE_OK) {
-      r = AG_RS_ERR_BAD_ENCODING;
+    // (okv is host memory the upload reads: the caller synchronizes before it changes)
+    AG_HIP(hipStreamSynchronize(c->stream));
+    return AG_RS_OK;
+  };
+  for (int pass = fast_ok ? 0 : 1; pass < 2; ++pass) {
+    // 1. network::deserialize
+    if (ag::launch_shred_deserialize(packets, packet_stride, packet_lens, N, cols, wire, c->stream) != hipSuccess)
+      return AG_RS_ERR_DEVICE;
+    // 2. ValidatedShred::try_new with the blockstore's cached commitment (the Regular pipeline's
+    //    steps 2-3 with this shredder's data / coding layout)
+    uint8_t *pick, *gdata, *gproof, *gslot, *gsidx, *glast, *gidx, *gsig, *pstat, *commits, *hasc, *plaus;
+    if ((st = pipe_buf(c, 12, n, &pick)) || (st = pipe_buf(c, 13, n * S, &gdata)) ||
+        (st = pipe_buf(c, 14, kPipeProofBytes * n, &gproof)) || (st = pipe_buf(c, 15, 8 * n, &gslot)) ||
+        (st = pipe_buf(c, 16, 8 * n, &gsidx)) || (st = pipe_buf(c, 17, n, &glast)) || (st = pipe_buf(c, 18, 4 * n, &gidx)) ||
+        (st = pipe_buf(c, 19, 64 * n, &gsig)) || (st = pipe_buf(c, 21, ag::kSliceCommitmentLen * n, &commits)) ||
+        (st = pipe_buf(c, 22, n, &hasc)) || (st = pipe_buf(c, 24, N, &plaus)) || (st = pipe_buf(c, 27, n, &pstat)))
+      return st;
+    ag::PipePickParams pp{};
+    pp.nslices = n;
+    pp.shred_bytes = static_cast<uint32_t>(S);
+    pp.num_data = k.num_data;
+    pp.wire_status = wire;
+    pp.cols = cols;
+    pp.pick = pick;
+    pp.g_data = gdata;
+    pp.g_proof = gproof;
+    pp.g_slot = reinterpret_cast<uint64_t*>(gslot);
+    pp.g_slice_index = reinterpret_cast<uint64_t*>(gsidx);
+    pp.g_is_last = glast;
+    pp.g_shred_index = reinterpret_cast<uint32_t*>(gidx);
+    pp.g_sig = gsig;
+    pp.plausible = plaus;
+    AG_HIP(hipMemsetAsync(gdata, 0, n * S, c->stream));
+    AG_HIP(hipMemsetAsync(gidx, 0, 4 * n, c->stream));
+    if (ag::launch_pipe_pick(pp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    if ((st = shred_validate_impl(c, n, gdata, S, S, pp.g_shred_index, gproof, kPipeProofBytes, ag::kPipeHeight,
+                                  pp.g_slot, pp.g_slice_index, glast, gsig, 64, pk, nullptr, nullptr, 1, nullptr, pstat,
+                                  nullptr, commits)))
+      return st;
+    if (ag::launch_pipe_cache_flags(pick, pstat, n, hasc, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    if ((st = shred_validate_impl(c, N, cols.data, S, S, cols.shred_index, proof, kPipeProofBytes, ag::kPipeHeight,
+                                  cols.slot, cols.slice_index, last, sig, 64, pk, commits, hasc, ag::kPipeShreds, plaus,
+                                  vstat, roots, nullptr, nullptr, 0, 0, cw_stride, k.skip)))
+      return st;
+    // 3. per slice: the shreds kept, the root, header and signature
+    uint8_t* per_slice;
+    if ((st = pipe_buf(c, 23, (8 + 8 + 8 + 32 + 32 + 64 + 8) * n, &per_slice))) return st;
+    sroot = per_slice;
+    uint8_t* roots2 = sroot + 32 * n;
+    ssig = roots2 + 32 * n;
+    d_present = reinterpret_cast<uint64_t*>(ssig + 64 * n);
+    d_slot = d_present + n;
+    ssidx = reinterpret_cast<uint8_t*>(d_slot + n);
+    slast = ssidx + 8 * n;
+    ag::PipeCheckParams kp{};
+    kp.nslices = n;
+    kp.shred_bytes = static_cast<uint32_t>(S);
+    kp.num_data = k.num_data;
+    kp.wire_status = wire;
+    kp.val_status = vstat;
+    kp.roots = roots;
+    kp.cols = cols;
+    kp.present = d_present;
+    kp.root = sroot;
+    kp.slot = d_slot;
+    kp.slice_index = reinterpret_cast<uint64_t*>(ssidx);
+    kp.is_last = slast;
+    kp.sig = ssig;
+    if (ag::launch_pipe_check(kp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    AG_HIP(hipMemcpyAsync(h_present.data(), d_present, 8 * n, hipMemcpyDeviceToHost, c->stream));
+    AG_HIP(hipMemcpyAsync(h_slot.data(), d_slot, 8 * n, hipMemcpyDeviceToHost, c->stream));
+    AG_HIP(hipMemcpyAsync(h_sidx.data(), ssidx, 8 * n, hipMemcpyDeviceToHost, c->stream));
+    AG_HIP(hipMemcpyAsync(h_last.data(), slast, n, hipMemcpyDeviceToHost, c->stream));
+    AG_HIP(hipStreamSynchronize(c->stream));
+    // 4. deshred_validated_shreds: ReedSolomonCoder::deshred over the kept shreds (in their
+    //    codeword rows already), then decrypt_payload (PETS / AONT) after the raw shreds are
+    //    taken.  Pass 0: ANY_K with the window patterns built on the device from the kept
+    //    shreds' codeword-row words; pass 1: the crate's decoder over every kept shred (EXACT)
+    std::vector<int64_t> plen(n);
+    bool surplus = false;
+    for (size_t s = 0; s < n; ++s) surplus |= __builtin_popcountll(h_present[s]) > static_cast<int>(kDataShreds);
+    if (pass == 0) {
+      // codeword-row present words (pipe_coder_deshred: data | coding 0..31 << 32, coding
+      // 32..63 in word 1 when m > 32); AONT's rows are the codeword rows
+      const size_t wps = k.m > kDataShreds ? 2 : 1;
+      const uint64_t* words = d_present;
+      bool full_data = false;
+      if (kind != AG_SHREDDER_AONT) {
+        uint8_t* dw;
+        if ((st = pipe_buf(c, 25, 8 * wps * n, &dw)) || (st = c->h_strip.ensure(8 * wps * n))) return st;
+        uint64_t* hw = c->h_strip.as<uint64_t>();
+        for (size_t s = 0; s < n; ++s) {
+          const uint64_t o = h_present[s];
+          if (kind == AG_SHREDDER_CODING_ONLY) {  // output j = coding j
+            hw[2 * s] = (o & 0xFFFFFFFFull) << 32;
+            hw[2 * s + 1] = o >> 32;
+          } else {  // PETS: output j < 31 = data j, output 31 + i = coding i
+            hw[2 * s] = (o & 0x7FFFFFFFull) | (((o >> 31) & 0xFFFFFFFFull) << 32);
+            hw[2 * s + 1] = o >> 63;
+          }
+        }
+        AG_HIP(hipMemcpyAsync(dw, hw, 8 * wps * n, hipMemcpyHostToDevice, c->stream));
+        words = reinterpret_cast<const uint64_t*>(dw);
+      } else {
+        for (size_t s = 0; s < n; ++s) full_data |= (h_present[s] & 0xFFFFFFFFull) == 0xFFFFFFFFull;
+      }
+      // (pipe_coder_deshred reads its results back through h_strip after the upload completed)
+      if ((st = pipe_coder_deshred(c, n, S, codewords, cw_stride, words, plen.data(), k.m, !surplus && !full_data)))
+        return st;
+    } else {
+      std::vector<uint8_t> dp(n * kDataShreds, 0), cp(n * k.m, 0);
+      for (size_t s = 0; s < n; ++s)
+        for (uint32_t j = 0; j < ag::kPipeShreds; ++j) {
+          const uint32_t r = kind_row(k, j);
+          const uint8_t bit = static_cast<uint8_t>((h_present[s] >> j) & 1);
+          if (r < kDataShreds) dp[s * kDataShreds + r] = bit;
+          else cp[s * k.m + (r - kDataShreds)] = bit;
+        }
+      if ((st = ag_rs_coder_deshred_batch(c, k.m, n, S, codewords, cw_stride, dp.data(), cp.data(), AG_RS_DECODE_EXACT,
+                                          plen.data())))
+        return st;
     }
-    status[s] = r;
-    ok[s] = r == AG_RS_OK;
-    slots_out[s] = ok[s] ? h_slot[s] : 0;
-    slice_indices_out[s] = ok[s] ? h_sidx[s] : 0;
-    is_last_out[s] = ok[s] ? h_last[s] : 0;
+    // 5. check_merkle_tree over the raw output shreds (before any decryption: they are the
+    //    codeword rows)
+    if ((st = kind_merkle(c, k, n, S, codewords, cw_stride, roots2, proof))) return st;
+    uint8_t* same = pstat;
+    if (ag::launch_pipe_root_cmp(roots2, sroot, n, same, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    std::vector<uint8_t> h_same(n);
+    AG_HIP(hipMemcpyAsync(h_same.data(), same, n, hipMemcpyDeviceToHost, c->stream));
+    AG_HIP(hipStreamSynchronize(c->stream));
+    if (k.aon >= 0) {
+      // the absent datagrams of the slices that decoded and match their root, serialized from
+      // the encrypted rows; then decrypt_payload (BadEncoding for a failed key check)
+      for (size_t s = 0; s < n; ++s) pre_ok[s] = plen[s] >= 0 && h_same[s];
+      if ((st = serialize_absent(pre_ok))) return st;
+      std::vector<uint32_t> cl(n);
+      for (size_t s = 0; s < n; ++s) cl[s] = pre_ok[s] ? static_cast<uint32_t>(plen[s]) : 0;
+      std::vector<int64_t> pl(n);
+      if ((st = ag_aon_decrypt_batch(c, k.aon, n, codewords, cw_stride, cl.data(), pl.data()))) return st;
+      for (size_t s = 0; s < n; ++s)
+        if (pre_ok[s]) plen[s] = pl[s];
+    }
+    // 6. SlicePayload::try_from on the (decrypted) payload
+    std::vector<uint8_t> sstat(n);
+    if ((st = ag_slice_parse_batch(c, n, codewords, cw_stride, plen.data(), sstat.data(), parent_flags_out,
+                                   parent_ids_out, data_offsets_out, data_lens_out)))
+      return st;
+    bool redo = false;
+    for (size_t s = 0; s < n; ++s) {
+      int32_t r = AG_RS_OK;
+      if (plen[s] < 0) {
+        r = -plen[s] == AG_RS_ERR_INVALID_PADDING ? AG_RS_ERR_BAD_ENCODING : static_cast<int32_t>(-plen[s]);
+      } else if (!h_same[s]) {
+        r = AG_RS_ERR_INVALID_MERKLE_TREE;
+      } else if (sstat[s] == AG_SLICE_TOO_LARGE) {
+        r = AG_RS_ERR_TOO_MUCH_DATA;
+      } else if (sstat[s] != AG_SLICE_OK) {
+        r = AG_RS_ERR_BAD_ENCODING;
+      }
+      status[s] = r;
+      ok[s] = r == AG_RS_OK;
+      slots_out[s] = ok[s] ? h_slot[s] : 0;
+      slice_indices_out[s] = ok[s] ? h_sidx[s] : 0;
+      is_last_out[s] = ok[s] ? h_last[s] : 0;
+      redo |= !ok[s] && __builtin_popcountll(h_present[s]) > static_cast<int>(kDataShreds);
+    }
+    if (!redo) break;
   }
-  // 7. fill_missing_shreds
-  uint8_t *d_ok, *fresh;
-  if ((st = pipe_buf(c, 20, n, &d_ok)) || (st = pipe_buf(c, 10, 4 * N, &fresh))) return st;
+  // 7. fill_missing_shreds: every absent slot of a successful slice gets its datagram
+  if (k.aon < 0 && (st = serialize_absent(ok))) return st;
+  uint8_t* d_ok;
+  if ((st = pipe_buf(c, 20, n, &d_ok))) return st;
   AG_HIP(hipMemcpyAsync(d_ok, ok.data(), n, hipMemcpyHostToDevice, c->stream));
-  ag::PipeExpandParams ep{};
-  ep.nslices = n;
-  ep.shred_bytes = static_cast<uint32_t>(S);
-  ep.num_data = k.num_data;
-  ep.skip = d_present;
-  ep.slice_ok = d_ok;
-  ep.kind = kcol;
-  ep.shred_index = cols.shred_index;
-  ep.data_len = cols.data_len;
-  ep.height = cols.height;
-  if (ag::launch_pipe_expand(ep, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
-  ag::ShredColumns fc = cols;
-  fc.slot = d_slot;
-  fc.slice_index = reinterpret_cast<uint64_t*>(ssidx);
-  fc.is_last = slast;
-  fc.sig = ssig;
-  fc.hdr_group = ag::kPipeShreds;
-  if (ag::launch_shred_serialize(fc, N, packets, packet_stride, reinterpret_cast<uint32_t*>(fresh), c->stream) !=
-          hipSuccess ||
-      ag::launch_pipe_merge_lens(reinterpret_cast<uint32_t*>(fresh), d_present, d_ok, n, packet_lens, c->stream) !=
-          hipSuccess)
+  if (ag::launch_pipe_merge_lens(reinterpret_cast<uint32_t*>(fresh), d_present, d_ok, n, packet_lens, c->stream) !=
+      hipSuccess)
     return AG_RS_ERR_DEVICE;
   AG_HIP(hipStreamSynchronize(c->stream));
   return AG_RS_OK;

@@ -46,7 +46,7 @@ __global__ __launch_bounds__(64) void pipe_pick_kernel(const PipePickParams p) {
   if (pick == kPipeNone) return;
   const uint64_t r = s * kPipeShreds + pick;
   // payload row (2-byte aligned: S is only even), proof, signature, header
-  const uint16_t* src = reinterpret_cast<const uint16_t*>(p.cols.data + r * p.cols.data_stride);
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(p.cols.data + data_row_offset(p.cols, r));
   uint16_t* dst = reinterpret_cast<uint16_t*>(p.g_data + s * p.shred_bytes);
   for (uint32_t i = j; i < p.shred_bytes / 2; i += kPipeShreds) dst[i] = src[i];
   const uint8_t* pp = p.cols.proof + r * p.cols.proof_stride;

@@ -82,7 +82,7 @@ __device__ __forceinline__ void copy16_any(uint8_t* __restrict__ dst, const uint
 }
 // the data rows are 4-byte aligned (every row, so word copies never leave a row)
 __device__ __forceinline__ bool word_rows(const ShredColumns& c) {
-  return ((reinterpret_cast<uintptr_t>(c.data) | c.data_stride) & 3) == 0;
+  return ((reinterpret_cast<uintptr_t>(c.data) | c.data_stride | c.group_stride) & 3) == 0;
 }
 
 __global__ __launch_bounds__(256) void shred_deserialize_kernel(const uint8_t* __restrict__ packets,
@@ -132,7 +132,7 @@ __global__ __launch_bounds__(256) void shred_deserialize_kernel(const uint8_t* _
     }
   }
   if (st != kWireOk) return;
-  uint8_t* dd = c.data + t * c.data_stride;
+  uint8_t* dd = c.data + data_row_offset(c, t);
   if (word_rows(c)) copy_to_aligned(dd, pk + kShredHeadBytes, static_cast<uint32_t>(dlen), lane);
   else for (uint32_t i = lane; i < dlen; i += 64) dd[i] = pk[kShredHeadBytes + i];
   c.sig[64 * t + lane] = pk[o_sig + lane];
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(256) void shred_serialize_kernel(const ShredColumns
     st8u(pk + o_sig + 64, make_uint2(plen, 0));
     packet_lens[t] = o_sig + 72 + 32 * plen;
   }
-  const uint8_t* dd = c.data + t * c.data_stride;
+  const uint8_t* dd = c.data + data_row_offset(c, t);
   // unaligned 16-byte stores (the datagram rows sit at any byte offset)
   copy16_any(pk + kShredHeadBytes, dd, dlen, lane);
   copy16_any(pk + o_sig, c.sig + 64 * h, 64, lane);

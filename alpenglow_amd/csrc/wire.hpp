@@ -4,6 +4,8 @@
 
 #include <cstdint>
 
+#include "merkle.hpp"  // grouped_row_offset
+
 namespace ag {
 
 // network.rs:45 / types/slice_index.rs:15 / shredder.rs:47
@@ -28,7 +30,12 @@ struct ShredColumns {
   uint32_t* height;
   uint32_t hdr_group;    // serialize only: > 1 reads slot / slice_index / is_last / sig of row
                          // t / hdr_group (one header per slice); 0 or 1: per shred
+  uint64_t group_stride;  // data row t at data + grouped_row_offset(t, data_stride, group_stride,
+  uint32_t skip_row;      // skip_row) (group_stride 0: t * data_stride)
 };
+__host__ __device__ inline uint64_t data_row_offset(const ShredColumns& c, uint64_t t) {
+  return grouped_row_offset(t, c.data_stride, c.group_stride, c.skip_row);
+}
 
 // network::deserialize::<Shred> for n packets (packet t at packets + t*packet_stride,
 // packet_lens[t] bytes) into the columns; status[t] = kWireOk / kWireMalformed (wincode

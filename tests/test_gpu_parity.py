@@ -714,12 +714,13 @@ def test_coder_shred_batch_errors(ctx, dev):
 
 @pytest.mark.parametrize("S", [1024, 96])
 @pytest.mark.parametrize("mode", [rs.DECODE_EXACT, rs.DECODE_ANY_K])
-@pytest.mark.parametrize("m", [32, 64])
+@pytest.mark.parametrize("m", [32, 33, 64])
 def test_coder_deshred_batch(ctx, dev, S, mode, m):
     """Batched deshred vs the oracle's ReedSolomonCoder::deshred: restored payload, all data
     shards, re-encoded coding shards; NotEnoughShreds / InvalidPadding slices untouched.
     m = 64 is CodingOnlyShredder's coder (LowRate 32:64; at S = 1024 the device-pattern path
-    with the W = 128 window), including slices that keep only coding shreds."""
+    with the W = 128 window), including slices that keep only coding shreds; m = 33 is
+    PetsShredder's (the same window, coding shreds past 33 never present)."""
     rng = random.Random(S + mode + m)
     n = 9
     stride = (32 + m) * S
@@ -743,8 +744,8 @@ def test_coder_deshred_batch(ctx, dev, S, mode, m):
             keep = set(range(32 + m))
         elif b == 1:
             keep = set(range(32, 64))           # all data lost (coding 0..31)
-        elif b == 2 and m == 64:
-            keep = set(rng.sample(range(32, 96), 32))  # CodingOnly random arrival: coding shreds only
+        elif b == 2 and m > 32:
+            keep = set(rng.sample(range(32, 32 + m), 32))  # coding shreds only (CodingOnly random arrival)
         elif b == 3:
             keep = set(rng.sample(range(32 + m), 31))  # not enough
         else:
