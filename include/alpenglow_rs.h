@@ -469,11 +469,16 @@ int ag_shredder_deshred_batch(ag_rs_ctx* ctx, size_t nslices, size_t shred_bytes
  * (codeword_stride >= (32 + m) * S, a multiple of 4).  keys (DEVICE, 16 bytes per slice; PETS /
  * AONT only): the key cipher::encrypt_with_random_key drew (crypto/cipher.rs) -- the caller
  * supplies it, so the output is reproducible.  MAX_DATA_SIZE is 16 bytes less for PETS / AONT
- * (TooMuchData).  The deshred side decodes with the crate's decoder over every kept shred
- * (EXACT), decrypts after the raw shreds are taken (decrypt_payload: BadEncoding for a
- * buffer shorter than the key, :512-528), then check_merkle_tree, SlicePayload::try_from and
- * fill_missing_shreds exactly as ag_shredder_deshred_batch; the parsed data is at codewords +
- * s * codeword_stride + data_offsets_out[s].  Arguments otherwise as the Regular calls. */
+ * (TooMuchData).  The deshred side gives the verdicts of the crate's decoder over every kept
+ * shred (EXACT: a batch decodes ANY_K on the device and is redone with EXACT when a slice with
+ * surplus shreds fails), decrypts after the raw shreds are taken (decrypt_payload: BadEncoding
+ * for a buffer shorter than the key or a failed key check, :512-528), then check_merkle_tree,
+ * SlicePayload::try_from and fill_missing_shreds as ag_shredder_deshred_batch; the parsed data
+ * is at codewords + s * codeword_stride + data_offsets_out[s].  The datagrams are parsed into
+ * and serialized from their codeword rows.  PETS / AONT serialize the absent datagrams before
+ * decrypting, so a slice that fails only at decryption or SlicePayload may find bytes written
+ * in its absent (length-0) slots; lengths change only for successful slices.  Arguments
+ * otherwise as the Regular calls. */
 enum { AG_SHREDDER_REGULAR = 0, AG_SHREDDER_CODING_ONLY = 1, AG_SHREDDER_PETS = 2, AG_SHREDDER_AONT = 3 };
 int ag_shredder_shred_batch_kind(ag_rs_ctx* ctx, int kind, size_t nslices, size_t shred_bytes,
                                  const uint8_t* parent_flags, const uint8_t* parent_ids, const uint8_t* data,
