@@ -197,6 +197,7 @@ struct ag_rs_ctx {
   ag::LatencyMailbox* mb_dev = nullptr;
   hipStream_t server_stream = nullptr;
   uint32_t server_seq = 0;
+  uint32_t server_p_seq = 0, server_dp_seq = 0;  // versions of the parameters last posted
   bool server_broken = false;  // a job timed out: the server path is off for this context
   bool fail_next_server_job = false;  // test aid: the next server job takes the timeout path
   uint64_t server_jobs[4] = {};        // jobs posted per LatencyJob kind (test aid)
@@ -1388,6 +1389,11 @@ int ag_rs_internal_server_jobs(ag_rs_ctx* c, uint64_t* out4) {
   return AG_RS_OK;
 }
 
+// Diagnostic (not in the header): the in-kernel duration of the last per-call server job on the
+// coder's context, doorbell seen -> its stores released, then its four phases (kind read,
+// parameters + cache invalidate, tile, release): ns[5], 0 before any job.
+int ag_rs_internal_coder_last_job_ns(ag_rs_coder* coder, uint64_t* ns);
+
 // Test aid (not in the header): the context's next per-call server job takes the timeout path
 // (retired, staging abandoned, server path off) without waiting 5 s.
 int ag_rs_internal_fail_next_server_job(ag_rs_ctx* c) {
@@ -1852,10 +1858,16 @@ int server_job(ag_rs_ctx* c, uint32_t kind, const ag::XformParams& p, uint64_t m
   }
   mb->kind = kind;
   mb->mask = mask;
+  // parameters only when their bytes changed (the server reuses its copy of the same version;
+  // a fresh server launch holds no copy and reads them)
   if (dp) {
-    std::memcpy(static_cast<void*>(&mb->dp), dp, sizeof *dp);
-  } else {
+    if (std::memcmp(static_cast<const void*>(&mb->dp), dp, sizeof *dp) != 0 || c->server_dp_seq == 0) {
+      std::memcpy(static_cast<void*>(&mb->dp), dp, sizeof *dp);
+      mb->dp_seq = ++c->server_dp_seq;
+    }
+  } else if (std::memcmp(static_cast<const void*>(&mb->p), &p, sizeof p) != 0 || c->server_p_seq == 0) {
     std::memcpy(static_cast<void*>(&mb->p), &p, sizeof p);
+    mb->p_seq = ++c->server_p_seq;
   }
   if (kind < 4) ++c->server_jobs[kind];
   const uint32_t seq = ++c->server_seq;
@@ -2212,6 +2224,14 @@ struct ag_rs_coder {
     ag_rs_ctx_destroy(owned);
   }
 };
+
+int ag_rs_internal_coder_last_job_ns(ag_rs_coder* coder, uint64_t* ns) {
+  if (!coder || !coder->ctx || !ns) return AG_RS_ERR_INVALID_ARGUMENT;
+  const ag::LatencyMailbox* mb = coder->ctx->mb;
+  ns[0] = mb ? __atomic_load_n(&mb->job_ticks, __ATOMIC_ACQUIRE) * 10 : 0;  // 100 MHz wall clock
+  for (int i = 0; i < 4; ++i) ns[1 + i] = mb ? uint64_t{__atomic_load_n(&mb->phase_ticks[i], __ATOMIC_ACQUIRE)} * 10 : 0;
+  return AG_RS_OK;
+}
 
 namespace {
 constexpr size_t kDataShreds = AG_RS_DATA_SHREDS;

@@ -2193,9 +2193,10 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
   __shared__ uint4 lds[16 * 4 * kXfLanes];
   __shared__ X8Flags flags;
   constexpr unsigned kXw = sizeof(XformParams) / 4, kDw = sizeof(DecodeXParams) / 4;
-  __shared__ __attribute__((aligned(16))) uint32_t job[kXw > kDw ? kXw : kDw];
+  __shared__ __attribute__((aligned(16))) uint32_t job[kXw];    // the transform jobs' XformParams
+  __shared__ __attribute__((aligned(16))) uint32_t jobd[kDw];   // kJobDecodePk's DecodeXParams
   __shared__ uint64_t mask;
-  __shared__ uint32_t cmd;
+  __shared__ uint32_t cmd, reload;
   __shared__ PkShared pk;                 // kJobDecodePk: the tile's lists
   __shared__ uint64_t pk_mask[4];         // slice 0: present, restored; slice 1: none
   __shared__ PkLocTables loc;             // kJobDecodePk: the locator's tables
@@ -2220,6 +2221,8 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
     loc.apow_hi[threadIdx.x] = static_cast<uint16_t>(hi);
   }
   uint32_t last = 0;
+  uint64_t t_job = 0, t_kind = 0, t_par = 0, t_tile = 0;  // thread 0: phase boundaries of the job
+  uint32_t have_p = 0, have_dp = 0;  // thread 0: versions of the parameter copies in LDS (0: none)
   if (threadIdx.x == 0) {
     last = sys_load(&mb->done);
     __hip_atomic_store(&mb->alive, 1u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2231,8 +2234,18 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
       for (;;) {
         const uint32_t d = __hip_atomic_load(&mb->doorbell, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
         if (d != last) {
+          t_job = wall_clock64();
           last = d;
+          // one round trip: the job's header words are loaded together (no load depends on another)
           kind = sys_load(&mb->kind);
+          const uint32_t* m = reinterpret_cast<const uint32_t*>(&mb->mask);
+          const uint32_t m0 = sys_load(m), m1 = sys_load(m + 1), ps = sys_load(&mb->p_seq), ds = sys_load(&mb->dp_seq);
+          mask = static_cast<uint64_t>(m0) | static_cast<uint64_t>(m1) << 32;
+          const uint32_t seq = kind == kJobDecodePk ? ds : ps;
+          uint32_t& have = kind == kJobDecodePk ? have_dp : have_p;
+          reload = seq != have ? 1u : 0u;
+          have = seq;
+          t_kind = wall_clock64();
           break;
         }
         if (wall_clock64() - t0 > idle_ticks) break;
@@ -2243,22 +2256,21 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
     __syncthreads();
     const uint32_t kind = __builtin_amdgcn_readfirstlane(cmd);
     if (kind >= kJobQuit) break;
-    if (kind == kJobDecodePk) {
-      if (threadIdx.x < kDw) job[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->dp) + threadIdx.x);
-    } else if (threadIdx.x < kXw) {
-      job[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->p) + threadIdx.x);
-    }
-    if (threadIdx.x == 64) {
-      const uint32_t* m = reinterpret_cast<const uint32_t*>(&mb->mask);
-      mask = static_cast<uint64_t>(sys_load(m)) | static_cast<uint64_t>(sys_load(m + 1)) << 32;
+    if (__builtin_amdgcn_readfirstlane(reload)) {
+      if (kind == kJobDecodePk) {
+        if (threadIdx.x < kDw) jobd[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->dp) + threadIdx.x);
+      } else if (threadIdx.x < kXw) {
+        job[threadIdx.x] = sys_load(reinterpret_cast<const uint32_t*>(&mb->p) + threadIdx.x);
+      }
     }
     if (threadIdx.x >= 128 && threadIdx.x < 144) reinterpret_cast<uint32_t*>(&flags)[threadIdx.x - 128] = 0;
     __syncthreads();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: no stale input bytes in this CU's caches
+    if (threadIdx.x == 0) t_par = wall_clock64();
     if (kind == kJobDecodePk) {
       // the tile reads its parameters from the LDS copy: a private copy would be indexed by the
       // rec / orig selects and land in scratch
-      DecodeXParams& dp = *reinterpret_cast<DecodeXParams*>(job);
+      DecodeXParams& dp = *reinterpret_cast<DecodeXParams*>(jobd);
       if (threadIdx.x == 0) {
         pk_mask[0] = mask;   // present positions
         pk_mask[1] = ~mask;  // restored: every absent data and coding position
@@ -2267,9 +2279,18 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
       }
       __syncthreads();
       decode_pk_tile<-1, true>(dp, 0, lds, &flags, pk, &loc);
+      if (threadIdx.x == 0) t_tile = wall_clock64();
       __threadfence_system();
       __syncthreads();
-      if (threadIdx.x == 0) __hip_atomic_store(&mb->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      if (threadIdx.x == 0) {
+        const uint64_t t_end = wall_clock64();
+        __hip_atomic_store(&mb->phase_ticks[0], static_cast<uint32_t>(t_kind - t_job), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->phase_ticks[1], static_cast<uint32_t>(t_par - t_kind), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->phase_ticks[2], static_cast<uint32_t>(t_tile - t_par), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->phase_ticks[3], static_cast<uint32_t>(t_end - t_tile), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->job_ticks, t_end - t_job, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(&mb->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
       continue;
     }
     XformParams p;
@@ -2283,9 +2304,18 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
       xform8_tile<0, 32>(p, 0, lds, &flags);
     else
       xform8_tile<0, 32, true>(p, 0, lds, &flags);
+    if (threadIdx.x == 0) t_tile = wall_clock64();
     __threadfence_system();  // this wave's stores reach the host before done is published
     __syncthreads();
-    if (threadIdx.x == 0) __hip_atomic_store(&mb->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 0) {
+      const uint64_t t_end = wall_clock64();
+      __hip_atomic_store(&mb->phase_ticks[0], static_cast<uint32_t>(t_kind - t_job), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->phase_ticks[1], static_cast<uint32_t>(t_par - t_kind), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->phase_ticks[2], static_cast<uint32_t>(t_tile - t_par), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->phase_ticks[3], static_cast<uint32_t>(t_end - t_tile), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->job_ticks, t_end - t_job, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&mb->done, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
   if (threadIdx.x == 0) __hip_atomic_store(&mb->alive, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }

@@ -218,8 +218,14 @@ struct LatencyMailbox {
   uint32_t alive;     // 0 no server, 1 server running, 2 launch requested (host)
   uint32_t kind;      // LatencyJob
   uint64_t mask;      // decode: store mask (bit s: shard s restored); pk: present positions
+  uint32_t p_seq;     // host: version of p / dp (bumped when the bytes change; the server keeps
+  uint32_t dp_seq;    // its last copy in LDS, so a call with unchanged parameters skips that read)
   XformParams p;      // in / out: device addresses of mapped host memory; p.out_mask ignored
   DecodeXParams dp;   // kJobDecodePk: rec / orig / strides (pmask set by the server; rows unused)
+  uint64_t job_ticks; // server: wall-clock ticks (100 MHz) of the last job, doorbell seen -> stores
+                      // released (diagnostic: the in-kernel share of a per-call latency)
+  uint32_t phase_ticks[4];  // the same job's phases: kind read, parameters read + cache
+                            // invalidate, the tile (loads, transform, stores issued), the release
 };
 // log_t: the device log table (the server caches log x for x < 64 at start)
 hipError_t launch_latency_server(LatencyMailbox* mb_dev, uint64_t idle_ticks, const uint16_t* log_t,

@@ -19,6 +19,9 @@
 
 #include "alpenglow_rs.h"
 
+// diagnostic accessor of the library (not in the header): the last server job's in-kernel ns
+extern "C" int ag_rs_internal_coder_last_job_ns(ag_rs_coder* coder, uint64_t* ns);
+
 using clk = std::chrono::steady_clock;
 
 struct Stat {
@@ -55,13 +58,22 @@ int main(int argc, char** argv) {
     return ag_rs_coder_deshred(coder, 32, ptr.data(), lens.data(), is_data.data(), pout.data(), &plen, dout.data(),
                                cout.data(), &S);
   };
+  std::vector<double> job;  // the last timed series' server-job microseconds (in-kernel)
+  std::vector<double> ph[4];  // and its phases
   auto time = [&](auto&& f) {
     for (int i = 0; i < 20; ++i) f();
     std::vector<double> t;
+    job.clear();
+    for (auto& v : ph) v.clear();
     for (int i = 0; i < calls; ++i) {
       const auto a = clk::now();
       if (f()) std::exit(2);
       t.push_back(std::chrono::duration<double, std::micro>(clk::now() - a).count());
+      uint64_t ns[5] = {};
+      if (ag_rs_internal_coder_last_job_ns(coder, ns) == 0) {
+        job.push_back(ns[0] * 1e-3);
+        for (int k = 0; k < 4; ++k) ph[k].push_back(ns[1 + k] * 1e-3);
+      }
     }
     return stat(t);
   };
@@ -70,6 +82,9 @@ int main(int argc, char** argv) {
   for (int i = 32; i < 64; ++i) coding_only.push_back(i);
   set_present(coding_only);
   const Stat s_dc = time(deshred);
+  const Stat j_dc = stat(job);
+  double p_dc[4];
+  for (int k = 0; k < 4; ++k) p_dc[k] = stat(ph[k]).med;
   if (plen != payload.size() || std::memcmp(pout.data(), payload.data(), plen)) return 3;
   std::vector<int> all(64);
   for (int i = 0; i < 64; ++i) all[i] = i;
@@ -77,6 +92,9 @@ int main(int argc, char** argv) {
   all.resize(32);
   set_present(all);
   const Stat s_dr = time(deshred);
+  const Stat j_dr = stat(job);
+  double p_dr[4];
+  for (int k = 0; k < 4; ++k) p_dr[k] = stat(ph[k]).med;
   if (plen != payload.size() || std::memcmp(pout.data(), payload.data(), plen) ||
       std::memcmp(cout.data(), coding.data(), 32 * S))
     return 4;
@@ -131,10 +149,14 @@ int main(int argc, char** argv) {
               "\"deshred_random_32_of_64\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
               "\"route_a_encoder\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
               "\"route_a_decoder_coding_only\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
-              "\"route_a_decoder_random_32_of_64\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}}\n",
+              "\"route_a_decoder_random_32_of_64\": {\"median\": %.2f, \"p90\": %.2f, \"min\": %.2f}, "
+              "\"server_job_in_kernel\": {\"phases\": [\"kind read\", \"parameters + invalidate\", \"tile\", \"release\"], "
+              "\"deshred_coding_only\": {\"median\": %.2f, \"min\": %.2f, \"phase_medians\": [%.2f, %.2f, %.2f, %.2f]}, "
+              "\"deshred_random_32_of_64\": {\"median\": %.2f, \"min\": %.2f, \"phase_medians\": [%.2f, %.2f, %.2f, %.2f]}}}\n",
               calls, s_shred.med, s_shred.p90, s_shred.min, s_dc.med, s_dc.p90, s_dc.min, s_dr.med, s_dr.p90, s_dr.min,
               s_enc.med, s_enc.p90, s_enc.min, s_dec_c.med, s_dec_c.p90, s_dec_c.min, s_dec_r.med, s_dec_r.p90,
-              s_dec_r.min);
+              s_dec_r.min, j_dc.med, j_dc.min, p_dc[0], p_dc[1], p_dc[2], p_dc[3], j_dr.med, j_dr.min, p_dr[0], p_dr[1],
+              p_dr[2], p_dr[3]);
   ag_rs_encoder_free(enc);
   ag_rs_decoder_free(dec);
   ag_rs_coder_free(coder);
