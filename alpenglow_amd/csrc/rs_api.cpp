@@ -2407,6 +2407,9 @@ int ag_rs_coder_shred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, const ui
 namespace {
 int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
                        int64_t* plen, size_t m, bool no_surplus = false);
+// shred sizes pipe_coder_deshred decodes on the device: whole 64-byte chunks (any m of the
+// device-pattern path), or for 32:32 a last chunk of T = S mod 64 >= 16 bytes
+bool pipe_tail_ok(size_t S, size_t m) { return S % 64 == 0 || (m == kDataShreds && S % 64 >= 16 && S % 2 == 0); }
 }  // namespace
 
 namespace {
@@ -2556,7 +2559,7 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   // path below (a single transform launch).
   // CodingOnlyShredder's 32:64 and PetsShredder's 32:33 (LowRate, 32 < m <= 64) take the same
   // path with the W = 128 window (positions of coding shreds past m are simply never present).
-  if (m >= kDataShreds && m <= 2 * kDataShreds && S % 64 == 0 && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
+  if (m >= kDataShreds && m <= 2 * kDataShreds && pipe_tail_ok(S, m) && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
     const size_t wps = m == kDataShreds ? 1 : 2;  // present words per slice
     // packed straight into pinned staging, so the upload is one DMA with no pageable bounce
     // (once the previous call's upload of it has completed)
@@ -3032,7 +3035,9 @@ namespace {
 // patterns come from the kept-shred masks on the device (launch_pipe_patterns), the per-lane
 // window decoder restores the data shreds, coder_strip finds each payload's padding, and the
 // 32-point encode rewrites the coding shreds of the slices that decoded and stripped (store
-// masks per slice; the others keep theirs).  plen[s] as ag_rs_coder_deshred_batch: the
+// masks per slice; the others keep theirs).  HighRate 32:32 also takes shreds with a tail of
+// T = S mod 64 >= 16 bytes (pipe_tail_ok): the tail is the last column (decode_h8's TAIL
+// variant, the TAIL encode).  plen[s] as ag_rs_coder_deshred_batch: the
 // payload length, or -NotEnoughShreds / -InvalidPadding.
 //
 // pipe_coder_enqueue runs slices s0 .. s0 + n of a batch whose scratch pipe_coder_reserve
@@ -3132,7 +3137,9 @@ int pipe_coder_enqueue_lowrate(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint
 int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw, size_t cw_stride,
                        const uint64_t* d_present, size_t m, bool no_surplus) {
   constexpr size_t k = kDataShreds;
-  const size_t cps = S / 64;
+  // whole 64-byte chunks, then (S mod 64 = T >= 16) the shard's T-byte tail as one more column
+  const size_t cps = (S + 63) / 64;
+  const uint32_t tail = static_cast<uint32_t>(S % 64);
   if (n == 0) return AG_RS_OK;
   if (m > kDataShreds) return pipe_coder_enqueue_lowrate(c, s0, n, S, cw, cw_stride, d_present, m);
   constexpr size_t W = 64;
@@ -3168,6 +3175,7 @@ int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw,
   p.rows_w = static_cast<uint32_t>(W);
   p.any_k = 1;  // launch_pipe_patterns keeps exactly k survivors
   p.fuse = fuse ? 1u : 0u;
+  p.tail_bytes = tail;
   if (ag::launch_decode_x(static_cast<unsigned>(W), 0, p, (p.total_columns + 63) / 64, c->stream,
                           &c->last_window_kernels) != hipSuccess)
     return AG_RS_ERR_DEVICE;
@@ -3189,6 +3197,7 @@ int pipe_coder_enqueue(ag_rs_ctx* c, size_t s0, size_t n, size_t S, uint8_t* cw,
   xp.chunks_per_shard = static_cast<uint32_t>(cps);
   xp.total_columns = static_cast<uint64_t>(n) * cps;
   xp.skip_idle = fuse ? 1u : 0u;  // tiles of fused slices only: nothing to re-encode
+  xp.tail_bytes = tail;
   // fused, no slice with surplus shreds and none with every data shred: every store mask is
   // zero (exactly 32 kept: restored by the decode; fewer, or a failed strip: untouched)
   if (fuse && no_surplus) return AG_RS_OK;
@@ -3435,7 +3444,8 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   // 4. ReedSolomonCoder::deshred over the kept shreds (restores the data shreds, re-encodes
   //    all coding shreds, strips the padding); on the device for whole-chunk shreds
   std::vector<int64_t> plen(n);
-  if (S % 64 == 0) {
+  const bool device_coder = pipe_tail_ok(S, kDataShreds);
+  if (device_coder) {
     if ((st = pipe_coder_deshred(c, n, S, codewords, cw_stride, d_present, plen.data(), kDataShreds))) return st;
   } else {
     std::vector<uint8_t> dp(n * ag::kPipeData), cp(n * (ag::kPipeShreds - ag::kPipeData));
@@ -3468,7 +3478,7 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
         (st = ensure_empty_roots(c)))
       return st;
     // the host coder path (shreds not whole 64-byte chunks) re-encodes every coding shred
-    if (ag::launch_pipe_leaf_flags(d_present, n, S % 64 != 0, lflags, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    if (ag::launch_pipe_leaf_flags(d_present, n, !device_coder, lflags, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
     ag::MerkleBuildParams mb{};
     mb.leaves = codewords;
     mb.leaf_stride = S;
@@ -3747,7 +3757,7 @@ int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_
   uint64_t* d_present = nullptr;
   uint8_t *sroot = nullptr, *ssig = nullptr, *ssidx = nullptr, *slast = nullptr, *fresh = nullptr;
   uint64_t* d_slot = nullptr;
-  const bool fast_ok = S % 64 == 0 && n > 1 && k.m >= kDataShreds && k.m <= 2 * kDataShreds;
+  const bool fast_ok = pipe_tail_ok(S, k.m) && n > 1 && k.m >= kDataShreds && k.m <= 2 * kDataShreds;
   // 7. fill_missing_shreds (part 1): the absent datagrams of the slices in `okv`, lengths into
   // `fresh` (pipe_merge_lens moves the final slices' lengths into packet_lens)
   auto serialize_absent = [&](const std::vector<uint8_t>& okv) -> int {

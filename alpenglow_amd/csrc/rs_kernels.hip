@@ -631,10 +631,15 @@ __global__ __launch_bounds__(1024, 4) void decode_x16_kernel(const DecodeXParams
 // The derivative's regions are handed over by the swaps' epoch flags (no workgroup barriers):
 // ready = published, done = this wave's reads finished; a region is rewritten once every
 // reader of its last epoch is done.  Epochs: swaps 1-3, derivative rounds 4-5, swaps 6-8.
-template <int OUTH, int PASS, int DIN, int DOUT>
+// TAIL: shards of S = 64 C + T bytes (16 <= T < 64; p.chunks_per_shard = C + 1): the lanes of
+// column C move their block's T-byte tail chunk whole (load_tail_chunk / store_tail_chunk:
+// 16-byte accesses inside the tail only), so the follower's slices of any even shred size with
+// T >= 16 decode in place, with no restride.
+template <int OUTH, int PASS, int DIN, int DOUT, bool TAIL = false>
 __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p) {
   static_assert(PASS != 0 || (DIN == 0 && DOUT == 0), "the one-pass window starts at 0");
   static_assert(PASS != 2 || DIN == DOUT, "pass 2 loads its output half");
+  static_assert(!TAIL || PASS == 0, "tail chunks on the one-pass window");
   using LB = X8Lay<2, 1, 3, 4, 5>;
   using LC = X8Lay<2, 3, 1, 4, 5>;
   using LD = X8Lay<4, 3, 1, 2, 5>;
@@ -662,6 +667,7 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
   const uint32_t d = ok ? cc / p.chunks_per_shard : 0;
   const uint64_t blk = sb0 + d;
   const uint64_t col = ok ? cc - d * p.chunks_per_shard : 0;
+  const bool tail_lane = TAIL && ok && col + 1 == p.chunks_per_shard;
   const uint64_t in_mask = ok ? p.pmask[2 * blk] : 0;
   const uint64_t out_mask = ok ? p.pmask[2 * blk + 1] : 0;
   const uint32_t* coef = lcoef + (blk - sb0) * W;
@@ -681,14 +687,18 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
     if ((in_mask >> j) & 1) {
       const uint8_t* src = is_rec ? p.rec + (g - rpos) * p.rec_shard_stride + off_r
                                   : p.orig + (g - opos) * p.orig_shard_stride + off_o;
-      static_for<4>([&](auto Q) {
-        constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(src + 16 * q);
-        r[t][4 * q] = x.x;
-        r[t][4 * q + 1] = x.y;
-        r[t][4 * q + 2] = x.z;
-        r[t][4 * q + 3] = x.w;
-      });
+      if (tail_lane) {
+        load_tail_chunk(src, p.tail_bytes, r[t]);
+      } else {
+        static_for<4>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          const uint4 x = ld_piece(src + 16 * q);
+          r[t][4 * q] = x.x;
+          r[t][4 * q + 1] = x.y;
+          r[t][4 * q + 2] = x.z;
+          r[t][4 * q + 3] = x.w;
+        });
+      }
     } else {
       static_for<16>([&](auto P) { r[t][decltype(P)::value] = 0; });
     }
@@ -838,7 +848,15 @@ __global__ __launch_bounds__(512, 4) void decode_h8_kernel(const DecodeXParams p
         dev::xor_planes(r[t], o);
       }
       if constexpr (PASS != 1) dev::mul_rt_poly(r[t], coef[j]);
-      dev::store_chunk<true>(dst, r[t]);  // PASS 1: the unmultiplied partial
+      if (tail_lane) {
+        uint32_t raw[16];
+        static_for<16>([&](auto P) { raw[decltype(P)::value] = r[t][decltype(P)::value]; });
+        dev::transpose8(raw);
+        dev::transpose8(raw + 8);
+        store_tail_chunk(dst, p.tail_bytes, raw);
+      } else {
+        dev::store_chunk<true>(dst, r[t]);  // PASS 1: the unmultiplied partial
+      }
     }
   });
 }
@@ -2050,9 +2068,19 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
   if (t32 > 0x7FFFFFFFull) return hipErrorInvalidValue;
   const dim3 g32(static_cast<unsigned>(t32));
 #define AG_H8(O, PS, DI, DO) hipLaunchKernelGGL((decode_h8_kernel<O, PS, DI, DO>), g32, dim3(512), 0, stream, p)
+#define AG_H8T(O) hipLaunchKernelGGL((decode_h8_kernel<O, 0, 0, 0, true>), g32, dim3(512), 0, stream, p)
 #define AG_X16(PS, DI, DO) hipLaunchKernelGGL((decode_x16_kernel<PS, DI, DO>), grid, dim3(1024), 0, stream, p)
   if (W == 64 && pass == 0) {
     if (p.rows_w != 64) return hipErrorInvalidValue;
+    if (p.tail_bytes) {
+      // shards with a T-byte tail chunk (per-lane HighRate chunk 32): decode_h8's TAIL variant
+      if (!pl || p.low_rate || p.chunk != 32 || p.tail_bytes < 16 || p.tail_bytes >= 64 || p.tail_bytes % 2)
+        return hipErrorInvalidValue;
+      if (p.fuse) AG_H8T(-1);
+      else AG_H8T(1);
+      rec(p.fuse ? kDxH8Fused : kDxH8);
+      return hipGetLastError();
+    }
     const bool packed = pl && p.any_k && p.chunks_per_shard == 16 && (p.low_rate || p.chunk == 32);
     // fused coding restore: the caller's patterns restore absent coding positions too and skip
     // those slices in the re-encode, which decode_pk<-1> and the full-FFT decode_h8<-1> honour
@@ -2103,6 +2131,7 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
     return hipErrorInvalidValue;
   }
 #undef AG_H8
+#undef AG_H8T
 #undef AG_X16
   return hipGetLastError();
 }

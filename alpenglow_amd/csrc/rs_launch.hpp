@@ -181,6 +181,8 @@ struct DecodeXParams {
   uint32_t any_k;          // 1: every pattern loads at most k survivors (ANY_K; the packed kernel)
   uint32_t fuse;           // packed kernel, HighRate: the restored set may include recovery positions
                            // (every erased position of an exactly-k pattern: decode_pk<-1>)
+  uint32_t tail_bytes;     // T = S mod 64 (even, >= 16; W = 64 per-lane HighRate only): column
+                           // chunks_per_shard - 1 of every shard is its T-byte tail (decode_h8 TAIL)
 };
 // W = 32 / 64: pass 0.  W = 128: pass 1 (the other half's inputs, raw partial outputs), then
 // pass 2 (the output half's inputs, the partial added, output multiply); masks per pass.

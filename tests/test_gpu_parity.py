@@ -835,12 +835,13 @@ def test_coder_deshred_uniform_lowrate_chunks(ctx, dev, S, keep, kernels):
         assert host[b, 32 * S:].tobytes() == b"".join(raw.coding), b
 
 
-@pytest.mark.parametrize("S", [1024, 512, 64])
+@pytest.mark.parametrize("S", [1024, 512, 64, 1000, 1022, 80, 126])
 @pytest.mark.parametrize("mode", [rs.DECODE_ANY_K, rs.DECODE_EXACT])
 def test_coder_deshred_fused_coding_restore(ctx, dev, mode, S):
     """The follower's deshred at exactly k = 32 kept shreds (slot_block_data.rs:343-355): the
     window decoder restores the absent coding shreds in the same transform as the data shreds
-    (1 KiB shreds: decode_pk<-1>; other whole-chunk sizes: decode_h8<-1>; no re-encode pass),
+    (1 KiB shreds: decode_pk<-1>; other sizes: decode_h8<-1>, whose TAIL variant moves a last
+    chunk of T = S mod 64 >= 16 bytes (S = 1000, 1022, 80, 126) whole; no re-encode pass),
     bit-exact against the oracle's re-encode (o.encode of the restored data,
     reed_solomon.rs:206), mixed with slices that keep the separate re-encode (surplus shreds;
     every data shred present), NotEnoughShreds and InvalidPadding slices.  Every absent shred is
@@ -902,7 +903,7 @@ def test_coder_deshred_fused_coding_restore(ctx, dev, mode, S):
     assert rs.last_window_kernels(ctx) == {"decode_pk_fused" if S == 1024 else "decode_h8_fused"}
 
 
-@pytest.mark.parametrize("S", [1024, 256])
+@pytest.mark.parametrize("S", [1024, 256, 1000])
 def test_coder_deshred_fused_at_scale(ctx, dev, S):
     """The fused route at production scale: 4096 slices, each received as a random 32 of its 64
     shreds (absent shreds overwritten with garbage).  Every slice must come back as its

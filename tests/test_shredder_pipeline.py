@@ -220,7 +220,7 @@ def test_deshred_batch_matches_oracle(ctx, dev):
 # absent coding shreds (store mask ~present) and whose Merkle rebuild reuses the proof check's
 # leaf digests for kept rows; S = 2: a tail-only shred (S % 64 != 0: every coding shred
 # re-encoded, the LIST leaf kernel) -- ADVICE r5.
-@pytest.mark.parametrize("S", [1024, 512, 64, 2])
+@pytest.mark.parametrize("S", [1024, 512, 64, 2, 1000])
 def test_deshred_batch_adversarial_random(ctx, dev, S):
     """24 slices, about half of them from a leader that altered one random shred after
     encoding, each received as a random 32..64 of its datagrams (every fourth slice exactly
@@ -240,7 +240,7 @@ def test_deshred_batch_adversarial_random(ctx, dev, S):
     _check_against_oracle(res, out, cw, want)
 
 
-@pytest.mark.parametrize("S", [1024, 512, 64, 2])
+@pytest.mark.parametrize("S", [1024, 512, 64, 2, 1000])
 def test_pipeline_roundtrip_random_arrival(ctx, dev, S):
     """shred_batch -> a random 32..64 of each slice's datagrams (every other slice exactly 32)
     -> deshred_batch restores every payload and every datagram (256 slices of shred size S)."""
@@ -343,7 +343,7 @@ def _deshred_kind(ctx, dev, kind, rows, pk, S):
 
 
 @pytest.mark.parametrize("kind", KINDS)
-@pytest.mark.parametrize("S", [1024, 64])
+@pytest.mark.parametrize("S", [1024, 64, 1000])
 def test_deshred_batch_kind_matches_oracle(ctx, dev, kind, S):
     """Shredder::deshred of the other three shredders behind the receiver's checks: 12 slices,
     every third from a leader that altered one shred after encoding, each received as a random
