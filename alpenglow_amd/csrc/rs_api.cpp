@@ -589,6 +589,10 @@ int decode_cols(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t sstride, size
 int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblocks, uint8_t* orig, size_t ostride,
                        const uint8_t* rec, size_t rstride, const uint8_t* opres, const uint8_t* rpres, size_t npat,
                        int mode);
+int decode_cols_device_patterns(ag_rs_ctx* c, size_t S, size_t sstride, size_t nblocks, uint8_t* orig,
+                                size_t ostride, const uint8_t* rec, size_t rstride, const uint8_t* opres,
+                                const uint8_t* rpres);
+constexpr int kNotApplicable = -1;
 
 // last_classes counts every pattern of the outermost call: the whole-chunk decode and the
 // tail restride's inner decode of a shard size with S % 64 != 0 add up (reset once per call)
@@ -666,6 +670,12 @@ int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblock
         if (all_full) return decode_tail32(c, k, m, S, nblocks, orig, ostride, rec, rstride, opres, npat);
       }
       int st;
+      // per-block 32:32 patterns with lost recovery shards (ANY_K): the per-lane window decode
+      // takes the whole shards, the T-byte tail as one more column (decode_h8 TAIL), no restride
+      if (tail >= 16 && npat > 1 && npat == nblocks && k == 32 && m == 32 && hr == 1 && mode == AG_RS_DECODE_ANY_K) {
+        st = decode_cols_device_patterns(c, S, S, nblocks, orig, ostride, rec, rstride, opres, rpres);
+        if (st != kNotApplicable) return st;
+      }
       if (full && (st = decode_cols(c, k, m, full, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode)))
         return st;
       return decode_restrided(c, k, m, tail, S, full, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
@@ -674,7 +684,6 @@ int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblock
   return decode_cols(c, k, m, S, S, nblocks, orig, ostride, rec, rstride, opres, rpres, npat, mode);
 }
 
-constexpr int kNotApplicable = -1;
 
 // Per-block patterns of the 32:32 code on tiles that straddle blocks (chunks per shard not a
 // multiple of 64: the follower's slices, tail shreds' whole chunks and their restrided tails),
@@ -689,7 +698,8 @@ int decode_cols_device_patterns(ag_rs_ctx* c, size_t S, size_t sstride, size_t n
                                 size_t ostride, const uint8_t* rec, size_t rstride, const uint8_t* opres,
                                 const uint8_t* rpres) {
   constexpr size_t k = 32, m = 32, W = 64;
-  const size_t n = nblocks, cps = S / 64;
+  // S = 64 C, or 64 C + T with a tail of T >= 16 bytes as the last column (decode_h8 TAIL)
+  const size_t n = nblocks, cps = (S + 63) / 64;
   int st;
   if (c->present_ev) AG_HIP(hipEventSynchronize(c->present_ev));  // the previous upload has read h_present
   else AG_HIP(hipEventCreateWithFlags(&c->present_ev, hipEventDisableTiming));
@@ -741,6 +751,7 @@ int decode_cols_device_patterns(ag_rs_ctx* c, size_t S, size_t sstride, size_t n
   p.per_lane = 1;
   p.rows_w = static_cast<uint32_t>(W);
   p.any_k = 1;  // launch_pipe_patterns keeps exactly k survivors
+  p.tail_bytes = static_cast<uint32_t>(S % 64);
   if (ag::launch_decode_x(static_cast<unsigned>(W), 0, p, (p.total_columns + 63) / 64, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   return AG_RS_OK;

@@ -286,83 +286,68 @@ __device__ __forceinline__ void keep16(uint32_t* v, uint32_t len) {
     v[k] &= m;
   });
 }
-// bytes [a, a + 16) of the 16-byte pieces p[0..N) laid end to end, zeros outside [0, 16 N)
-// (a uniform, -64 < a < 16 N): the two pieces around a picked by uniform selects, one funnel
-template <int N>
-__device__ __forceinline__ void bytes_at(const uint32_t (&p)[N][4], int a, uint32_t* out) {
-  a = __builtin_amdgcn_readfirstlane(a);
-  const int i = (a + 64) / 16 - 4;  // floor(a / 16)
-  uint32_t lo[4] = {0u, 0u, 0u, 0u}, hi[4] = {0u, 0u, 0u, 0u};
-  static_for<N>([&](auto K) {
-    constexpr int k = decltype(K)::value;
-    if (i == k) static_for<4>([&](auto W) { lo[decltype(W)::value] = p[k][decltype(W)::value]; });
-    if (i + 1 == k) static_for<4>([&](auto W) { hi[decltype(W)::value] = p[k][decltype(W)::value]; });
-  });
-  funnel16(lo, hi, static_cast<uint32_t>(a - 16 * i), out);
-}
 // One lane's whole tail chunk (T = S mod 64 bytes, 16 <= T < 64, even, uniform; h = T / 2
 // symbols): the crate keeps the h low bytes then the h high bytes, i.e. the
 // 64-byte chunk (low bytes [0, 32), high bytes [32, 64)) with symbols h..31 zero.  Moved with
-// 16-byte accesses inside [0, T) only -- the last one at T - 16, overlapping its predecessor --
-// so no byte of the next shard is touched.  Raw chunk words in v[16] (before planes_from_raw /
-// after the inverse transpose).
+// 16-byte accesses inside [0, T) only, so no byte of the next shard is touched: a run that
+// would cross T comes from (goes to) the window [T - 16, T) through one uniform funnel.  Raw
+// chunk words in v[16] (before planes_from_raw / after the inverse transpose).
 __device__ __forceinline__ void load_tail_chunk(const uint8_t* src, uint32_t T, uint32_t* v) {
   T = __builtin_amdgcn_readfirstlane(T);
+  const uint32_t h = T / 2;
   const uint32_t z[4] = {0u, 0u, 0u, 0u};
-  uint32_t L[4][4];  // the tail's bytes [0, 64), zeros from T on
-  static_for<4>([&](auto K) {
-    constexpr uint32_t k = decltype(K)::value;
-    if (16 * k + 16 <= T) {
-      const uint4 x = ld16u(src + 16 * k);
-      L[k][0] = x.x; L[k][1] = x.y; L[k][2] = x.z; L[k][3] = x.w;
-    } else if (16 * k < T) {  // bytes [16 k, T) sit at 16 k + 16 - T of the window [T - 16, T)
-      const uint4 x = ld16u(src + T - 16);
-      const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-      funnel16(w, z, 16 * k + 16 - T, L[k]);
-    } else {
-      static_for<4>([&](auto W) { L[k][decltype(W)::value] = 0u; });
-    }
-  });
-  const int h = static_cast<int>(T / 2);
-  bytes_at<4>(L, 0, v);
-  keep16(v, static_cast<uint32_t>(h));
-  bytes_at<4>(L, 16, v + 4);
-  keep16(v + 4, static_cast<uint32_t>(h > 16 ? h - 16 : 0));
-  bytes_at<4>(L, h, v + 8);
-  keep16(v + 8, static_cast<uint32_t>(h));
-  bytes_at<4>(L, h + 16, v + 12);
-  keep16(v + 12, static_cast<uint32_t>(h > 16 ? h - 16 : 0));
+  auto ld = [&](uint32_t off, uint32_t* out) __attribute__((always_inline)) {
+    const uint4 x = ld16u(src + off);
+    out[0] = x.x; out[1] = x.y; out[2] = x.z; out[3] = x.w;
+  };
+  uint32_t w[4];
+  ld(T - 16, w);  // tail bytes [T - 16, T)
+  if (h >= 16) {  // low [0, 16) [16, h), high [h, h + 16) and [h + 16, T) from the last window
+    ld(0, v);
+    ld(16, v + 4);
+    keep16(v + 4, h - 16);
+    ld(h, v + 8);
+    funnel16(w, z, 32 - h, v + 12);  // high byte 16 sits at 32 - h of the window
+    keep16(v + 12, h - 16);
+  } else {        // T < 32: low [0, h) from the first 16 bytes, high [0, h) from the last window
+    ld(0, v);
+    keep16(v, h);
+    funnel16(w, z, 16 - h, v + 8);
+    keep16(v + 8, h);
+    static_for<4>([&](auto W) {
+      v[4 + decltype(W)::value] = 0u;
+      v[12 + decltype(W)::value] = 0u;
+    });
+  }
 }
+// The inverse: the T bytes of a restored tail chunk (raw words v[16], symbols h..31 zero).
+// Stores go low run first, then high run, so a window's bytes past the low run are rewritten
+// by the high run's stores in program order; overlapping windows carry equal bytes.
 __device__ __forceinline__ void store_tail_chunk(uint8_t* dst, uint32_t T, const uint32_t* v) {
   T = __builtin_amdgcn_readfirstlane(T);
-  const int h = static_cast<int>(T / 2);
-  uint32_t lo[2][4], hi[2][4];  // the low / high bytes of symbols 0..31, zeros from h on
-  static_for<4>([&](auto W) {
-    constexpr int w = decltype(W)::value;
-    lo[0][w] = v[w]; lo[1][w] = v[4 + w]; hi[0][w] = v[8 + w]; hi[1][w] = v[12 + w];
-  });
-  keep16(lo[0], static_cast<uint32_t>(h));
-  keep16(lo[1], static_cast<uint32_t>(h > 16 ? h - 16 : 0));
-  keep16(hi[0], static_cast<uint32_t>(h));
-  keep16(hi[1], static_cast<uint32_t>(h > 16 ? h - 16 : 0));
-  uint32_t L[4][4];  // the tail's bytes: low bytes [0, h), high bytes [h, 2 h)
-  static_for<4>([&](auto K) {
-    constexpr int k = decltype(K)::value;
-    uint32_t a[4], b[4];
-    bytes_at<2>(lo, 16 * k, a);
-    bytes_at<2>(hi, 16 * k - h, b);
-    static_for<4>([&](auto W) { L[k][decltype(W)::value] = a[decltype(W)::value] | b[decltype(W)::value]; });
-  });
-  static_for<4>([&](auto K) {
-    constexpr uint32_t k = decltype(K)::value;
-    if (16 * k + 16 <= T) {
-      st16u(dst + 16 * k, make_uint4(L[k][0], L[k][1], L[k][2], L[k][3]));
-    } else if (16 * k < T) {  // the window [T - 16, T), overlapping piece k - 1 with equal bytes
-      uint32_t w[4];
-      bytes_at<4>(L, static_cast<int>(T) - 16, w);
-      st16u(dst + T - 16, make_uint4(w[0], w[1], w[2], w[3]));
-    }
-  });
+  const uint32_t h = T / 2;
+  const uint32_t z[4] = {0u, 0u, 0u, 0u};
+  auto st = [&](uint32_t off, const uint32_t* x) __attribute__((always_inline)) {
+    st16u(dst + off, make_uint4(x[0], x[1], x[2], x[3]));
+  };
+  if (h >= 16) {
+    st(0, v);      // low [0, 16)
+    st(16, v + 4); // low [16, h) (bytes [h, 32) are rewritten below)
+    st(h, v + 8);  // high [0, 16) at [h, h + 16)
+    uint32_t w[4];
+    funnel16(v + 8, v + 12, h - 16, w);  // high [h - 16, h) at [T - 16, T)
+    st(T - 16, w);
+  } else {
+    st(0, v);      // low [0, h) (bytes [h, 16) are rewritten below)
+    // the window [T - 16, T) = low [T - 16, h) ++ high [0, h): the 32 bytes low | high << h
+    uint32_t lo[4] = {v[0], v[1], v[2], v[3]}, a[4], b[4], w[4];
+    keep16(lo, h);
+    funnel16(z, v + 8, 16 - h, a);  // high [0, 16 - h) at byte h
+    static_for<4>([&](auto W) { a[decltype(W)::value] |= lo[decltype(W)::value]; });
+    funnel16(v + 8, z, 16 - h, b);  // high [16 - h, h) at byte 16
+    funnel16(a, b, T - 16, w);
+    st(T - 16, w);
+  }
 }
 
 // piece q of shard `base` (a tail piece is its lane's whole window: tail_fix_all after the

@@ -1073,10 +1073,12 @@ def test_decode_per_slice_random_patterns(ctx, dev, S, n, mode):
     assert np.array_equal(got, blocks)
 
 
-@pytest.mark.parametrize("S,n", [(1024, 300), (960, 257), (1000, 300), (192, 131), (64, 600), (2000, 90)])
+@pytest.mark.parametrize("S,n", [(1024, 300), (960, 257), (1000, 300), (192, 131), (64, 600), (2000, 90), (968, 200),
+                                 (1022, 150)])
 def test_decode_device_patterns_lost_coding(ctx, dev, S, n):
     """Per-block patterns of the 32:32 code with lost coding shreds on tiles that straddle blocks
-    (S < 4 KiB, and the whole chunks plus restrided tail of S = 1000 / 2000): the window decode
+    (S < 4 KiB; S = 1000 / 2000 / 1022 with their T >= 16-byte tails as the last column of the
+    same decode, decode_h8 TAIL; S = 968's 8-byte tail restrided): the window decode
     with its masks built on the device from the packed presence words (decode_cols_device_
     patterns).  Random 8-20 data shards erased and 1-12 coding shards lost per block, a few
     blocks with every data shard present; absent shards overwritten with garbage; ANY_K.
@@ -1099,7 +1101,8 @@ def test_decode_device_patterns_lost_coding(ctx, dev, S, n):
             d_r[b, j] = 0x99
     got = gpu_decode(ctx, dev, d_o, d_r, op, rp, rs.DECODE_ANY_K)
     assert np.array_equal(got, blocks)
-    parts = 1 if S % 64 == 0 else 2  # whole chunks, then the restrided tail: both add patterns
+    # one decode, or the whole chunks then the restrided tail (T < 16): both add patterns
+    parts = 1 if S % 64 == 0 or S % 64 >= 16 else 2
     assert rs.last_decode_classes(ctx) == {"window64": parts * restore, "none": parts * (n - restore)}
 
 
