@@ -946,7 +946,9 @@ __device__ __forceinline__ uint32_t poly_pow_a(const PkLocTables& t, uint32_t l)
 
 // SRV: the per-call server's one-slice job; the locator constants of slice 0 are computed in
 // the list phase by wave 0 (decode_rows' Walsh route over `loc`) instead of read from p.rows.
-template <int OUTH, bool SRV = false>
+// TAIL: shreds of S = 960 + T bytes (16 <= T < 64): column 15 of an item is the shred's T-byte
+// tail, moved whole by its lanes (load_tail_chunk / store_tail_chunk, as decode_h8's TAIL).
+template <int OUTH, bool SRV = false, bool TAIL = false>
 __device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t tile, uint4* lds, X8Flags* fl,
                                                PkShared& sh, const PkLocTables* loc = nullptr) {
   static_assert(OUTH >= -1 && OUTH <= 1, "OUTH: the restored positions' window half, -1 both");
@@ -1001,6 +1003,7 @@ __device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t 
   const uint32_t nout = noA + static_cast<uint32_t>(__builtin_popcountll(omB));
   if (nout == 0) return;  // nothing restored in either slice (workgroup-uniform)
   const int col = lane & 15, row = lane >> 4;
+  const bool tail_lane = TAIL && col == kSl - 1;
   // the byte offset of position g's shard of slice sl, column col (recovery shards below the
   // originals in HighRate)
   auto src_of = [&](uint32_t sl, uint32_t g) -> const uint8_t* {
@@ -1019,14 +1022,18 @@ __device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t 
     if (i < nin) {
       const uint32_t sl = i < nA ? 0u : 1u;
       const uint8_t* src = src_of(sl, ilist[sl][i - (sl ? nA : 0u)]);
-      static_for<4>([&](auto Q) {
-        constexpr int q = decltype(Q)::value;
-        const uint4 x = ld_piece(src + 16 * q);
-        v[u][4 * q] = x.x;
-        v[u][4 * q + 1] = x.y;
-        v[u][4 * q + 2] = x.z;
-        v[u][4 * q + 3] = x.w;
-      });
+      if (tail_lane) {
+        load_tail_chunk(src, p.tail_bytes, v[u]);
+      } else {
+        static_for<4>([&](auto Q) {
+          constexpr int q = decltype(Q)::value;
+          const uint4 x = ld_piece(src + 16 * q);
+          v[u][4 * q] = x.x;
+          v[u][4 * q + 1] = x.y;
+          v[u][4 * q + 2] = x.z;
+          v[u][4 * q + 3] = x.w;
+        });
+      }
     } else {
       static_for<16>([&](auto P) { v[u][decltype(P)::value] = 0; });
     }
@@ -1206,18 +1213,24 @@ __device__ __forceinline__ void decode_pk_tile(const DecodeXParams& p, uint32_t 
           v[4 * q + 3] = x.w;
         });
         dev::mul_rt_poly(v, lcoef[sl * W + j]);
-        dev::store_chunk<true>(const_cast<uint8_t*>(src_of(sl, j)), v);
+        if (tail_lane) {
+          dev::transpose8(v);
+          dev::transpose8(v + 8);
+          store_tail_chunk(const_cast<uint8_t*>(src_of(sl, j)), p.tail_bytes, v);
+        } else {
+          dev::store_chunk<true>(const_cast<uint8_t*>(src_of(sl, j)), v);
+        }
       }
     }
   });
 }
 
-template <int OUTH>
+template <int OUTH, bool TAIL = false>
 __global__ __launch_bounds__(512, 4) void decode_pk_kernel(const DecodeXParams p) {
   __shared__ uint4 lds[16 * 4 * kXfLanes];
   __shared__ X8Flags flags;
   __shared__ PkShared sh;
-  decode_pk_tile<OUTH>(p, dev::xcd_tile(blockIdx.x, gridDim.x), lds, &flags, sh);
+  decode_pk_tile<OUTH, false, TAIL>(p, dev::xcd_tile(blockIdx.x, gridDim.x), lds, &flags, sh);
 }
 
 // Per pattern and window position x: the decoder's locator constant as a bitsliced
@@ -2076,6 +2089,12 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
       // shards with a T-byte tail chunk (per-lane HighRate chunk 32): decode_h8's TAIL variant
       if (!pl || p.low_rate || p.chunk != 32 || p.tail_bytes < 16 || p.tail_bytes >= 64 || p.tail_bytes % 2)
         return hipErrorInvalidValue;
+      if (p.any_k && p.chunks_per_shard == 16) {  // S = 960 + T: the packed decoder, tail column 15
+        if (p.fuse) hipLaunchKernelGGL((decode_pk_kernel<-1, true>), g32, dim3(512), 0, stream, p);
+        else hipLaunchKernelGGL((decode_pk_kernel<1, true>), g32, dim3(512), 0, stream, p);
+        rec(p.fuse ? kDxPkFused : kDxPk);
+        return hipGetLastError();
+      }
       if (p.fuse) AG_H8T(-1);
       else AG_H8T(1);
       rec(p.fuse ? kDxH8Fused : kDxH8);

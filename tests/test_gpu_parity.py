@@ -840,8 +840,9 @@ def test_coder_deshred_uniform_lowrate_chunks(ctx, dev, S, keep, kernels):
 def test_coder_deshred_fused_coding_restore(ctx, dev, mode, S):
     """The follower's deshred at exactly k = 32 kept shreds (slot_block_data.rs:343-355): the
     window decoder restores the absent coding shreds in the same transform as the data shreds
-    (1 KiB shreds: decode_pk<-1>; other sizes: decode_h8<-1>, whose TAIL variant moves a last
-    chunk of T = S mod 64 >= 16 bytes (S = 1000, 1022, 80, 126) whole; no re-encode pass),
+    (16 columns per shred -- 1 KiB, or 960 + T bytes -- decode_pk<-1>; other sizes decode_h8<-1>;
+    the TAIL variants move a last chunk of T = S mod 64 >= 16 bytes (S = 1000, 1022, 80, 126)
+    whole; no re-encode pass),
     bit-exact against the oracle's re-encode (o.encode of the restored data,
     reed_solomon.rs:206), mixed with slices that keep the separate re-encode (surplus shreds;
     every data shred present), NotEnoughShreds and InvalidPadding slices.  Every absent shred is
@@ -900,7 +901,7 @@ def test_coder_deshred_fused_coding_restore(ctx, dev, mode, S):
         assert host[b, :32 * S].tobytes() == b"".join(raw.data), b
         assert host[b, 32 * S:].tobytes() == b"".join(raw.coding), b
     assert ok >= n - 4
-    assert rs.last_window_kernels(ctx) == {"decode_pk_fused" if S == 1024 else "decode_h8_fused"}
+    assert rs.last_window_kernels(ctx) == {"decode_pk_fused" if (S + 63) // 64 == 16 else "decode_h8_fused"}
 
 
 @pytest.mark.parametrize("S", [1024, 256, 1000])
@@ -930,7 +931,7 @@ def test_coder_deshred_fused_at_scale(ctx, dev, S):
     res = rs.coder_deshred_batch(ctx, m, n, S, d_cw, stride, dp, cp, rs.DECODE_ANY_K, as_array=True)
     assert (res == L).all()
     assert torch.equal(d_cw, want)
-    assert rs.last_window_kernels(ctx) == {"decode_pk_fused" if S == 1024 else "decode_h8_fused"}
+    assert rs.last_window_kernels(ctx) == {"decode_pk_fused" if (S + 63) // 64 == 16 else "decode_h8_fused"}
     assert rs.last_encode_kernels(ctx) == set()  # the re-encode was skipped
     host = want[:4].cpu().numpy()
     for b in range(4):
