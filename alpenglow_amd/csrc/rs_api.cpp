@@ -1954,11 +1954,13 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, PinBuf& pin, cons
       return st;
     return AG_RS_OK;
   }
-  if (present == k && S == 1024 && server_fits(c, k, m, S)) {
-    // exactly k = 32 of the 64 shreds of a 32:32 slice of 1 KiB shreds (the follower's deshred
-    // at its 32nd arriving shred): decode_pk<-1>'s one-slice window decode on the server
-    // restores every absent data and coding shred in place -- the codeword through the 32
-    // survivors is unique, so the restored coding shreds are the re-encode, bit for bit
+  const bool pk_size = S == 1024 || (S > 960 && S < 1024 && S % 64 >= 16 && S % 2 == 0);
+  if (present == k && pk_size && k == 32 && m == 32 && !c->server_broken) {
+    // exactly k = 32 of the 64 shreds of a 32:32 slice of 1 KiB shreds, or of 960 + T bytes
+    // with a T >= 16-byte tail (the follower's deshred at its 32nd arriving shred):
+    // decode_pk<-1>'s one-slice window decode on the server restores every absent data and
+    // coding shred in place -- the codeword through the 32 survivors is unique, so the restored
+    // coding shreds are the re-encode, bit for bit
     uint64_t pres = 0;
     for (size_t j = 0; j < m; ++j)
       if (rpres[j]) pres |= uint64_t{1} << j;
@@ -1981,6 +1983,7 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, PinBuf& pin, cons
     dp.rows_w = 64;
     dp.any_k = 1;
     dp.fuse = 1;
+    dp.tail_bytes = static_cast<uint32_t>(S % 64);
     std::fill(std::begin(c->last_classes), std::end(c->last_classes), uint64_t{0});
     ++c->last_classes[9];  // "server_window64"
     if ((st = server_job(c, ag::kJobDecodePk, ag::XformParams{}, pres, pin, &dp))) return st;

@@ -1494,7 +1494,7 @@ def test_per_call_server_jobs_and_restart(ctx):
 
     coder = rs.ReedSolomonCoder(ctx, 32)
     rng = random.Random(4242)
-    sizes = [32767, 32704, 2047, 4095, 1000, 16383, 63, 0, 20000]
+    sizes = [32767, 32704, 2047, 4095, 1000, 16383, 63, 0, 20000, 31999, 32700]
     jobs0 = rs.server_jobs(ctx)
     pk_calls = 0
     for i in range(45):
@@ -1504,8 +1504,8 @@ def test_per_call_server_jobs_and_restart(ctx):
         assert raw.data == exp.data and raw.coding == exp.coding, (i, len(payload))
         got, raw2 = coder.deshred([None] * 32 + [(False, c) for c in raw.coding])
         assert got == payload and raw2.coding == exp.coding, (i, len(payload))
-        # random arrival: exactly 32 of 64 (S = 1 KiB: the server's decode_pk job, data and
-        # coding restored in one job), and a surplus set (launch path)
+        # random arrival: exactly 32 of 64 (S = 1 KiB or 960 + T: the server's decode_pk job, data
+        # and coding restored in one job), and a surplus set (launch path)
         for cnt in (32, 40):
             keep = sorted(rng.sample(range(64), cnt))
             shreds = [((j < 32), (raw.data + raw.coding)[j]) if j in keep else None for j in range(64)]
@@ -1514,7 +1514,9 @@ def test_per_call_server_jobs_and_restart(ctx):
             assert got == payload and raw3.data == exp.data and raw3.coding == exp.coding, (i, keep)
             served = rs.server_jobs(ctx)["decode_pk"] - before
             lost = set(range(64)) - set(keep)
-            fits = (cnt == 32 and len(raw.data[0]) == 1024 and any(j < 32 for j in lost)
+            S = len(raw.data[0])  # 1 KiB, or 960 + T with a T >= 16-byte tail (S = 1000, 1022)
+            pk_size = S == 1024 or (960 < S < 1024 and S % 64 >= 16)
+            fits = (cnt == 32 and pk_size and any(j < 32 for j in lost)
                     and any(j >= 32 for j in lost))  # else: no decode, or the coding-only transform
             assert served == (1 if fits else 0), (i, cnt, len(raw.data[0]))
             pk_calls += served
