@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--arrived", type=int, default=32, help="datagrams received per slice before deshred (32..64)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--shred-bytes", type=int, default=1024,
+                    help="shred size S (even, <= 1024): payloads of 32 S - 1 bytes; 1024 = maximum slices")
     ap.add_argument("--kind", choices=list(KINDS), default="regular",
                     help="the shredder (shredder.rs:336-500); the CPU baseline is timed for regular only")
     args = ap.parse_args()
@@ -54,7 +56,8 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     ctx.set_stream(stream.cuda_stream)
-    n, S = args.slices, 1024
+    n, S = args.slices, args.shred_bytes
+    assert S % 2 == 0 and 64 <= S <= 1024, "--shred-bytes: even, 64..1024"
     kind, m, extra = KINDS[args.kind]
     D = 32 * S - 1 - 9 - extra  # data bytes: framed payload (+ key) = MAX_DATA_PER_SLICE
     stride = (32 + m) * S
@@ -130,7 +133,8 @@ def main():
         spot &= all(hp[b * 64 + j, :hl[b * 64 + j]].tobytes() == want[j] for j in range(64))
     steps = args.steps
     line = {
-        "metric": f"slices/s composed {NAMES[args.kind]} shred + deshred (datagrams in, datagrams out), max slices",
+        "metric": f"slices/s composed {NAMES[args.kind]} shred + deshred (datagrams in, datagrams out), "
+                  + ("max slices" if S == 1024 else f"{S}-byte shreds"),
         "value": n * steps / (t_sh + t_de),
         "unit": "slices/s",
         "n_gpus": 1,
@@ -142,7 +146,7 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (splitmix64 payloads, device-generated; one leader key)",
-        "config": {"workload": f"{n} slices x {D + 9} B payload, 64 datagrams of 1325 B per slice; deshred from a "
+        "config": {"workload": f"{n} slices x {D + 9} B payload, 64 datagrams of {S + 301} B per slice; deshred from a "
                                f"random {args.arrived} of 64 datagrams per slice"},
         "payload_GiBps": n * (D + 9) * steps / (t_sh + t_de) / GIB,
         "calls_ms": {"shred_batch": t_sh * 1e3 / steps, "deshred_batch": t_de * 1e3 / steps},
