@@ -672,7 +672,7 @@ int decode_device_body(ag_rs_ctx* c, size_t k, size_t m, size_t S, size_t nblock
       int st;
       // per-block 32:32 patterns with lost recovery shards (ANY_K): the per-lane window decode
       // takes the whole shards, the T-byte tail as one more column (decode_h8 TAIL), no restride
-      if (tail >= 16 && npat > 1 && npat == nblocks && k == 32 && m == 32 && hr == 1 && mode == AG_RS_DECODE_ANY_K) {
+      if (tail != 0 && npat > 1 && npat == nblocks && k == 32 && m == 32 && hr == 1 && mode == AG_RS_DECODE_ANY_K) {
         st = decode_cols_device_patterns(c, S, S, nblocks, orig, ostride, rec, rstride, opres, rpres);
         if (st != kNotApplicable) return st;
       }
@@ -2422,8 +2422,13 @@ namespace {
 int pipe_coder_deshred(ag_rs_ctx* c, size_t n, size_t S, uint8_t* cw, size_t cw_stride, const uint64_t* d_present,
                        int64_t* plen, size_t m, bool no_surplus = false);
 // shred sizes pipe_coder_deshred decodes on the device: whole 64-byte chunks (any m of the
-// device-pattern path), or for 32:32 a last chunk of T = S mod 64 >= 16 bytes
-bool pipe_tail_ok(size_t S, size_t m) { return S % 64 == 0 || (m == kDataShreds && S % 64 >= 16 && S % 2 == 0); }
+// device-pattern path), or for 32:32 a last chunk of T = S mod 64 bytes -- T >= 16 always, a
+// shorter T when no slice needs the re-encode (no_reencode: no surplus shreds, no slice with
+// every data shred; the TAIL encode takes T >= 16 only)
+bool pipe_tail_ok(size_t S, size_t m, bool no_reencode = false) {
+  const size_t T = S % 64;
+  return T == 0 || (m == kDataShreds && S % 2 == 0 && (T >= 16 || no_reencode));
+}
 }  // namespace
 
 namespace {
@@ -2573,7 +2578,8 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
   // path below (a single transform launch).
   // CodingOnlyShredder's 32:64 and PetsShredder's 32:33 (LowRate, 32 < m <= 64) take the same
   // path with the W = 128 window (positions of coding shreds past m are simply never present).
-  if (m >= kDataShreds && m <= 2 * kDataShreds && pipe_tail_ok(S, m) && n > 1 && !odd_layout(cw, cw, cw_stride, cw_stride)) {
+  if (m >= kDataShreds && m <= 2 * kDataShreds && pipe_tail_ok(S, m, true) && n > 1 &&
+      !odd_layout(cw, cw, cw_stride, cw_stride)) {
     const size_t wps = m == kDataShreds ? 1 : 2;  // present words per slice
     // packed straight into pinned staging, so the upload is one DMA with no pageable bounce
     // (once the previous call's upload of it has completed)
@@ -2587,7 +2593,7 @@ int ag_rs_coder_deshred_batch(ag_rs_ctx* c, size_t m, size_t n, size_t S, uint8_
     // measured even with one whole-batch range, profiles/r05_ab_coder_ranges.jsonl.)
     bool full_data = false;
     const bool surplus = pack_present_words(dpres, cpres, m, n, pres, &full_data);
-    if (mode == AG_RS_DECODE_ANY_K || !surplus) {
+    if ((mode == AG_RS_DECODE_ANY_K || !surplus) && pipe_tail_ok(S, m, !surplus && !full_data)) {
       if ((st = c->d_present.ensure(wps * n * 8, c->stream))) return st;
       AG_HIP(hipMemcpyAsync(c->d_present.ptr, pres, wps * n * 8, hipMemcpyHostToDevice, c->stream));
       AG_HIP(hipEventRecord(c->present_ev, c->stream));
@@ -3458,9 +3464,14 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   // 4. ReedSolomonCoder::deshred over the kept shreds (restores the data shreds, re-encodes
   //    all coding shreds, strips the padding); on the device for whole-chunk shreds
   std::vector<int64_t> plen(n);
-  const bool device_coder = pipe_tail_ok(S, kDataShreds);
+  bool no_reencode = true;  // no surplus shreds and no slice with every data shred
+  for (size_t s = 0; s < n && no_reencode; ++s)
+    no_reencode = __builtin_popcountll(h_present[s]) <= static_cast<int>(ag::kPipeData) &&
+                  (h_present[s] & 0xFFFFFFFFull) != 0xFFFFFFFFull;
+  const bool device_coder = pipe_tail_ok(S, kDataShreds, no_reencode);
   if (device_coder) {
-    if ((st = pipe_coder_deshred(c, n, S, codewords, cw_stride, d_present, plen.data(), kDataShreds))) return st;
+    if ((st = pipe_coder_deshred(c, n, S, codewords, cw_stride, d_present, plen.data(), kDataShreds, no_reencode)))
+      return st;
   } else {
     std::vector<uint8_t> dp(n * ag::kPipeData), cp(n * (ag::kPipeShreds - ag::kPipeData));
     for (size_t s = 0; s < n; ++s)
@@ -3771,7 +3782,7 @@ int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_
   uint64_t* d_present = nullptr;
   uint8_t *sroot = nullptr, *ssig = nullptr, *ssidx = nullptr, *slast = nullptr, *fresh = nullptr;
   uint64_t* d_slot = nullptr;
-  const bool fast_ok = pipe_tail_ok(S, k.m) && n > 1 && k.m >= kDataShreds && k.m <= 2 * kDataShreds;
+  const bool fast_ok = pipe_tail_ok(S, k.m, true) && n > 1 && k.m >= kDataShreds && k.m <= 2 * kDataShreds;
   // 7. fill_missing_shreds (part 1): the absent datagrams of the slices in `okv`, lengths into
   // `fresh` (pipe_merge_lens moves the final slices' lengths into packet_lens)
   auto serialize_absent = [&](const std::vector<uint8_t>& okv) -> int {
@@ -3880,12 +3891,14 @@ int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_
     std::vector<int64_t> plen(n);
     bool surplus = false;
     for (size_t s = 0; s < n; ++s) surplus |= __builtin_popcountll(h_present[s]) > static_cast<int>(kDataShreds);
-    if (pass == 0) {
+    bool full_data = false;
+    if (kind == AG_SHREDDER_AONT)
+      for (size_t s = 0; s < n; ++s) full_data |= (h_present[s] & 0xFFFFFFFFull) == 0xFFFFFFFFull;
+    if (pass == 0 && pipe_tail_ok(S, k.m, !surplus && !full_data)) {
       // codeword-row present words (pipe_coder_deshred: data | coding 0..31 << 32, coding
       // 32..63 in word 1 when m > 32); AONT's rows are the codeword rows
       const size_t wps = k.m > kDataShreds ? 2 : 1;
       const uint64_t* words = d_present;
-      bool full_data = false;
       if (kind != AG_SHREDDER_AONT) {
         uint8_t* dw;
         if ((st = pipe_buf(c, 25, 8 * wps * n, &dw)) || (st = c->h_strip.ensure(8 * wps * n))) return st;
@@ -3902,8 +3915,6 @@ int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_
         }
         AG_HIP(hipMemcpyAsync(dw, hw, 8 * wps * n, hipMemcpyHostToDevice, c->stream));
         words = reinterpret_cast<const uint64_t*>(dw);
-      } else {
-        for (size_t s = 0; s < n; ++s) full_data |= (h_present[s] & 0xFFFFFFFFull) == 0xFFFFFFFFull;
       }
       // (pipe_coder_deshred reads its results back through h_strip after the upload completed)
       if ((st = pipe_coder_deshred(c, n, S, codewords, cw_stride, words, plen.data(), k.m, !surplus && !full_data)))

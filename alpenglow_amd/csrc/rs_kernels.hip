@@ -2087,8 +2087,7 @@ hipError_t launch_decode_x(unsigned W, int pass, const DecodeXParams& p, uint64_
     if (p.rows_w != 64) return hipErrorInvalidValue;
     if (p.tail_bytes) {
       // shards with a T-byte tail chunk (per-lane HighRate chunk 32): decode_h8's TAIL variant
-      if (!pl || p.low_rate || p.chunk != 32 || p.tail_bytes < 16 || p.tail_bytes >= 64 || p.tail_bytes % 2)
-        return hipErrorInvalidValue;
+      if (!pl || p.low_rate || p.chunk != 32 || p.tail_bytes >= 64 || p.tail_bytes % 2) return hipErrorInvalidValue;
       if (p.any_k && p.chunks_per_shard == 16) {  // S = 960 + T: the packed decoder, tail column 15
         if (p.fuse) hipLaunchKernelGGL((decode_pk_kernel<-1, true>), g32, dim3(512), 0, stream, p);
         else hipLaunchKernelGGL((decode_pk_kernel<1, true>), g32, dim3(512), 0, stream, p);

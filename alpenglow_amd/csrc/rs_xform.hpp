@@ -286,16 +286,59 @@ __device__ __forceinline__ void keep16(uint32_t* v, uint32_t len) {
     v[k] &= m;
   });
 }
-// One lane's whole tail chunk (T = S mod 64 bytes, 16 <= T < 64, even, uniform; h = T / 2
+// A short tail (T < 16 bytes, even, uniform) as one 16-byte value, zeros from T on: its 8-, 4-
+// and 2-byte parts where present (accesses inside [0, T) only)
+__device__ __forceinline__ void load_short_tail(const uint8_t* src, uint32_t T, uint32_t* b) {
+  b[0] = b[1] = b[2] = b[3] = 0u;
+  if (T & 8) {
+    const uint2 x = ld8u(src);
+    b[0] = x.x;
+    b[1] = x.y;
+  }
+  if (T & 4) {
+    const uint32_t x = ld4u(src + (T & 8));
+    if (T & 8) b[2] = x;
+    else b[0] = x;
+  }
+  if (T & 2) {
+    const uint32_t x = ld2u(src + (T & 12));  // word (T & 12) / 4, low half
+    const uint32_t w = (T & 12) >> 2;
+    if (w == 0) b[0] |= x;
+    else if (w == 1) b[1] |= x;
+    else if (w == 2) b[2] |= x;
+    else b[3] |= x;
+  }
+}
+__device__ __forceinline__ void store_short_tail(uint8_t* dst, uint32_t T, const uint32_t* b) {
+  if (T & 8) st8u(dst, make_uint2(b[0], b[1]));
+  if (T & 4) st4u(dst + (T & 8), (T & 8) ? b[2] : b[0]);
+  if (T & 2) {
+    const uint32_t w = (T & 12) >> 2;
+    st2u(dst + (T & 12), w == 0 ? b[0] : w == 1 ? b[1] : w == 2 ? b[2] : b[3]);
+  }
+}
+// One lane's whole tail chunk (T = S mod 64 bytes, 2 <= T < 64, even, uniform; h = T / 2
 // symbols): the crate keeps the h low bytes then the h high bytes, i.e. the
 // 64-byte chunk (low bytes [0, 32), high bytes [32, 64)) with symbols h..31 zero.  Moved with
-// 16-byte accesses inside [0, T) only, so no byte of the next shard is touched: a run that
-// would cross T comes from (goes to) the window [T - 16, T) through one uniform funnel.  Raw
-// chunk words in v[16] (before planes_from_raw / after the inverse transpose).
+// accesses inside [0, T) only, so no byte of the next shard is touched: for T >= 16, 16-byte
+// windows, a run that would cross T coming from (going to) the window [T - 16, T) through one
+// uniform funnel; a shorter tail as its 8-, 4- and 2-byte parts.  Raw chunk words in v[16]
+// (before planes_from_raw / after the inverse transpose).
 __device__ __forceinline__ void load_tail_chunk(const uint8_t* src, uint32_t T, uint32_t* v) {
   T = __builtin_amdgcn_readfirstlane(T);
   const uint32_t h = T / 2;
   const uint32_t z[4] = {0u, 0u, 0u, 0u};
+  if (T < 16) {  // low [0, h) and high [0, h) of the one short value
+    load_short_tail(src, T, v);
+    funnel16(v, z, h, v + 8);
+    keep16(v, h);
+    keep16(v + 8, h);
+    static_for<4>([&](auto W) {
+      v[4 + decltype(W)::value] = 0u;
+      v[12 + decltype(W)::value] = 0u;
+    });
+    return;
+  }
   auto ld = [&](uint32_t off, uint32_t* out) __attribute__((always_inline)) {
     const uint4 x = ld16u(src + off);
     out[0] = x.x; out[1] = x.y; out[2] = x.z; out[3] = x.w;
@@ -327,6 +370,14 @@ __device__ __forceinline__ void store_tail_chunk(uint8_t* dst, uint32_t T, const
   T = __builtin_amdgcn_readfirstlane(T);
   const uint32_t h = T / 2;
   const uint32_t z[4] = {0u, 0u, 0u, 0u};
+  if (T < 16) {  // low [0, h) | high [0, h) << h as one short value
+    uint32_t lo[4] = {v[0], v[1], v[2], v[3]}, hs[4];
+    keep16(lo, h);
+    funnel16(z, v + 8, 16 - h, hs);
+    static_for<4>([&](auto W) { lo[decltype(W)::value] |= hs[decltype(W)::value]; });
+    store_short_tail(dst, T, lo);
+    return;
+  }
   auto st = [&](uint32_t off, const uint32_t* x) __attribute__((always_inline)) {
     st16u(dst + off, make_uint4(x[0], x[1], x[2], x[3]));
   };

@@ -27,5 +27,13 @@ __device__ __forceinline__ uint4 ld16u(const void* p) {
 __device__ __forceinline__ void st16u(void* p, uint4 v) { *static_cast<u32x4_u*>(p) = u32x4_u{v.x, v.y, v.z, v.w}; }
 __device__ __forceinline__ void st8u(void* p, uint2 v) { *static_cast<u32x2_u*>(p) = u32x2_u{v.x, v.y}; }
 __device__ __forceinline__ void st4u(void* p, uint32_t v) { *static_cast<u32_u*>(p) = v; }
+typedef uint16_t u16_u __attribute__((aligned(1)));
+__device__ __forceinline__ uint2 ld8u(const void* p) {
+  const u32x2_u v = *static_cast<const u32x2_u*>(p);
+  return make_uint2(v.x, v.y);
+}
+__device__ __forceinline__ uint32_t ld4u(const void* p) { return *static_cast<const u32_u*>(p); }
+__device__ __forceinline__ uint32_t ld2u(const void* p) { return *static_cast<const u16_u*>(p); }
+__device__ __forceinline__ void st2u(void* p, uint32_t v) { *static_cast<u16_u*>(p) = static_cast<uint16_t>(v); }
 
 }  // namespace ag

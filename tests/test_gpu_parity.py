@@ -904,10 +904,11 @@ def test_coder_deshred_fused_coding_restore(ctx, dev, mode, S):
     assert rs.last_window_kernels(ctx) == {"decode_pk_fused" if (S + 63) // 64 == 16 else "decode_h8_fused"}
 
 
-@pytest.mark.parametrize("S", [1024, 256, 1000])
+@pytest.mark.parametrize("S", [1024, 256, 1000, 968, 66])
 def test_coder_deshred_fused_at_scale(ctx, dev, S):
     """The fused route at production scale: 4096 slices, each received as a random 32 of its 64
-    shreds (absent shreds overwritten with garbage).  Every slice must come back as its
+    shreds (absent shreds overwritten with garbage); S = 1000 / 968 / 66 end in a tail chunk of
+    40 / 8 / 2 bytes (short tails take the device path because no slice needs the re-encode).  Every slice must come back as its
     original codeword (data and coding shreds); the kernel record shows the fused window
     decoder ran and no re-encode kernel was launched (no slice has surplus or every data
     shred).  A sample of slices is also checked against the oracle's coder."""
@@ -1075,11 +1076,11 @@ def test_decode_per_slice_random_patterns(ctx, dev, S, n, mode):
 
 
 @pytest.mark.parametrize("S,n", [(1024, 300), (960, 257), (1000, 300), (192, 131), (64, 600), (2000, 90), (968, 200),
-                                 (1022, 150)])
+                                 (1022, 150), (66, 400)])
 def test_decode_device_patterns_lost_coding(ctx, dev, S, n):
     """Per-block patterns of the 32:32 code with lost coding shreds on tiles that straddle blocks
-    (S < 4 KiB; S = 1000 / 2000 / 1022 with their T >= 16-byte tails as the last column of the
-    same decode, decode_h8 TAIL; S = 968's 8-byte tail restrided): the window decode
+    (S < 4 KiB; S = 1000 / 2000 / 1022 / 968 / 66 with their tails as the last column of the
+    same decode, decode_h8 / decode_pk TAIL, no restride): the window decode
     with its masks built on the device from the packed presence words (decode_cols_device_
     patterns).  Random 8-20 data shards erased and 1-12 coding shards lost per block, a few
     blocks with every data shard present; absent shards overwritten with garbage; ANY_K.
@@ -1102,8 +1103,7 @@ def test_decode_device_patterns_lost_coding(ctx, dev, S, n):
             d_r[b, j] = 0x99
     got = gpu_decode(ctx, dev, d_o, d_r, op, rp, rs.DECODE_ANY_K)
     assert np.array_equal(got, blocks)
-    # one decode, or the whole chunks then the restrided tail (T < 16): both add patterns
-    parts = 1 if S % 64 == 0 or S % 64 >= 16 else 2
+    parts = 1  # one decode, the tail (if any) as its last column
     assert rs.last_decode_classes(ctx) == {"window64": parts * restore, "none": parts * (n - restore)}
 
 
