@@ -1954,7 +1954,7 @@ int run_one_decode(ag_rs_ctx* c, size_t k, size_t m, size_t S, PinBuf& pin, cons
       return st;
     return AG_RS_OK;
   }
-  const bool pk_size = S == 1024 || (S > 960 && S < 1024 && S % 64 >= 16 && S % 2 == 0);
+  const bool pk_size = S == 1024 || (S > 960 && S < 1024 && S % 2 == 0);  // 16 columns, tail included
   if (present == k && pk_size && k == 32 && m == 32 && !c->server_broken) {
     // exactly k = 32 of the 64 shreds of a 32:32 slice of 1 KiB shreds, or of 960 + T bytes
     // with a T >= 16-byte tail (the follower's deshred at its 32nd arriving shred):

@@ -2325,7 +2325,7 @@ __global__ __launch_bounds__(512, 1) void latency_server_kernel(LatencyMailbox* 
         dp.pmask = pk_mask;
       }
       __syncthreads();
-      if (dp.tail_bytes) decode_pk_tile<-1, true, true>(dp, 0, lds, &flags, pk, &loc);  // S = 960 + T
+      if (dp.tail_bytes) decode_pk_tile<-1, true, true>(dp, 0, lds, &flags, pk, &loc);  // S = 960 + T, T < 64
       else decode_pk_tile<-1, true>(dp, 0, lds, &flags, pk, &loc);
       if (threadIdx.x == 0) t_tile = wall_clock64();
       __threadfence_system();

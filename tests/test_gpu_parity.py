@@ -1494,7 +1494,7 @@ def test_per_call_server_jobs_and_restart(ctx):
 
     coder = rs.ReedSolomonCoder(ctx, 32)
     rng = random.Random(4242)
-    sizes = [32767, 32704, 2047, 4095, 1000, 16383, 63, 0, 20000, 31999, 32700]
+    sizes = [32767, 32704, 2047, 4095, 1000, 16383, 63, 0, 20000, 31999, 32700, 30999]
     jobs0 = rs.server_jobs(ctx)
     pk_calls = 0
     for i in range(45):
@@ -1514,8 +1514,8 @@ def test_per_call_server_jobs_and_restart(ctx):
             assert got == payload and raw3.data == exp.data and raw3.coding == exp.coding, (i, keep)
             served = rs.server_jobs(ctx)["decode_pk"] - before
             lost = set(range(64)) - set(keep)
-            S = len(raw.data[0])  # 1 KiB, or 960 + T with a T >= 16-byte tail (S = 1000, 1022)
-            pk_size = S == 1024 or (960 < S < 1024 and S % 64 >= 16)
+            S = len(raw.data[0])  # 1 KiB, or 960 + T with a T-byte tail (S = 1000, 1022, 970)
+            pk_size = S == 1024 or 960 < S < 1024
             fits = (cnt == 32 and pk_size and any(j < 32 for j in lost)
                     and any(j >= 32 for j in lost))  # else: no decode, or the coding-only transform
             assert served == (1 if fits else 0), (i, cnt, len(raw.data[0]))
