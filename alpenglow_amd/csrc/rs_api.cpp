@@ -169,6 +169,9 @@ struct ag_rs_ctx {
   DevBuf d_empty_roots;                     // Merkle EMPTY_ROOTS [32][8] words
   DevBuf d_merkle_nodes;                    // Merkle node scratch (callers without a nodes buffer)
   DevBuf d_aon_lens, d_aon_digests, d_aon_keys;  // all-or-nothing transforms
+  DevBuf d_aon_lens2;                            // the side stream's SHA-256 lengths (AONT deshred)
+  hipStream_t side = nullptr;                    // a second compute stream (AONT deshred's SHA-256)
+  hipEvent_t side_fork = nullptr, side_join = nullptr;
   DevBuf d_slice_meta;                           // slice framing / parsing metadata
   DevBuf stage_pad, stage_mask;                  // restrided shards (sizes not whole 64-byte chunks)
   DevBuf d_lens, d_strip;                   // coder batches: payload lengths, strip results
@@ -245,6 +248,14 @@ struct ag_rs_ctx {
     return {d_exp.as<uint16_t>(), d_log.as<uint16_t>(), d_skew.as<uint16_t>(), d_log_walsh.as<uint16_t>()};
   }
 
+  int ensure_side_stream() {
+    if (side) return AG_RS_OK;
+    AG_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    AG_HIP(hipEventCreateWithFlags(&side_fork, hipEventDisableTiming));
+    AG_HIP(hipEventCreateWithFlags(&side_join, hipEventDisableTiming));
+    return AG_RS_OK;
+  }
+
   int ensure_copy_streams() {
     if (h2d) return AG_RS_OK;
     AG_HIP(hipStreamCreateWithFlags(&h2d, hipStreamNonBlocking));
@@ -289,6 +300,13 @@ struct ag_rs_ctx {
 
   ~ag_rs_ctx() {
     server_stop();
+    if (side) {
+      (void)hipSetDevice(device);
+      (void)hipStreamSynchronize(side);
+      (void)hipEventDestroy(side_fork);
+      (void)hipEventDestroy(side_join);
+      (void)hipStreamDestroy(side);
+    }
     if (own_stream) {
       (void)hipSetDevice(device);
       (void)hipStreamSynchronize(own_stream);
@@ -306,7 +324,7 @@ struct ag_rs_ctx {
       (void)hipStreamDestroy(d2h);
     }
     for (DevBuf* b : {&d_exp, &d_log, &d_skew, &d_log_walsh, &scratch, &d_flags, &d_loc, &d_blocks, &d_mask,
-                      &d_xmask, &d_rows, &d_xblocks, &d_x128, &d_rows128, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_lens, &d_strip, &d_reenc_mask, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
+                      &d_xmask, &d_rows, &d_xblocks, &d_x128, &d_rows128, &d_syn, &d_synblocks, &d_corr, &d_corrk, &d_corrblocks, &d_empty_roots, &d_merkle_nodes, &d_aon_lens, &d_aon_digests, &d_aon_keys, &d_aon_lens2, &d_lens, &d_strip, &d_reenc_mask, &d_ed_base, &d_sh_roots, &d_sh_commit, &d_sh_onvalid, &d_sh_list, &stage_in, &stage_out, &stage_pad, &stage_mask, &d_slice_meta, &one_in,
                       &one_out, &d_pipe_few, &d_pipe_mask, &d_present})
       b->release();
     for (DevBuf& b : pipe) b.release();
@@ -3932,6 +3950,37 @@ int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_
                                           plen.data())))
         return st;
     }
+    // AONT: the SHA-256 of every decoded ciphertext (decrypt_payload's key mask) runs on the side
+    // stream, overlapping the Merkle rebuild, the root comparison and the absent datagrams'
+    // serialization below (all of them only read the rows); one SHA-256 chain per slice leaves
+    // most of the chip's issue slots to them
+    bool sha_side = false;
+    if (k.aon == AG_AON_AONT) {
+      std::vector<uint32_t> shl(n);
+      uint32_t mx = ag::kCipherKeyBytes;
+      for (size_t s = 0; s < n; ++s) {
+        shl[s] = plen[s] >= static_cast<int64_t>(ag::kCipherKeyBytes) ? static_cast<uint32_t>(plen[s])
+                                                                      : static_cast<uint32_t>(ag::kCipherKeyBytes);
+        mx = std::max(mx, shl[s]);
+      }
+      if ((st = c->ensure_side_stream()) || (st = c->d_aon_lens2.ensure(n * 4, c->stream)) ||
+          (st = c->d_aon_digests.ensure(n * 32, c->stream)))
+        return st;
+      AG_HIP(hipStreamSynchronize(c->stream));
+      AG_HIP(hipMemcpy(c->d_aon_lens2.ptr, shl.data(), n * 4, hipMemcpyHostToDevice));
+      ag::BufferBatch sb;
+      sb.base = codewords;
+      sb.stride = cw_stride;
+      sb.lens = c->d_aon_lens2.as<uint32_t>();
+      sb.n = n;
+      sb.max_len = mx;
+      AG_HIP(hipEventRecord(c->side_fork, c->stream));
+      AG_HIP(hipStreamWaitEvent(c->side, c->side_fork, 0));
+      if (ag::launch_sha256(sb, ag::kCipherKeyBytes, c->d_aon_digests.as<uint8_t>(), c->side) != hipSuccess)
+        return AG_RS_ERR_DEVICE;
+      AG_HIP(hipEventRecord(c->side_join, c->side));
+      sha_side = true;
+    }
     // 5. check_merkle_tree over the raw output shreds (before any decryption: they are the
     //    codeword rows)
     if ((st = kind_merkle(c, k, n, S, codewords, cw_stride, roots2, proof))) return st;
@@ -3948,7 +3997,27 @@ int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_
       std::vector<uint32_t> cl(n);
       for (size_t s = 0; s < n; ++s) cl[s] = pre_ok[s] ? static_cast<uint32_t>(plen[s]) : 0;
       std::vector<int64_t> pl(n);
-      if ((st = ag_aon_decrypt_batch(c, k.aon, n, codewords, cw_stride, cl.data(), pl.data()))) return st;
+      if (sha_side) {
+        // decrypt_payload with the side stream's digests (ag_aon_decrypt_batch's key and
+        // length rules; the digests of the slices decrypted here hash the same lengths)
+        for (size_t s = 0; s < n; ++s) {
+          pl[s] = cl[s] < ag::kCipherKeyBytes ? -AG_RS_ERR_BAD_ENCODING
+                                              : static_cast<int64_t>(cl[s]) - ag::kCipherKeyBytes;
+          if (cl[s] < ag::kCipherKeyBytes) cl[s] = ag::kCipherKeyBytes;  // no-op
+        }
+        ag::BufferBatch bb;
+        if ((st = aon_batch(c, n, codewords, cw_stride, cl.data(), 0, &bb)) ||
+            (st = c->d_aon_keys.ensure(n * 16, c->stream)))
+          return st;
+        AG_HIP(hipStreamWaitEvent(c->stream, c->side_join, 0));
+        if (ag::launch_derive_keys(bb, 1, c->d_aon_digests.as<uint8_t>(), c->d_aon_keys.as<uint8_t>(), c->stream) !=
+                hipSuccess ||
+            ag::launch_apply_keystream(bb, c->d_aon_keys.as<uint8_t>(), ag::kCipherKeyBytes, c->stream) != hipSuccess)
+          return AG_RS_ERR_DEVICE;
+        AG_HIP(hipStreamSynchronize(c->stream));
+      } else if ((st = ag_aon_decrypt_batch(c, k.aon, n, codewords, cw_stride, cl.data(), pl.data()))) {
+        return st;
+      }
       for (size_t s = 0; s < n; ++s)
         if (pre_ok[s]) plen[s] = pl[s];
     }
