@@ -2691,7 +2691,7 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
                         const uint8_t* has_cached, uint32_t cached_group, const uint8_t* active, uint8_t* status,
                         uint8_t* roots_out, uint8_t* commitments_out, uint8_t* leaf_nodes = nullptr,
                         size_t leaf_nodes_stride = 0, uint32_t leaves_per_tree = 0, size_t group_stride = 0,
-                        uint32_t skip_row = 0);
+                        uint32_t skip_row = 0, bool roots_ready = false);
 }  // namespace
 
 int ag_ed25519_public_key_batch(ag_rs_ctx* c, size_t n, const uint8_t* seeds, uint8_t* pks) {
@@ -2775,7 +2775,10 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
                         const uint8_t* sigs, size_t sig_stride, const uint8_t* pk, const uint8_t* cached,
                         const uint8_t* has_cached, uint32_t cached_group, const uint8_t* active, uint8_t* status,
                         uint8_t* roots_out, uint8_t* commitments_out, uint8_t* leaf_nodes, size_t leaf_nodes_stride,
-                        uint32_t leaves_per_tree, size_t group_stride, uint32_t skip_row) {
+                        uint32_t leaves_per_tree, size_t group_stride, uint32_t skip_row, bool roots_ready) {
+  // roots_ready: step 1 already ran (launch_derive_roots, e.g. on another stream): roots_out holds
+  // every active shred's derived root
+  if (roots_ready && !roots_out) return AG_RS_ERR_INVALID_ARGUMENT;
   if (!c || n >= kMaxSigBatch || data_bytes >= (size_t{1} << 28) ||
       height > static_cast<size_t>(ag::kMerkleMaxHeight) ||
       (n && (!shred_index || !slots || !slice_indices || !is_last || !sigs || !pk || !status ||
@@ -2818,7 +2821,7 @@ int shred_validate_impl(ag_rs_ctx* c, size_t n, const uint8_t* data, size_t data
   mp.leaves_per_tree = leaves_per_tree;
   mp.group_stride = group_stride;
   mp.skip_row = skip_row;
-  if (ag::launch_merkle_verify(mp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  if (!roots_ready && ag::launch_merkle_verify(mp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   // 2. SliceCommitment + cached-commitment rule (validated_shred.rs:57-64)
   AG_HIP(hipMemsetAsync(count, 0, 4, c->stream));
   ag::ShredCommitParams cp{};
@@ -3431,20 +3434,49 @@ int ag_shredder_deshred_batch(ag_rs_ctx* c, size_t nslices, size_t S, uint8_t* p
   AG_HIP(hipMemsetAsync(gdata, 0, n * S, c->stream));  // slices without a pick: defined bytes
   AG_HIP(hipMemsetAsync(gidx, 0, 4 * n, c->stream));
   if (ag::launch_pipe_pick(pp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+  // every plausible shred's root (derive_root, with its leaf digest for the Merkle rebuild's level
+  // 0: step 5 hashes only the rows the coder restores or may rewrite) on the side stream: it needs
+  // only the parse and the pick's plausibility flags, so it overlaps the picked shreds'
+  // signature checks below (one signature per lane: a latency-bound kernel)
+  const size_t nodes_stride = (32 * ag_merkle_node_count(ag::kPipeShreds) + 255) / 256 * 256;
+  uint8_t* dlist;
+  if ((st = c->d_merkle_nodes.ensure(n * nodes_stride, c->stream)) || (st = c->ensure_side_stream()) ||
+      (st = pipe_buf(c, 26, 4 * (N + 1), &dlist)))
+    return st;
+  uint8_t* nodes = c->d_merkle_nodes.as<uint8_t>();
+  {
+    ag::MerkleVerifyParams mp{};
+    mp.leaves = codewords;
+    mp.leaf_stride = S;
+    mp.leaf_bytes = static_cast<uint32_t>(S);
+    mp.height = ag::kPipeHeight;
+    mp.index = cols.shred_index;
+    mp.proofs = proof;
+    mp.proofs_stride = kPipeProofBytes;
+    mp.n = N;
+    mp.roots_out = roots;
+    mp.active = plaus;
+    mp.list = reinterpret_cast<uint32_t*>(dlist);
+    mp.leaf_nodes = nodes;
+    mp.leaf_nodes_stride = nodes_stride;
+    mp.leaves_per_tree = ag::kPipeShreds;
+    AG_HIP(hipEventRecord(c->side_fork, c->stream));
+    AG_HIP(hipStreamWaitEvent(c->side, c->side_fork, 0));
+    if (ag::launch_merkle_verify(mp, c->side) != hipSuccess) return AG_RS_ERR_DEVICE;
+    AG_HIP(hipEventRecord(c->side_join, c->side));
+  }
   if ((st = shred_validate_impl(c, n, gdata, S, S, pp.g_shred_index, gproof, kPipeProofBytes, ag::kPipeHeight,
                                 pp.g_slot, pp.g_slice_index, glast, gsig, 64, pk, nullptr, nullptr, 1, nullptr, pstat,
-                                nullptr, commits)))
+                                nullptr, commits))) {
+    (void)hipStreamSynchronize(c->side);
     return st;
+  }
   if (ag::launch_pipe_cache_flags(pick, pstat, n, hasc, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
   // ... then every shred against its slice's commitment (signature only without a cache)
-  // (each checked shred's leaf digest goes to the Merkle rebuild's level 0: step 5 hashes only
-  // the rows the coder restores or may rewrite)
-  const size_t nodes_stride = (32 * ag_merkle_node_count(ag::kPipeShreds) + 255) / 256 * 256;
-  if ((st = c->d_merkle_nodes.ensure(n * nodes_stride, c->stream))) return st;
-  uint8_t* nodes = c->d_merkle_nodes.as<uint8_t>();
+  AG_HIP(hipStreamWaitEvent(c->stream, c->side_join, 0));
   if ((st = shred_validate_impl(c, N, codewords, S, S, cols.shred_index, proof, kPipeProofBytes, ag::kPipeHeight,
                                 cols.slot, cols.slice_index, last, sig, 64, pk, commits, hasc, ag::kPipeShreds, plaus,
-                                vstat, roots, nullptr, nodes, nodes_stride, ag::kPipeShreds)))
+                                vstat, roots, nullptr, nodes, nodes_stride, ag::kPipeShreds, 0, 0, true)))
     return st;
   // 3. per slice: the shreds kept, the root, header and signature
   uint8_t* per_slice;
@@ -3863,14 +3895,41 @@ int ag_shredder_deshred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_
     AG_HIP(hipMemsetAsync(gdata, 0, n * S, c->stream));
     AG_HIP(hipMemsetAsync(gidx, 0, 4 * n, c->stream));
     if (ag::launch_pipe_pick(pp, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    // every plausible shred's root on the side stream, overlapping the picked shreds' signature
+    // checks (as the Regular pipeline)
+    uint8_t* dlist;
+    if ((st = c->ensure_side_stream()) || (st = pipe_buf(c, 25, 4 * (N + 1), &dlist))) return st;
+    {
+      ag::MerkleVerifyParams mp{};
+      mp.leaves = cols.data;
+      mp.leaf_stride = S;
+      mp.leaf_bytes = static_cast<uint32_t>(S);
+      mp.height = ag::kPipeHeight;
+      mp.index = cols.shred_index;
+      mp.proofs = proof;
+      mp.proofs_stride = kPipeProofBytes;
+      mp.n = N;
+      mp.roots_out = roots;
+      mp.active = plaus;
+      mp.list = reinterpret_cast<uint32_t*>(dlist);
+      mp.group_stride = cw_stride;
+      mp.skip_row = k.skip;
+      AG_HIP(hipEventRecord(c->side_fork, c->stream));
+      AG_HIP(hipStreamWaitEvent(c->side, c->side_fork, 0));
+      if (ag::launch_merkle_verify(mp, c->side) != hipSuccess) return AG_RS_ERR_DEVICE;
+      AG_HIP(hipEventRecord(c->side_join, c->side));
+    }
     if ((st = shred_validate_impl(c, n, gdata, S, S, pp.g_shred_index, gproof, kPipeProofBytes, ag::kPipeHeight,
                                   pp.g_slot, pp.g_slice_index, glast, gsig, 64, pk, nullptr, nullptr, 1, nullptr, pstat,
-                                  nullptr, commits)))
+                                  nullptr, commits))) {
+      (void)hipStreamSynchronize(c->side);
       return st;
+    }
     if (ag::launch_pipe_cache_flags(pick, pstat, n, hasc, c->stream) != hipSuccess) return AG_RS_ERR_DEVICE;
+    AG_HIP(hipStreamWaitEvent(c->stream, c->side_join, 0));
     if ((st = shred_validate_impl(c, N, cols.data, S, S, cols.shred_index, proof, kPipeProofBytes, ag::kPipeHeight,
                                   cols.slot, cols.slice_index, last, sig, 64, pk, commits, hasc, ag::kPipeShreds, plaus,
-                                  vstat, roots, nullptr, nullptr, 0, 0, cw_stride, k.skip)))
+                                  vstat, roots, nullptr, nullptr, 0, 0, cw_stride, k.skip, true)))
       return st;
     // 3. per slice: the shreds kept, the root, header and signature
     uint8_t* per_slice;
