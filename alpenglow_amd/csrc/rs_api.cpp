@@ -3304,6 +3304,28 @@ int pipe_rerun_exact(ag_rs_ctx* c, size_t s, size_t S, const uint8_t* packets, s
 
 }  // namespace
 
+namespace {
+// ag_slice_sign_batch on the context's side stream, forked from the main stream's current point
+// (the roots): the signing (one signature per lane, latency-bound) overlaps the serialization of
+// everything else in the datagrams; the caller waits on side_join before launch_shred_sig_patch.
+int sign_on_side(ag_rs_ctx* c, size_t n, const uint8_t* seed, const uint8_t* pk, const uint64_t* slots,
+                 const uint64_t* slice_indices, const uint8_t* is_last, const uint8_t* roots, uint8_t* sigs) {
+  int st;
+  if ((st = c->ensure_side_stream())) return st;
+  AG_HIP(hipEventRecord(c->side_fork, c->stream));
+  AG_HIP(hipStreamWaitEvent(c->side, c->side_fork, 0));
+  std::swap(c->stream, c->side);
+  st = ag_slice_sign_batch(c, n, seed, pk, slots, slice_indices, is_last, roots, sigs, nullptr);
+  std::swap(c->stream, c->side);
+  if (st) {
+    (void)hipStreamSynchronize(c->side);
+    return st;
+  }
+  AG_HIP(hipEventRecord(c->side_join, c->side));
+  return AG_RS_OK;
+}
+}  // namespace
+
 extern "C" {
 
 int ag_shredder_shred_batch(ag_rs_ctx* c, size_t nslices, size_t S, const uint8_t* parent_flags,
@@ -3339,7 +3361,8 @@ int ag_shredder_shred_batch(ag_rs_ctx* c, size_t nslices, size_t S, const uint8_
                                   ag::kPipeShreds * kPipeProofBytes)))
     return st;
   // 4. slice_sig = sign(SliceCommitment(header, root))
-  if ((st = ag_slice_sign_batch(c, n, seed, pk, slots, slice_indices, is_last, roots, sigs, nullptr))) return st;
+  // 4b. signed on the side stream while 5 serializes the rest of the datagrams
+  if ((st = sign_on_side(c, n, seed, pk, slots, slice_indices, is_last, roots, sigs))) return st;
   // 5. the 64 datagrams per slice (header and signature shared by the slice's rows)
   ag::PipeExpandParams ep{};
   ep.nslices = n;
@@ -3364,7 +3387,13 @@ int ag_shredder_shred_batch(ag_rs_ctx* c, size_t nslices, size_t S, const uint8_
   cols.proof_stride = kPipeProofBytes;
   cols.height = ep.height;
   cols.hdr_group = ag::kPipeShreds;
-  if (ag::launch_shred_serialize(cols, N, packets, packet_stride, packet_lens, c->stream) != hipSuccess)
+  cols.skip_sig = 1;
+  if (ag::launch_shred_serialize(cols, N, packets, packet_stride, packet_lens, c->stream) != hipSuccess) {
+    (void)hipStreamSynchronize(c->side);
+    return AG_RS_ERR_DEVICE;
+  }
+  AG_HIP(hipStreamWaitEvent(c->stream, c->side_join, 0));
+  if (ag::launch_shred_sig_patch(cols, N, packets, packet_stride, packet_lens, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   return AG_RS_OK;
 }
@@ -3751,7 +3780,8 @@ int ag_shredder_shred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_t 
       (st = pipe_buf(c, 6, 4 * N, &height)))
     return st;
   if ((st = kind_merkle(c, k, n, S, codewords, cw_stride, roots, proofs))) return st;
-  if ((st = ag_slice_sign_batch(c, n, seed, pk, slots, slice_indices, is_last, roots, sigs, nullptr))) return st;
+  // 4b. signed on the side stream while 5 serializes the rest of the datagrams
+  if ((st = sign_on_side(c, n, seed, pk, slots, slice_indices, is_last, roots, sigs))) return st;
   ag::PipeExpandParams ep{};
   ep.nslices = n;
   ep.shred_bytes = static_cast<uint32_t>(S);
@@ -3774,7 +3804,13 @@ int ag_shredder_shred_batch_kind(ag_rs_ctx* c, int kind, size_t nslices, size_t 
   cols.proof_stride = kPipeProofBytes;
   cols.height = ep.height;
   cols.hdr_group = ag::kPipeShreds;
-  if (ag::launch_shred_serialize(cols, N, packets, packet_stride, packet_lens, c->stream) != hipSuccess)
+  cols.skip_sig = 1;
+  if (ag::launch_shred_serialize(cols, N, packets, packet_stride, packet_lens, c->stream) != hipSuccess) {
+    (void)hipStreamSynchronize(c->side);
+    return AG_RS_ERR_DEVICE;
+  }
+  AG_HIP(hipStreamWaitEvent(c->stream, c->side_join, 0));
+  if (ag::launch_shred_sig_patch(cols, N, packets, packet_stride, packet_lens, c->stream) != hipSuccess)
     return AG_RS_ERR_DEVICE;
   return AG_RS_OK;
 }

@@ -171,8 +171,20 @@ __global__ __launch_bounds__(256) void shred_serialize_kernel(const ShredColumns
   const uint8_t* dd = c.data + data_row_offset(c, t);
   // unaligned 16-byte stores (the datagram rows sit at any byte offset)
   copy16_any(pk + kShredHeadBytes, dd, dlen, lane);
-  copy16_any(pk + o_sig, c.sig + 64 * h, 64, lane);
+  if (!c.skip_sig) copy16_any(pk + o_sig, c.sig + 64 * h, 64, lane);
   copy16_any(pk + o_sig + 72, c.proof + t * c.proof_stride, 32 * plen, lane);
+}
+
+__global__ __launch_bounds__(256) void shred_sig_patch_kernel(const ShredColumns c, uint64_t n,
+                                                              uint8_t* __restrict__ packets, uint64_t packet_stride,
+                                                              const uint32_t* __restrict__ packet_lens) {
+  const uint64_t t = static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (t >= n || packet_lens[t] == 0) return;
+  const uint64_t h = c.hdr_group > 1 ? t / c.hdr_group : t;
+  uint8_t* dst = packets + t * packet_stride + kShredHeadBytes + c.data_len[t];
+  const uint8_t* src = c.sig + 64 * h;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) st16u(dst + 16 * q, ld16u(src + 16 * q));
 }
 
 }  // namespace
@@ -191,6 +203,15 @@ hipError_t launch_shred_serialize(const ShredColumns& c, uint64_t n, uint8_t* pa
   if (n == 0) return hipSuccess;
   if ((n + 3) / 4 > 0x7FFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(shred_serialize_kernel, dim3(static_cast<unsigned>((n + 3) / 4)), dim3(256), 0, stream, c, n,
+                     packets, packet_stride, packet_lens);
+  return hipGetLastError();
+}
+
+hipError_t launch_shred_sig_patch(const ShredColumns& c, uint64_t n, uint8_t* packets, uint64_t packet_stride,
+                                  const uint32_t* packet_lens, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if ((n + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(shred_sig_patch_kernel, dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0, stream, c, n,
                      packets, packet_stride, packet_lens);
   return hipGetLastError();
 }

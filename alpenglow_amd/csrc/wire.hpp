@@ -32,6 +32,7 @@ struct ShredColumns {
                          // t / hdr_group (one header per slice); 0 or 1: per shred
   uint64_t group_stride;  // data row t at data + grouped_row_offset(t, data_stride, group_stride,
   uint32_t skip_row;      // skip_row) (group_stride 0: t * data_stride)
+  uint32_t skip_sig;      // serialize only: leave the 64 signature bytes for launch_shred_sig_patch
 };
 __host__ __device__ inline uint64_t data_row_offset(const ShredColumns& c, uint64_t t) {
   return grouped_row_offset(t, c.data_stride, c.group_stride, c.skip_row);
@@ -46,5 +47,10 @@ hipError_t launch_shred_deserialize(const uint8_t* packets, uint64_t packet_stri
 // untouched, when the shred does not fit packet_stride or its columns' rows).
 hipError_t launch_shred_serialize(const ShredColumns& c, uint64_t n, uint8_t* packets, uint64_t packet_stride,
                                   uint32_t* packet_lens, hipStream_t stream);
+// The signatures of datagrams serialized with skip_sig: packet t (packet_lens[t] != 0) gets the
+// 64 bytes of c.sig row t / hdr_group (or t) at its signature offset (37 + data_len[t]); one
+// thread per datagram.  Lets the signing overlap the bulk of the serialization.
+hipError_t launch_shred_sig_patch(const ShredColumns& c, uint64_t n, uint8_t* packets, uint64_t packet_stride,
+                                  const uint32_t* packet_lens, hipStream_t stream);
 
 }  // namespace ag
