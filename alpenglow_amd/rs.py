@@ -837,6 +837,8 @@ def _parent_arrays(parents, nslices: int):
         raise ValueError("parents do not match the batch")
     flags = np.zeros(nslices, np.uint8)
     ids = np.zeros((nslices, BLOCK_ID_BYTES), np.uint8)
+    if parents.count(None) == nslices:  # (list.count runs in C: a batch of slices without parents)
+        return flags, ids
     for b, par in enumerate(parents):
         if par is not None:
             slot, h = par
@@ -844,6 +846,17 @@ def _parent_arrays(parents, nslices: int):
             ids[b, :8] = np.frombuffer(int(slot).to_bytes(8, "little"), np.uint8)
             ids[b, 8:] = np.frombuffer(bytes(h), np.uint8)
     return flags, ids
+
+
+def _parent_list(flags, ids) -> list:
+    """The parents (None or (slot, hash bytes)) of the slices whose flag is set: only those
+    slices are visited (the others stay None)."""
+    import numpy as np
+
+    out = [None] * len(flags)
+    for b in np.flatnonzero(flags):
+        out[b] = (int.from_bytes(ids[b, :8].tobytes(), "little"), ids[b, 8:].tobytes())
+    return out
 
 
 def slice_frame_batch(ctx: Context, nslices: int, shred_bytes: int, parents, data, data_stride: int, data_lens,
@@ -880,8 +893,7 @@ def slice_parse_batch(ctx: Context, nslices: int, codewords, codeword_stride: in
     _check(load().ag_slice_parse_batch(ctx.handle, nslices, _ptr(codewords), codeword_stride, lens.ctypes.data,
                                        st.ctypes.data, flags.ctypes.data, ids.ctypes.data, offs.ctypes.data,
                                        dl.ctypes.data), "ag_slice_parse_batch")
-    parents = [(int.from_bytes(ids[b, :8].tobytes(), "little"), ids[b, 8:].tobytes()) if flags[b] else None
-               for b in range(nslices)]
+    parents = _parent_list(flags, ids)
     return st, parents, offs, dl
 
 
@@ -943,8 +955,7 @@ def shredder_deshred_batch(ctx: Context, nslices: int, shred_bytes: int, packets
                                             slots.ctypes.data, sidx.ctypes.data, last.ctypes.data, flags.ctypes.data,
                                             ids.ctypes.data, offs.ctypes.data, dl.ctypes.data),
            "ag_shredder_deshred_batch")
-    parents = [(int.from_bytes(ids[b, :8].tobytes(), "little"), ids[b, 8:].tobytes()) if flags[b] else None
-               for b in range(nslices)]
+    parents = _parent_list(flags, ids)
     return DeshredBatch(st, slots, sidx, last, parents, offs, dl)
 
 
@@ -997,6 +1008,5 @@ def shredder_deshred_batch_kind(ctx: Context, kind: int, nslices: int, shred_byt
                                                  last.ctypes.data, flags.ctypes.data, ids.ctypes.data,
                                                  offs.ctypes.data, dl.ctypes.data),
            "ag_shredder_deshred_batch_kind")
-    parents = [(int.from_bytes(ids[b, :8].tobytes(), "little"), ids[b, 8:].tobytes()) if flags[b] else None
-               for b in range(nslices)]
+    parents = _parent_list(flags, ids)
     return DeshredBatch(st, slots, sidx, last, parents, offs, dl)
