@@ -833,11 +833,13 @@ BLOCK_ID_BYTES = 40
 def _parent_arrays(parents, nslices: int):
     import numpy as np
 
+    if not isinstance(parents, (list, tuple)):
+        parents = list(parents)
     if len(parents) != nslices:
         raise ValueError("parents do not match the batch")
     flags = np.zeros(nslices, np.uint8)
     ids = np.zeros((nslices, BLOCK_ID_BYTES), np.uint8)
-    if parents.count(None) == nslices:  # (list.count runs in C: a batch of slices without parents)
+    if parents.count(None) == nslices:  # (count runs in C: a batch of slices without parents)
         return flags, ids
     for b, par in enumerate(parents):
         if par is not None:

@@ -178,3 +178,21 @@ def test_gpu_deshred_parse_matches_oracle(ctx, mode):
         assert st == wst, b
         if wst == so.OK:
             assert par == wpar and data == wdata, b
+
+
+def test_parent_arrays_round_trip():
+    """The binding's parent conversion (rs._parent_arrays / rs._parent_list): None entries stay
+    None, set entries keep slot and hash, and any sequence type is accepted (host logic only)."""
+    from alpenglow_amd import rs
+
+    h1, h2 = bytes(range(32)), bytes(range(100, 132))
+    parents = [None, (7, h1), None, None, ((1 << 64) - 1, h2)]
+    for seq in (parents, tuple(parents), iter(parents)):
+        flags, ids = rs._parent_arrays(seq, len(parents))
+        assert flags.tolist() == [0, 1, 0, 0, 1]
+        assert rs._parent_list(flags, ids) == parents
+    flags, ids = rs._parent_arrays([None] * 4, 4)
+    assert not flags.any() and not ids.any()
+    assert rs._parent_list(flags, ids) == [None] * 4
+    with pytest.raises(ValueError):
+        rs._parent_arrays([None] * 3, 4)
